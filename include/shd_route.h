@@ -1,0 +1,136 @@
+/*
+ * shd_route.h -- C-ABI of the MI355X-native topology routing engine.
+ *
+ * This is the boundary that replaces the igraph-backed path computation inside
+ * Shadow 1.14's src/main/routing/topology.c (mckerrigan/shadow).  Shadow keeps
+ * its public routing API unchanged (topology.h:17-28); its topology.c front end
+ * calls this module instead of igraph for every number that ends up in a Path
+ * (path.c:13-21: latency, reliability).  Plain C types only; no HIP/torch types
+ * in any signature.  One context per GPU; contexts are not re-entrant.
+ *
+ * Reference interface each entry point replaces (file:line in the reference):
+ *   shd_route_create   <- _topology_loadGraph/_topology_checkGraph/_topology_extractEdgeWeights
+ *                         (topology.c:371-399, 1187-1246): graph in, validated, resident
+ *   shd_route_rows     <- _topology_computeSourcePaths (topology.c:1655-1875) =
+ *                         igraph_get_shortest_paths_dijkstra (topology.c:1756) +
+ *                         _topology_computePathProperties (topology.c:1407-1523),
+ *                         batched over many sources; with SHD_ROUTE_DISPATCH also the
+ *                         direct-path dispatch of _topology_getPathEntry (topology.c:2019-2031)
+ *                         and _topology_lookupDirectPath (topology.c:1877-1927)
+ *   shd_route_direct   <- _topology_lookupDirectPath (topology.c:1877-1927) for many pairs
+ *   shd_route_self     <- _topology_computeShortestPathToSelf (topology.c:1545-1653)
+ *   shd_route_min_reduce <- minimumPathLatency tracking (topology.c:1374-1385)
+ *   shd_route_fw       <- (no reference equivalent; dense all-pairs alternative)
+ *
+ * Semantics of one (s,t) entry are exactly the Path the reference would cache:
+ *   t != s : lat = 0.0 + sum of edge latencies along the chosen shortest path, summed
+ *            from s (bit-exact: any relaxation order reaches the same left-fold minimum);
+ *            rel = ((1.0*f_s)*f_t) * prod(1 - loss_e) with absent vertex factors skipped.
+ *            The engine multiplies f_t last, so rel is bit-exact whenever f_t is absent
+ *            or 1.0 and within a few ulp otherwise.
+ *   t == s : the batch self-loop entry (path [s]): lat = w_ss, rel = (1.0*f_s)*r_ss;
+ *            SHD_ROUTE_ENOEDGE if s has no self-loop (topology.c:1488-1495).
+ * Ties between equal-latency paths are broken deterministically: the parent of v is
+ * the tight in-arc (u->v) with the smallest (dist[u], u, edge id).  Latency never
+ * depends on ties; reliability matches igraph wherever the shortest path is unique.
+ */
+#ifndef SHD_ROUTE_H
+#define SHD_ROUTE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes: 0 = success, negative = failure (topology.c maps them to critical()) */
+#define SHD_ROUTE_OK 0
+#define SHD_ROUTE_EINVAL (-1)       /* bad argument / graph fails topology.c validation */
+#define SHD_ROUTE_ENOMEM (-2)       /* host or device allocation failed */
+#define SHD_ROUTE_EDEVICE (-3)      /* HIP runtime error */
+#define SHD_ROUTE_ENOEDGE (-4)      /* a hop has no edge (missing self-loop; topology.c:1488) */
+#define SHD_ROUTE_EUNREACH (-5)     /* a target is unreachable (graph not strongly connected) */
+#define SHD_ROUTE_EUNSUPPORTED (-6) /* request outside what this build supports */
+
+/* flags for shd_route_rows */
+#define SHD_ROUTE_DISPATCH 0x1u /* apply topology.c:2019 dispatch: complete graph -> direct,
+                                   prefer-direct && adjacent -> direct, else source paths */
+
+typedef struct shd_route shd_route_t;
+
+/* A topology as igraph holds it after igraph_read_graph_graphml: vertices and edges
+ * numbered in graphml document order.  Arrays are read during shd_route_create only. */
+typedef struct shd_graph {
+    int32_t n_vertices;
+    int32_t n_edges;
+    const int32_t* edge_src;          /* [n_edges] */
+    const int32_t* edge_dst;          /* [n_edges] */
+    const double* edge_latency;       /* [n_edges] ms, > 0        (topology.c:1070) */
+    const double* edge_packetloss;    /* [n_edges] in [0,1]       (topology.c:1090) */
+    const double* vertex_packetloss;  /* [n_vertices] or NULL; NaN = absent (topology.c:330-347) */
+    int32_t directed;                 /* graphml edgedefault="directed" */
+    int32_t prefer_direct;            /* graph attribute preferdirectpaths (topology.c:761-790) */
+} shd_graph_t;
+
+typedef struct shd_route_info {
+    int32_t n_vertices;
+    int32_t n_edges;
+    int32_t n_arcs;          /* CSR arcs used by SSSP (self-loops excluded) */
+    int32_t is_complete;     /* topology.c:450-552 */
+    int32_t directed;
+    int32_t prefer_direct;
+    int32_t integer_weights; /* every latency integral and path sums exact in u32 */
+    int32_t multigraph;      /* parallel edges present (SURVEY hazard H3) */
+    int32_t device;
+    int32_t lds_resident;    /* per-source state fits the 160 KiB LDS */
+    uint64_t device_bytes;   /* resident graph bytes */
+    double min_edge_latency;
+} shd_route_info_t;
+
+int shd_route_create(shd_route_t** out, const shd_graph_t* graph, int device);
+void shd_route_destroy(shd_route_t* ctx);
+int shd_route_get_info(const shd_route_t* ctx, shd_route_info_t* info);
+const char* shd_route_strerror(int code);
+
+/* Eager batch of SOURCE(s,.) rows: for i < ns, j < nt,
+ *   lat_out[i*nt + j], rel_out[i*nt + j] = Path(src[i] -> tgt[j]);
+ *   row_min_out[i] = min_j lat_out[i*nt + j]   (any of the three outputs may be NULL).
+ * Host pointers; the call blocks. */
+int shd_route_rows(shd_route_t* ctx, const int32_t* src, int32_t ns, const int32_t* tgt,
+                   int32_t nt, uint32_t flags, double* lat_out, double* rel_out,
+                   double* row_min_out);
+
+/* Same, all pointers device pointers (inputs already resident in HBM, outputs written
+ * in HBM with row stride ld >= nt); enqueued on `stream` (a hipStream_t, NULL =
+ * default stream); returns after enqueueing.  Errors detected on the device are
+ * reported by the next shd_route_sync(). */
+int shd_route_rows_async(shd_route_t* ctx, const int32_t* d_src, int32_t ns,
+                         const int32_t* d_tgt, int32_t nt, int64_t ld, uint32_t flags,
+                         double* d_lat, double* d_rel, double* d_row_min, void* stream);
+
+/* Wait for `stream` and return the first device-side error raised since the last sync. */
+int shd_route_sync(shd_route_t* ctx, void* stream);
+
+/* Direct-path pairs (topology.c:1877-1927) for the full src x tgt block. */
+int shd_route_direct(shd_route_t* ctx, const int32_t* src, int32_t ns, const int32_t* tgt,
+                     int32_t nt, double* lat_out, double* rel_out, double* row_min_out);
+
+/* Self paths (topology.c:1545-1653) for a list of vertices. */
+int shd_route_self(shd_route_t* ctx, const int32_t* v, int32_t nv, double* lat_out,
+                   double* rel_out);
+
+/* Device-wide min over `count` non-negative doubles (runahead, topology.c:1374-1385).
+ * Device pointers; result written to *d_out. */
+int shd_route_min_reduce_async(shd_route_t* ctx, const double* d_vals, int64_t count,
+                               double* d_out, void* stream);
+
+/* Dense all-pairs shortest latencies by blocked min-plus Floyd-Warshall over all
+ * vertices: d_dist is n x n (device, row-major).  Bit-exact against Dijkstra only
+ * for integer-valued latencies (fl sums of subpaths are not left folds otherwise). */
+int shd_route_fw_async(shd_route_t* ctx, double* d_dist, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHD_ROUTE_H */

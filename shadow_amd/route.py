@@ -1,0 +1,192 @@
+"""ctypes binding of the HIP engine (shadow_amd/libshd_route.so, include/shd_route.h).
+
+This is the same binding a maintainer would add on the reference side (see
+INTEGRATION.md); Python is only the test/bench driver.  There is no CPU fallback:
+if the HIP library is missing, importing the engine raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from .graph import Graph
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libshd_route.so")
+
+OK = 0
+EINVAL = -1
+ENOMEM = -2
+EDEVICE = -3
+ENOEDGE = -4
+EUNREACH = -5
+EUNSUPPORTED = -6
+DISPATCH = 0x1
+
+
+class RouteError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        super().__init__(f"{what}: {strerror(code)} ({code})")
+
+
+class _Graph(C.Structure):
+    _fields_ = [
+        ("n_vertices", C.c_int32), ("n_edges", C.c_int32),
+        ("edge_src", C.c_void_p), ("edge_dst", C.c_void_p),
+        ("edge_latency", C.c_void_p), ("edge_packetloss", C.c_void_p),
+        ("vertex_packetloss", C.c_void_p),
+        ("directed", C.c_int32), ("prefer_direct", C.c_int32),
+    ]
+
+
+class _Info(C.Structure):
+    _fields_ = [
+        ("n_vertices", C.c_int32), ("n_edges", C.c_int32), ("n_arcs", C.c_int32),
+        ("is_complete", C.c_int32), ("directed", C.c_int32), ("prefer_direct", C.c_int32),
+        ("integer_weights", C.c_int32), ("multigraph", C.c_int32), ("device", C.c_int32),
+        ("lds_resident", C.c_int32), ("device_bytes", C.c_uint64), ("min_edge_latency", C.c_double),
+    ]
+
+
+# every symbol include/shd_route.h declares
+EXPORTS = (
+    "shd_route_create", "shd_route_destroy", "shd_route_get_info", "shd_route_strerror",
+    "shd_route_rows", "shd_route_rows_async", "shd_route_sync", "shd_route_direct",
+    "shd_route_self", "shd_route_min_reduce_async", "shd_route_fw_async",
+)
+
+_lib = None
+
+
+def load_library():
+    """Load libshd_route.so (fails loudly if the HIP build is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"HIP engine not built: {LIB_PATH} missing (run __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    P, I32, I64, U32 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32
+    L.shd_route_strerror.restype = C.c_char_p
+    L.shd_route_strerror.argtypes = [C.c_int]
+    L.shd_route_create.restype = C.c_int
+    L.shd_route_create.argtypes = [C.POINTER(P), C.POINTER(_Graph), C.c_int]
+    L.shd_route_destroy.argtypes = [P]
+    L.shd_route_get_info.restype = C.c_int
+    L.shd_route_get_info.argtypes = [P, C.POINTER(_Info)]
+    L.shd_route_rows.restype = C.c_int
+    L.shd_route_rows.argtypes = [P, P, I32, P, I32, U32, P, P, P]
+    L.shd_route_rows_async.restype = C.c_int
+    L.shd_route_rows_async.argtypes = [P, P, I32, P, I32, I64, U32, P, P, P, P]
+    L.shd_route_sync.restype = C.c_int
+    L.shd_route_sync.argtypes = [P, P]
+    L.shd_route_direct.restype = C.c_int
+    L.shd_route_direct.argtypes = [P, P, I32, P, I32, P, P, P]
+    L.shd_route_self.restype = C.c_int
+    L.shd_route_self.argtypes = [P, P, I32, P, P]
+    L.shd_route_min_reduce_async.restype = C.c_int
+    L.shd_route_min_reduce_async.argtypes = [P, P, I64, P, P]
+    L.shd_route_fw_async.restype = C.c_int
+    L.shd_route_fw_async.argtypes = [P, P, P]
+    _lib = L
+    return L
+
+
+def strerror(code: int) -> str:
+    try:
+        return load_library().shd_route_strerror(int(code)).decode()
+    except RuntimeError:
+        return f"error {code}"
+
+
+def _p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def _check(rc, what):
+    if rc != OK:
+        raise RouteError(rc, what)
+
+
+class RouteEngine:
+    """One routing context on one GPU (one process per GPU)."""
+
+    def __init__(self, g: Graph, device: int = 0):
+        L = load_library()
+        self.graph = g
+        self._arrays = (
+            np.ascontiguousarray(g.src, np.int32), np.ascontiguousarray(g.dst, np.int32),
+            np.ascontiguousarray(g.latency, np.float64), np.ascontiguousarray(g.packetloss, np.float64),
+            None if g.vertex_packetloss is None else np.ascontiguousarray(g.vertex_packetloss, np.float64),
+        )
+        s, d, lat, loss, vl = self._arrays
+        desc = _Graph(int(g.n), len(s), s.ctypes.data, d.ctypes.data, lat.ctypes.data, loss.ctypes.data,
+                      None if vl is None else vl.ctypes.data, int(bool(g.directed)), int(bool(g.prefer_direct)))
+        h = C.c_void_p()
+        _check(L.shd_route_create(C.byref(h), C.byref(desc), int(device)), "shd_route_create")
+        self._h = h
+        self.device = device
+        inf = _Info()
+        _check(L.shd_route_get_info(self._h, C.byref(inf)), "shd_route_get_info")
+        self.info = {k: getattr(inf, k) for k, _ in _Info._fields_}
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            load_library().shd_route_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- host-pointer API -----------------------------------------------------
+    def rows(self, sources, targets, dispatch: bool = True):
+        s = np.ascontiguousarray(sources, np.int32)
+        t = np.ascontiguousarray(targets, np.int32)
+        lat = np.empty((len(s), len(t))); rel = np.empty((len(s), len(t))); mn = np.empty(len(s))
+        rc = load_library().shd_route_rows(self._h, _p(s), len(s), _p(t), len(t),
+                                           DISPATCH if dispatch else 0, _p(lat), _p(rel), _p(mn))
+        _check(rc, "shd_route_rows")
+        return lat, rel, mn
+
+    def direct(self, sources, targets):
+        s = np.ascontiguousarray(sources, np.int32)
+        t = np.ascontiguousarray(targets, np.int32)
+        lat = np.empty((len(s), len(t))); rel = np.empty((len(s), len(t))); mn = np.empty(len(s))
+        _check(load_library().shd_route_direct(self._h, _p(s), len(s), _p(t), len(t), _p(lat), _p(rel), _p(mn)),
+               "shd_route_direct")
+        return lat, rel, mn
+
+    def self_paths(self, vertices):
+        v = np.ascontiguousarray(vertices, np.int32)
+        lat = np.empty(len(v)); rel = np.empty(len(v))
+        _check(load_library().shd_route_self(self._h, _p(v), len(v), _p(lat), _p(rel)), "shd_route_self")
+        return lat, rel
+
+    # -- device-pointer API (torch tensors as HBM plumbing) --------------------
+    def rows_async(self, d_src, d_tgt, d_lat, d_rel, d_rowmin, stream=None, dispatch=True, ld=None):
+        ns, nt = int(d_src.numel()), int(d_tgt.numel())
+        ld = nt if ld is None else int(ld)
+        ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        rc = load_library().shd_route_rows_async(
+            self._h, ptr(d_src), ns, ptr(d_tgt), nt, ld, DISPATCH if dispatch else 0,
+            ptr(d_lat), ptr(d_rel), ptr(d_rowmin), C.c_void_p(stream) if stream else None)
+        _check(rc, "shd_route_rows_async")
+
+    def sync(self, stream=None):
+        _check(load_library().shd_route_sync(self._h, C.c_void_p(stream) if stream else None), "shd_route_sync")
+
+    def min_reduce_async(self, d_vals, d_out, stream=None):
+        rc = load_library().shd_route_min_reduce_async(self._h, C.c_void_p(d_vals.data_ptr()), int(d_vals.numel()),
+                                                       C.c_void_p(d_out.data_ptr()),
+                                                       C.c_void_p(stream) if stream else None)
+        _check(rc, "shd_route_min_reduce_async")
+
+    def fw_async(self, d_dist, stream=None):
+        _check(load_library().shd_route_fw_async(self._h, C.c_void_p(d_dist.data_ptr()),
+                                                 C.c_void_p(stream) if stream else None), "shd_route_fw_async")

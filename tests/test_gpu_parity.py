@@ -1,0 +1,99 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle.
+
+Latency must be bit-exact everywhere.  Reliability is bit-exact against the oracle's
+engine tie rule (ORC_TIE_MINKEY) when vertex factors are 1.0/absent, and matches
+igraph's tie rule wherever the shortest path is unique.  With non-unit vertex loss
+the engine multiplies f_t last: tolerance REL_TOL relative (north_star: 1e-12).
+"""
+import numpy as np
+import pytest
+
+from shadow_amd.graph import Graph, complete_graph, config, example_one_vertex, internet_like
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def route():
+    from shadow_amd import route as r
+    r.load_library()
+    return r
+
+
+def _check_rows(eng, og, oracle_mod, src, tgt, rel_exact=True):
+    lat, rel, mn = eng.rows(src, tgt, dispatch=False)
+    olat, orel, ouq, _ = og.source_rows(src, tgt, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    if rel_exact:
+        assert np.array_equal(rel, orel)
+    else:
+        np.testing.assert_allclose(rel, orel, rtol=REL_TOL, atol=0)
+    assert np.array_equal(mn, olat.min(axis=1))
+    ilat, irel, iuq, _ = og.source_rows(src, tgt, oracle_mod.TIE_IGRAPH)
+    assert np.array_equal(lat, ilat)
+    np.testing.assert_allclose(rel[iuq], irel[iuq], rtol=REL_TOL, atol=0)
+    return lat, rel
+
+
+def test_c2_rows_bitexact(route, oracle_mod):
+    g = config("c2")
+    eng = route.RouteEngine(g)
+    assert eng.info["lds_resident"] == 1
+    og = oracle_mod.OracleGraph(g)
+    src = np.arange(0, g.n, 13, dtype=np.int32)
+    _check_rows(eng, og, oracle_mod, src, g.targets())
+
+
+def test_c2_vertex_loss_within_tol(route, oracle_mod):
+    g = config("c2", vloss=True)
+    eng = route.RouteEngine(g)
+    og = oracle_mod.OracleGraph(g)
+    src = np.arange(3, g.n, 97, dtype=np.int32)
+    _check_rows(eng, og, oracle_mod, src, g.targets(), rel_exact=False)
+
+
+def test_hbm_resident_path(route, oracle_mod):
+    g = internet_like(8000, 3, seed=5, name="hbm")
+    eng = route.RouteEngine(g)
+    assert eng.info["lds_resident"] == 0
+    og = oracle_mod.OracleGraph(g)
+    src = np.array([0, 1, 7, 4000, 7999], np.int32)
+    _check_rows(eng, og, oracle_mod, src, g.targets())
+
+
+def test_example_kat(route):
+    # resource/examples/shadow.config.xml:2-24: lat 50.0, rel 0.99, runahead 50 ms
+    eng = route.RouteEngine(example_one_vertex(0.0, 0.01, 50.0))
+    assert eng.info["is_complete"] == 1
+    lat, rel, mn = eng.rows([0], [0])
+    assert lat[0, 0] == 50.0 and rel[0, 0] == 1.0 - 0.01 and mn[0] == 50.0
+    # src/test/tcp/tcp-blocking-lossy: no vertex packetloss key, edge loss 0.25
+    eng = route.RouteEngine(example_one_vertex(None, 0.25, 50.0))
+    lat, rel, _ = eng.rows([0], [0])
+    assert lat[0, 0] == 50.0 and rel[0, 0] == 0.75
+
+
+def test_complete_direct_dispatch(route, oracle_mod):
+    g = complete_graph(64, seed=3)
+    eng = route.RouteEngine(g)
+    assert eng.info["is_complete"] == 1
+    og = oracle_mod.OracleGraph(g)
+    t = np.arange(g.n, dtype=np.int32)
+    lat, rel, _ = eng.rows(t, t, dispatch=True)
+    for s in range(0, g.n, 9):
+        for j in range(g.n):
+            L, R = og.direct(s, j)
+            assert lat[s, j] == L and rel[s, j] == R
+
+
+def test_self_paths(route, oracle_mod):
+    g = internet_like(200, 2, seed=9)
+    eng = route.RouteEngine(g)
+    og = oracle_mod.OracleGraph(g)
+    v = np.arange(g.n, dtype=np.int32)
+    lat, rel = eng.self_paths(v)
+    for k in range(g.n):
+        L, R = og.self_path(k)
+        assert lat[k] == L and rel[k] == R

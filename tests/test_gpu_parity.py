@@ -97,3 +97,87 @@ def test_self_paths(route, oracle_mod):
     for k in range(g.n):
         L, R = og.self_path(k)
         assert lat[k] == L and rel[k] == R
+
+
+# ---------------------------------------------------------------------------
+# full-size parity through the committed golden fixtures (tests/golden/)
+import hashlib  # noqa: E402
+import json  # noqa: E402
+import os  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, np.float64).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def digests():
+    return json.load(open(os.path.join(GOLD, "rows_digests.json")))
+
+
+def test_c2_full_table_matches_golden(route, digests):
+    g = config("c2")
+    eng = route.RouteEngine(g)
+    T = g.targets()
+    lat, rel, mn = eng.rows(T, T)
+    rows = {r["src"]: r for r in digests["c2"]["rows"]}
+    assert len(rows) == len(T)
+    for i, s in enumerate(T):
+        r = rows[int(s)]
+        assert _sha(lat[i]) == r["lat_sha"] and _sha(rel[i]) == r["rel_sha"], s
+        assert mn[i] == r["row_min"]
+    # undirected, integer weights: the table is symmetric in latency
+    assert np.array_equal(lat, lat.T)
+
+
+@pytest.mark.parametrize("cfg", ["c3", "c4"])
+def test_sampled_rows_match_golden(route, digests, cfg):
+    g = config(cfg)
+    eng = route.RouteEngine(g)
+    T = g.targets()
+    S = np.array([r["src"] for r in digests[cfg]["rows"]], np.int32)
+    lat, rel, mn = eng.rows(S, T)
+    for i, r in enumerate(digests[cfg]["rows"]):
+        assert _sha(lat[i]) == r["lat_sha"] and _sha(rel[i]) == r["rel_sha"], (cfg, r["src"])
+        assert mn[i] == r["row_min"]
+
+
+def test_bundled_topology_engine(route):
+    z = np.load(os.path.join(GOLD, "bundled_topology.npz"))
+    exp = json.load(open(os.path.join(GOLD, "bundled_expected.json")))
+    g = Graph(n=int(z["n"]), src=z["src"], dst=z["dst"], latency=z["latency"], packetloss=z["packetloss"],
+              vertex_packetloss=z["vertex_packetloss"], directed=bool(z["directed"]))
+    eng = route.RouteEngine(g)
+    assert eng.info["is_complete"] == 1
+    A = np.arange(g.n, dtype=np.int32)
+    lat, rel, mn = eng.rows(A, A, dispatch=True)
+    assert _sha(lat) == exp["lat_sha"] and _sha(rel) == exp["rel_sha"]
+    assert mn.min() == exp["min_latency"] == 5.0
+
+
+def test_small_golden_tables_engine(route):
+    z = np.load(os.path.join(GOLD, "small_tables.npz"))
+    for name in z["names"]:
+        p = f"{name}__"
+        vl = z[p + "vertex_packetloss"]
+        g = Graph(n=int(z[p + "n"]), src=z[p + "src"], dst=z[p + "dst"], latency=z[p + "latency"],
+                  packetloss=z[p + "packetloss"], vertex_packetloss=vl if len(vl) else None,
+                  directed=bool(z[p + "directed"]), prefer_direct=bool(z[p + "prefer_direct"]))
+        eng = route.RouteEngine(g)
+        A = z[p + "attached"].astype(np.int32)
+        lat, rel, _ = eng.rows(A, A, dispatch=True)
+        # eager cache: lookup(i, j) = the Path stored from row min(i, j) (first writer wins)
+        iu = np.triu_indices(len(A))
+        E_lat = np.zeros_like(lat); E_rel = np.zeros_like(rel)
+        E_lat[iu] = lat[iu]; E_rel[iu] = rel[iu]
+        E_lat.T[iu] = lat[iu]; E_rel.T[iu] = rel[iu]
+        assert np.array_equal(E_lat, z[p + "lat"]), name
+        uq = z[p + "unique"]
+        np.testing.assert_allclose(E_rel[uq], z[p + "rel"][uq], rtol=REL_TOL, atol=0, err_msg=name)
+        if not len(vl) or np.all(vl == 0):
+            assert np.array_equal(E_rel[uq], z[p + "rel"][uq]), name
+        # raw rows against the golden raw rows too
+        assert np.array_equal(lat if not (g.prefer_direct or eng.info["is_complete"]) else z[p + "raw_lat"],
+                              z[p + "raw_lat"]) or g.prefer_direct or eng.info["is_complete"], name

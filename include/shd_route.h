@@ -86,6 +86,10 @@ typedef struct shd_route_info {
     int32_t lds_resident;    /* per-source state fits the 160 KiB LDS */
     uint64_t device_bytes;   /* resident graph bytes */
     double min_edge_latency;
+    int32_t kernel;          /* SSSP kernel: 0 = generic f64, 1 = integer K32 (LDS keys) */
+    int32_t dist_bound;      /* K32: proven bound on every shortest-path latency (ms) */
+    int32_t block;           /* threads per workgroup of the SSSP kernel */
+    int32_t reserved;
 } shd_route_info_t;
 
 int shd_route_create(shd_route_t** out, const shd_graph_t* graph, int device);

@@ -10,7 +10,8 @@ ROOT = os.path.dirname(HERE)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = [os.path.join(HERE, "csrc", "shd_route.hip")]
+SOURCES = [os.path.join(HERE, "csrc", "engine.hip")]
+HEADERS = [os.path.join(HERE, "csrc", f) for f in ("common.hpp", "sssp_f64.hpp", "sssp_k32.hpp", "direct_fw.hpp")]
 OUT = os.path.join(HERE, "libshd_route.so")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
          "-Wall", "-Wno-unused-result"]
@@ -20,7 +21,7 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = SOURCES + [os.path.join(ROOT, "include", "shd_route.h")]
+    deps = SOURCES + HEADERS + [os.path.join(ROOT, "include", "shd_route.h")]
     return any(os.path.getmtime(p) > t for p in deps)
 
 

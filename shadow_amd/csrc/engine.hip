@@ -1,0 +1,584 @@
+// engine.hip -- host side of the routing engine (C-ABI in include/shd_route.h).
+#include "common.hpp"
+#include "sssp_f64.hpp"
+#include "sssp_k32.hpp"
+#include "direct_fw.hpp"
+
+using namespace shd;
+
+// =============================================================================
+// Host side
+// =============================================================================
+struct shd_route {
+    int device = 0;
+    int n = 0, m = 0, nnz = 0;
+    int directed = 0, prefer_direct = 0, complete = 0, integer_w = 0, multigraph = 0;
+    double min_w = 0;
+    // device graph
+    int* d_row = nullptr; int* d_col = nullptr; double* d_w = nullptr; double* d_r = nullptr;
+    int* d_row_in = nullptr; int* d_col_in = nullptr; double* d_w_in = nullptr; double* d_r_in = nullptr;
+    double* d_vf = nullptr; double* d_self_w = nullptr; double* d_self_r = nullptr;
+    double* d_W = nullptr; double* d_R = nullptr;  // dense direct tables (complete graphs, lazy)
+    int* d_err = nullptr;
+    char* d_ws = nullptr; size_t ws_stride = 0; int ws_slots = 0;
+    bool lds = false;
+    size_t lds_bytes = 0;
+    // K32 integer fast path (sssp_k32.hpp)
+    int k32 = 0, k32_block = 256, k32_bound = 0;
+    size_t k32_lds = 0;
+    int* d_k32_row_in = nullptr;
+    ArcRec* d_arc = nullptr;
+    uint16_t* d_k32_col_in = nullptr;
+    double* d_k32_r_in = nullptr;
+    uint64_t device_bytes = 0;
+    // host copies needed for lazy dense build
+    std::vector<int32_t> e_src, e_dst;
+    std::vector<double> e_lat, e_rel;
+    std::vector<void*> allocs;
+};
+
+namespace {
+
+int hip_check(hipError_t e) { return e == hipSuccess ? SHD_ROUTE_OK : SHD_ROUTE_EDEVICE; }
+
+template <typename T>
+int upload(shd_route* c, T** dptr, const std::vector<T>& h) {
+    size_t bytes = sizeof(T) * (h.empty() ? 1 : h.size());
+    if (hipMalloc((void**)dptr, bytes) != hipSuccess) return SHD_ROUTE_ENOMEM;
+    c->allocs.push_back(*dptr);
+    c->device_bytes += bytes;
+    if (!h.empty() && hipMemcpy(*dptr, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return SHD_ROUTE_EDEVICE;
+    return SHD_ROUTE_OK;
+}
+
+DevGraph dev_graph(const shd_route* c) {
+    DevGraph g;
+    g.n = c->n; g.prefer_direct = c->prefer_direct;
+    g.row = c->d_row; g.col = c->d_col; g.w = c->d_w; g.r = c->d_r;
+    g.row_in = c->d_row_in; g.col_in = c->d_col_in; g.w_in = c->d_w_in; g.r_in = c->d_r_in;
+    g.vf = c->d_vf; g.self_w = c->d_self_w; g.self_r = c->d_self_r;
+    return g;
+}
+
+// Build a CSR (rows by `key`, columns by `other`), arcs sorted by (row, col, eid).
+void build_csr(int n, const std::vector<int32_t>& rows, const std::vector<int32_t>& cols,
+               const std::vector<int32_t>& eids, const std::vector<double>& lat,
+               const std::vector<double>& rel, std::vector<int>& row, std::vector<int>& col,
+               std::vector<double>& w, std::vector<double>& r, std::vector<int>* eid_out = nullptr) {
+    const size_t k = rows.size();
+    std::vector<size_t> idx(k);
+    std::iota(idx.begin(), idx.end(), 0);
+    std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
+        if (rows[a] != rows[b]) return rows[a] < rows[b];
+        if (cols[a] != cols[b]) return cols[a] < cols[b];
+        return eids[a] < eids[b];
+    });
+    row.assign(n + 1, 0);
+    col.resize(k); w.resize(k); r.resize(k);
+    for (size_t q = 0; q < k; q++) {
+        size_t a = idx[q];
+        row[rows[a] + 1]++;
+        col[q] = cols[a];
+        w[q] = lat[eids[a]];
+        r[q] = rel[eids[a]];
+    }
+    if (eid_out) {
+        eid_out->resize(k);
+        for (size_t q = 0; q < k; q++) (*eid_out)[q] = eids[idx[q]];
+    }
+    for (int v = 0; v < n; v++) row[v + 1] += row[v];
+}
+
+bool strongly_connected(int n, const std::vector<int>& row, const std::vector<int>& col,
+                        const std::vector<int>& row_in, const std::vector<int>& col_in) {
+    auto reach_all = [&](const std::vector<int>& R, const std::vector<int>& Cc) {
+        std::vector<char> seen(n, 0);
+        std::vector<int> st{0};
+        seen[0] = 1;
+        int cnt = 1;
+        while (!st.empty()) {
+            int u = st.back(); st.pop_back();
+            for (int a = R[u]; a < R[u + 1]; a++)
+                if (!seen[Cc[a]]) { seen[Cc[a]] = 1; cnt++; st.push_back(Cc[a]); }
+        }
+        return cnt == n;
+    };
+    return reach_all(row, col) && reach_all(row_in, col_in);
+}
+
+int alloc_ws(shd_route* c) {
+    // per-source state in HBM when it cannot live in LDS
+    StateLayout L = StateLayout::make(c->n);
+    c->ws_stride = a16(L.total) + 256;
+    c->ws_slots = 1024;  // 256 CUs x 4 workgroups
+    size_t bytes = c->ws_stride * (size_t)c->ws_slots;
+    if (hipMalloc((void**)&c->d_ws, bytes) != hipSuccess) return SHD_ROUTE_ENOMEM;
+    c->allocs.push_back(c->d_ws);
+    return SHD_ROUTE_OK;
+}
+
+int ensure_dense(shd_route* c) {
+    if (c->d_W) return SHD_ROUTE_OK;
+    const size_t nn = (size_t)c->n * c->n;
+    std::vector<double> W(nn, NAN), R(nn, NAN);
+    // igraph_get_eid on a simple graph returns the unique edge; for parallel edges we
+    // keep the lowest edge id (documented deviation, SURVEY hazard H3).
+    for (int e = c->m - 1; e >= 0; e--) {
+        int a = c->e_src[e], b = c->e_dst[e];
+        W[(size_t)a * c->n + b] = c->e_lat[e];
+        R[(size_t)a * c->n + b] = c->e_rel[e];
+        if (!c->directed) {
+            W[(size_t)b * c->n + a] = c->e_lat[e];
+            R[(size_t)b * c->n + a] = c->e_rel[e];
+        }
+    }
+    int rc = upload(c, &c->d_W, W);
+    if (rc) return rc;
+    return upload(c, &c->d_R, R);
+}
+
+// Host Dijkstra (exact for integer weights) -> eccentricity of vertex 0.
+double ecc0(int n, const std::vector<int>& row, const std::vector<int>& col, const std::vector<double>& w) {
+    std::vector<double> d(n, INFINITY);
+    std::vector<std::pair<double, int>> h;
+    d[0] = 0;
+    h.push_back({0.0, 0});
+    auto cmp = [](const std::pair<double, int>& a, const std::pair<double, int>& b) { return a.first > b.first; };
+    while (!h.empty()) {
+        std::pop_heap(h.begin(), h.end(), cmp);
+        auto [du, u] = h.back();
+        h.pop_back();
+        if (du > d[u]) continue;
+        for (int a = row[u]; a < row[u + 1]; a++) {
+            double nd = du + w[a];
+            if (nd < d[col[a]]) { d[col[a]] = nd; h.push_back({nd, col[a]}); std::push_heap(h.begin(), h.end(), cmp); }
+        }
+    }
+    double mx = 0;
+    for (double x : d) mx = std::max(mx, x);
+    return mx;
+}
+
+// K32 eligibility + device arrays: in-rows sorted by (-w, u, eid); out-arc records carry
+// the slot of the same arc in its head's in-row.
+int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int>& col,
+                const std::vector<double>& w, const std::vector<int>& eid, const std::vector<int>& row_in,
+                const std::vector<int>& col_in, const std::vector<double>& w_in) {
+    const int n = c->n;
+    const char* force = getenv("SHD_ROUTE_KERNEL");
+    if (force && !strcmp(force, "f64")) return SHD_ROUTE_OK;
+    if (!c->integer_w || n > 65535 || c->multigraph) return SHD_ROUTE_OK;
+    for (int a = 0; a < c->nnz; a++) if (w[a] > 65535.0) return SHD_ROUTE_OK;
+    std::vector<int> indeg(n, 0);
+    for (int a = 0; a < c->nnz; a++) indeg[col[a]]++;
+    for (int v = 0; v < n; v++) if (indeg[v] > 65535) return SHD_ROUTE_OK;
+    const double bound = ecc0(n, row, col, w) + ecc0(n, row_in, col_in, w_in);
+    if (!(bound < 65535.0)) return SHD_ROUTE_OK;
+    const K32Layout L = K32Layout::make(n);
+    size_t lds = 0;
+    int block = 0;
+    for (int b : {256, 512, 1024}) {
+        size_t sm = b == 256 ? k32_small_bytes<256>() : b == 512 ? k32_small_bytes<512>() : k32_small_bytes<1024>();
+        size_t tot = sm + L.total;
+        if (tot > kLdsBudget) continue;
+        int per_cu = (int)(kLdsBudget / tot);
+        if (per_cu * (b / 64) >= 16 || b == 1024) { block = b; lds = tot; break; }
+    }
+    if (!block) return SHD_ROUTE_OK;
+    // in-rows: every out-arc a = (u -> v) appears in v's in-row
+    std::vector<int> irow(n + 1, 0);
+    for (int a = 0; a < c->nnz; a++) irow[col[a] + 1]++;
+    for (int v = 0; v < n; v++) irow[v + 1] += irow[v];
+    std::vector<int> order(c->nnz), fill(irow.begin(), irow.end() - 1), src_of(c->nnz);
+    for (int u = 0; u < n; u++)
+        for (int a = row[u]; a < row[u + 1]; a++) { src_of[a] = u; order[fill[col[a]]++] = a; }
+    for (int v = 0; v < n; v++)
+        std::sort(order.begin() + irow[v], order.begin() + irow[v + 1], [&](int x, int y) {
+            if (w[x] != w[y]) return w[x] > w[y];
+            if (src_of[x] != src_of[y]) return src_of[x] < src_of[y];
+            return eid[x] < eid[y];
+        });
+    std::vector<ArcRec> arcs(c->nnz);
+    std::vector<uint16_t> cin(c->nnz);
+    std::vector<double> rin(c->nnz);
+    for (int v = 0; v < n; v++)
+        for (int q = irow[v]; q < irow[v + 1]; q++) {
+            int a = order[q];
+            arcs[a].rslot = (uint16_t)(q - irow[v]);
+            cin[q] = (uint16_t)src_of[a];
+            rin[q] = c->e_rel[eid[a]];
+        }
+    for (int a = 0; a < c->nnz; a++) {
+        arcs[a].col = (uint16_t)col[a];
+        arcs[a].w = (uint16_t)w[a];
+        arcs[a].pad = 0;
+    }
+    int rc = upload(c, &c->d_k32_row_in, irow);
+    if (!rc) rc = upload(c, &c->d_arc, arcs);
+    if (!rc) rc = upload(c, &c->d_k32_col_in, cin);
+    if (!rc) rc = upload(c, &c->d_k32_r_in, rin);
+    if (rc) return rc;
+    const void* fn = block == 256 ? (const void*)sssp_k32_kernel<256>
+                   : block == 512 ? (const void*)sssp_k32_kernel<512> : (const void*)sssp_k32_kernel<1024>;
+    rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (rc) return rc;
+    c->k32 = 1; c->k32_block = block; c->k32_lds = lds; c->k32_bound = (int)bound;
+    return SHD_ROUTE_OK;
+}
+
+int take_err(shd_route* c) {
+    int h = 0;
+    if (hipMemcpy(&h, c->d_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    if (h) {
+        int z = 0;
+        if (hipMemcpy(c->d_err, &z, sizeof(int), hipMemcpyHostToDevice) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    }
+    return h;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* shd_route_strerror(int code) {
+    switch (code) {
+        case SHD_ROUTE_OK: return "success";
+        case SHD_ROUTE_EINVAL: return "invalid argument or topology failed validation";
+        case SHD_ROUTE_ENOMEM: return "out of memory";
+        case SHD_ROUTE_EDEVICE: return "HIP device error";
+        case SHD_ROUTE_ENOEDGE: return "path hop without an edge (missing self-loop?)";
+        case SHD_ROUTE_EUNREACH: return "target unreachable";
+        case SHD_ROUTE_EUNSUPPORTED: return "unsupported request";
+        default: return "unknown error";
+    }
+}
+
+int shd_route_create(shd_route_t** out, const shd_graph_t* g, int device) {
+    if (!out || !g) return SHD_ROUTE_EINVAL;
+    *out = nullptr;
+    const int n = g->n_vertices, m = g->n_edges;
+    if (n <= 0 || m < 0 || (m > 0 && (!g->edge_src || !g->edge_dst || !g->edge_latency || !g->edge_packetloss)))
+        return SHD_ROUTE_EINVAL;
+    // validation as topology.c:1041-1124 (edges) and 811-978 (vertex packetloss)
+    for (int e = 0; e < m; e++) {
+        int a = g->edge_src[e], b = g->edge_dst[e];
+        double w = g->edge_latency[e], p = g->edge_packetloss[e];
+        if (a < 0 || a >= n || b < 0 || b >= n) return SHD_ROUTE_EINVAL;
+        if (!(w > 0.0) || std::isinf(w)) return SHD_ROUTE_EINVAL;
+        if (!(p >= 0.0 && p <= 1.0)) return SHD_ROUTE_EINVAL;
+    }
+    if (g->vertex_packetloss)
+        for (int v = 0; v < n; v++) {
+            double p = g->vertex_packetloss[v];
+            if (!std::isnan(p) && !(p >= 0.0 && p <= 1.0)) return SHD_ROUTE_EINVAL;
+        }
+    if (hipSetDevice(device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+
+    shd_route* c = new (std::nothrow) shd_route();
+    if (!c) return SHD_ROUTE_ENOMEM;
+    c->device = device; c->n = n; c->m = m;
+    c->directed = g->directed ? 1 : 0;
+    c->prefer_direct = g->prefer_direct ? 1 : 0;
+    c->e_src.assign(g->edge_src, g->edge_src + m);
+    c->e_dst.assign(g->edge_dst, g->edge_dst + m);
+    c->e_lat.assign(g->edge_latency, g->edge_latency + m);
+    c->e_rel.resize(m);
+    for (int e = 0; e < m; e++) c->e_rel[e] = (1.0f - g->edge_packetloss[e]);  // topology.c:437
+
+    // arcs for SSSP (self-loops excluded: w > 0 never relaxes them)
+    std::vector<int32_t> ar, ac, ae, ir, ic, ie;
+    std::vector<double> self_w(n, NAN), self_r(n, NAN);
+    std::vector<int> loops(n, 0), degm(n, 0);
+    double maxw = 0;
+    c->min_w = m ? INFINITY : 0;
+    bool integral = true;
+    for (int e = 0; e < m; e++) {
+        int a = g->edge_src[e], b = g->edge_dst[e];
+        double w = g->edge_latency[e];
+        maxw = std::max(maxw, w);
+        c->min_w = std::min(c->min_w, w);
+        if (w != std::floor(w) || w > 1048576.0) integral = false;
+        if (a == b) {
+            if (std::isnan(self_w[a])) { self_w[a] = w; self_r[a] = c->e_rel[e]; }
+            loops[a]++;
+            continue;
+        }
+        ar.push_back(a); ac.push_back(b); ae.push_back(e);
+        degm[a]++;
+        if (!c->directed) { ar.push_back(b); ac.push_back(a); ae.push_back(e); degm[b]++; }
+        else { ir.push_back(b); ic.push_back(a); ie.push_back(e); }
+    }
+    c->integer_w = integral && (double)n * maxw < 2147483647.0;
+    std::vector<int> row, col, row_in, col_in, eid;
+    std::vector<double> w, r, w_in, r_in;
+    build_csr(n, ar, ac, ae, c->e_lat, c->e_rel, row, col, w, r, &eid);
+    if (c->directed) build_csr(n, ir, ic, ie, c->e_lat, c->e_rel, row_in, col_in, w_in, r_in);
+    c->nnz = (int)col.size();
+    for (int v = 0; v < n && !c->multigraph; v++)
+        for (int a = row[v] + 1; a < row[v + 1]; a++)
+            if (col[a] == col[a - 1]) { c->multigraph = 1; break; }
+    for (int v = 0; v < n; v++) if (loops[v] > 1) c->multigraph = 1;
+
+    // topology.c:738-806: strongly connected, one cluster
+    if (!strongly_connected(n, row, col, c->directed ? row_in : row, c->directed ? col_in : col)) {
+        delete c;
+        return SHD_ROUTE_EINVAL;
+    }
+    // topology.c:450-552 isComplete: OUT-incident count (undirected: loops twice, minus one)
+    c->complete = 1;
+    for (int v = 0; v < n; v++) {
+        long long ecount;
+        if (c->directed) ecount = (row[v + 1] - row[v]) + loops[v];
+        else ecount = (row[v + 1] - row[v]) + 2LL * loops[v] - (loops[v] > 0 ? 1 : 0);
+        if (ecount < n) { c->complete = 0; break; }
+    }
+
+    std::vector<double> vf(n, NAN);
+    if (g->vertex_packetloss)
+        for (int v = 0; v < n; v++)
+            if (!std::isnan(g->vertex_packetloss[v])) vf[v] = (1.0f - g->vertex_packetloss[v]);
+
+    int rc = SHD_ROUTE_OK;
+    if (!rc) rc = upload(c, &c->d_row, row);
+    if (!rc) rc = upload(c, &c->d_col, col);
+    if (!rc) rc = upload(c, &c->d_w, w);
+    if (!rc) rc = upload(c, &c->d_r, r);
+    if (c->directed) {
+        if (!rc) rc = upload(c, &c->d_row_in, row_in);
+        if (!rc) rc = upload(c, &c->d_col_in, col_in);
+        if (!rc) rc = upload(c, &c->d_w_in, w_in);
+        if (!rc) rc = upload(c, &c->d_r_in, r_in);
+    } else {
+        c->d_row_in = c->d_row; c->d_col_in = c->d_col; c->d_w_in = c->d_w; c->d_r_in = c->d_r;
+    }
+    if (!rc) rc = upload(c, &c->d_vf, vf);
+    if (!rc) rc = upload(c, &c->d_self_w, self_w);
+    if (!rc) rc = upload(c, &c->d_self_r, self_r);
+    if (!rc) {
+        std::vector<int> z(1, 0);
+        rc = upload(c, &c->d_err, z);
+    }
+    StateLayout L = StateLayout::make(n);
+    c->lds_bytes = kSmallBytes + L.total;
+    c->lds = c->lds_bytes <= kLdsBudget;
+    if (!rc) {
+        if (c->lds) {
+            rc = hip_check(hipFuncSetAttribute((const void*)sssp_rows_kernel<true>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_bytes));
+        } else {
+            rc = alloc_ws(c);
+        }
+    }
+    if (!rc) rc = prepare_k32(c, row, col, w, eid, c->directed ? row_in : row, c->directed ? col_in : col,
+                              c->directed ? w_in : w);
+    if (rc) {
+        shd_route_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return SHD_ROUTE_OK;
+}
+
+void shd_route_destroy(shd_route_t* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    for (void* p : c->allocs) (void)hipFree(p);
+    delete c;
+}
+
+int shd_route_get_info(const shd_route_t* c, shd_route_info_t* info) {
+    if (!c || !info) return SHD_ROUTE_EINVAL;
+    info->n_vertices = c->n;
+    info->n_edges = c->m;
+    info->n_arcs = c->nnz;
+    info->is_complete = c->complete;
+    info->directed = c->directed;
+    info->prefer_direct = c->prefer_direct;
+    info->integer_weights = c->integer_w;
+    info->multigraph = c->multigraph;
+    info->device = c->device;
+    info->lds_resident = (c->lds || c->k32) ? 1 : 0;
+    info->kernel = c->k32 ? 1 : 0;
+    info->dist_bound = c->k32_bound;
+    info->block = c->k32 ? c->k32_block : kBlock;
+    info->device_bytes = c->device_bytes;
+    info->min_edge_latency = c->min_w;
+    return SHD_ROUTE_OK;
+}
+
+int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const int32_t* d_tgt,
+                         int32_t nt, int64_t ld, uint32_t flags, double* d_lat, double* d_rel,
+                         double* d_row_min, void* stream) {
+    if (!c || ns < 0 || nt < 0 || (ns && !d_src) || (nt && !d_tgt) || ld < nt) return SHD_ROUTE_EINVAL;
+    if (ns == 0) return SHD_ROUTE_OK;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    if ((flags & SHD_ROUTE_DISPATCH) && c->complete) {
+        int rc = ensure_dense(c);
+        if (rc) return rc;
+        int grid = std::min(ns, 65535);
+        hipLaunchKernelGGL(direct_rows_kernel, dim3(grid), dim3(kBlock), 0, st, c->n, c->d_W, c->d_R,
+                           c->d_vf, d_src, ns, d_tgt, nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
+        return hip_check(hipGetLastError());
+    }
+    const int dispatch = (flags & SHD_ROUTE_DISPATCH) ? 1 : 0;
+    if (c->k32 && !(dispatch && c->prefer_direct)) {
+        DevK32 k;
+        k.n = c->n; k.bound = c->k32_bound; k.row = c->d_row; k.arc = c->d_arc; k.row_in = c->d_k32_row_in;
+        k.col_in = c->d_k32_col_in; k.r_in = c->d_k32_r_in; k.vf = c->d_vf; k.self_w = c->d_self_w;
+        k.self_r = c->d_self_r;
+        const int grid = std::min(ns, 1 << 20);
+        if (c->k32_block == 256)
+            hipLaunchKernelGGL(sssp_k32_kernel<256>, dim3(grid), dim3(256), c->k32_lds, st, k, d_src, ns, d_tgt, nt,
+                               (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
+        else if (c->k32_block == 512)
+            hipLaunchKernelGGL(sssp_k32_kernel<512>, dim3(grid), dim3(512), c->k32_lds, st, k, d_src, ns, d_tgt, nt,
+                               (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
+        else
+            hipLaunchKernelGGL(sssp_k32_kernel<1024>, dim3(grid), dim3(1024), c->k32_lds, st, k, d_src, ns, d_tgt, nt,
+                               (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
+        return hip_check(hipGetLastError());
+    }
+    DevGraph g = dev_graph(c);
+    if (c->lds) {
+        int grid = std::min(ns, 1 << 20);
+        hipLaunchKernelGGL(sssp_rows_kernel<true>, dim3(grid), dim3(kBlock), c->lds_bytes, st, g, d_src, ns,
+                           d_tgt, nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, nullptr, (size_t)0,
+                           dispatch);
+    } else {
+        int grid = std::min(ns, c->ws_slots);
+        hipLaunchKernelGGL(sssp_rows_kernel<false>, dim3(grid), dim3(kBlock), kSmallBytes, st, g, d_src, ns,
+                           d_tgt, nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_ws, c->ws_stride,
+                           dispatch);
+    }
+    return hip_check(hipGetLastError());
+}
+
+int shd_route_sync(shd_route_t* c, void* stream) {
+    if (!c) return SHD_ROUTE_EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    return take_err(c);
+}
+
+}  // extern "C"
+
+namespace {
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    int alloc(size_t b) { return hipMalloc(&p, b ? b : 1) == hipSuccess ? SHD_ROUTE_OK : SHD_ROUTE_ENOMEM; }
+};
+
+// Host-pointer wrapper: chunks rows so device output stays bounded, copies back.
+template <typename Launch>
+int host_rows(shd_route* c, const int32_t* src, int32_t ns, const int32_t* tgt, int32_t nt, double* lat_out,
+              double* rel_out, double* row_min_out, Launch launch) {
+    if (!c || ns < 0 || nt < 0 || (ns && !src) || (nt && !tgt)) return SHD_ROUTE_EINVAL;
+    if (ns == 0) return SHD_ROUTE_OK;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    const size_t row_bytes = sizeof(double) * (size_t)std::max(nt, 1);
+    int32_t chunk = (int32_t)std::max<size_t>(1, std::min<size_t>(ns, (size_t)(1u << 30) / row_bytes));
+    DevBuf dsrc, dtgt, dlat, drel, dmin;
+    int rc;
+    if ((rc = dsrc.alloc(sizeof(int32_t) * chunk)) || (rc = dtgt.alloc(sizeof(int32_t) * std::max(nt, 1))) ||
+        (rc = dlat.alloc(row_bytes * chunk)) || (rc = drel.alloc(row_bytes * chunk)) ||
+        (rc = dmin.alloc(sizeof(double) * chunk)))
+        return rc;
+    if (nt && hipMemcpy(dtgt.p, tgt, sizeof(int32_t) * nt, hipMemcpyHostToDevice) != hipSuccess)
+        return SHD_ROUTE_EDEVICE;
+    for (int32_t i0 = 0; i0 < ns; i0 += chunk) {
+        int32_t k = std::min(chunk, ns - i0);
+        if (hipMemcpy(dsrc.p, src + i0, sizeof(int32_t) * k, hipMemcpyHostToDevice) != hipSuccess)
+            return SHD_ROUTE_EDEVICE;
+        rc = launch((const int32_t*)dsrc.p, k, (const int32_t*)dtgt.p, (double*)dlat.p, (double*)drel.p,
+                    (double*)dmin.p);
+        if (rc) return rc;
+        if ((rc = shd_route_sync(c, nullptr))) return rc;
+        if (lat_out && hipMemcpy(lat_out + (size_t)i0 * nt, dlat.p, row_bytes * k, hipMemcpyDeviceToHost) != hipSuccess)
+            return SHD_ROUTE_EDEVICE;
+        if (rel_out && hipMemcpy(rel_out + (size_t)i0 * nt, drel.p, row_bytes * k, hipMemcpyDeviceToHost) != hipSuccess)
+            return SHD_ROUTE_EDEVICE;
+        if (row_min_out && hipMemcpy(row_min_out + i0, dmin.p, sizeof(double) * k, hipMemcpyDeviceToHost) != hipSuccess)
+            return SHD_ROUTE_EDEVICE;
+    }
+    return SHD_ROUTE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int shd_route_rows(shd_route_t* c, const int32_t* src, int32_t ns, const int32_t* tgt, int32_t nt,
+                   uint32_t flags, double* lat_out, double* rel_out, double* row_min_out) {
+    return host_rows(c, src, ns, tgt, nt, lat_out, rel_out, row_min_out,
+                     [&](const int32_t* ds, int32_t k, const int32_t* dt, double* dl, double* dr, double* dm) {
+                         return shd_route_rows_async(c, ds, k, dt, nt, nt, flags, dl, dr, dm, nullptr);
+                     });
+}
+
+int shd_route_direct(shd_route_t* c, const int32_t* src, int32_t ns, const int32_t* tgt, int32_t nt,
+                     double* lat_out, double* rel_out, double* row_min_out) {
+    if (!c) return SHD_ROUTE_EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    int rc = ensure_dense(c);
+    if (rc) return rc;
+    return host_rows(c, src, ns, tgt, nt, lat_out, rel_out, row_min_out,
+                     [&](const int32_t* ds, int32_t k, const int32_t* dt, double* dl, double* dr, double* dm) {
+                         int grid = std::min(k, 65535);
+                         hipLaunchKernelGGL(direct_rows_kernel, dim3(grid), dim3(kBlock), 0, nullptr, c->n, c->d_W,
+                                            c->d_R, c->d_vf, ds, k, dt, nt, (long long)nt, dl, dr, dm, c->d_err);
+                         return hip_check(hipGetLastError());
+                     });
+}
+
+int shd_route_self(shd_route_t* c, const int32_t* v, int32_t nv, double* lat_out, double* rel_out) {
+    if (!c || nv < 0 || (nv && (!v || !lat_out || !rel_out))) return SHD_ROUTE_EINVAL;
+    if (nv == 0) return SHD_ROUTE_OK;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    DevBuf dv, dl, dr;
+    int rc;
+    if ((rc = dv.alloc(sizeof(int32_t) * nv)) || (rc = dl.alloc(sizeof(double) * nv)) ||
+        (rc = dr.alloc(sizeof(double) * nv)))
+        return rc;
+    if (hipMemcpy(dv.p, v, sizeof(int32_t) * nv, hipMemcpyHostToDevice) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    DevGraph g = dev_graph(c);
+    hipLaunchKernelGGL(self_kernel, dim3((nv + 255) / 256), dim3(256), 0, nullptr, g, (const int*)dv.p, nv,
+                       (double*)dl.p, (double*)dr.p, c->d_err);
+    if ((rc = hip_check(hipGetLastError()))) return rc;
+    if ((rc = shd_route_sync(c, nullptr))) return rc;
+    if (hipMemcpy(lat_out, dl.p, sizeof(double) * nv, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(rel_out, dr.p, sizeof(double) * nv, hipMemcpyDeviceToHost) != hipSuccess)
+        return SHD_ROUTE_EDEVICE;
+    return SHD_ROUTE_OK;
+}
+
+int shd_route_min_reduce_async(shd_route_t* c, const double* d_vals, int64_t count, double* d_out, void* stream) {
+    if (!c || count < 0 || !d_out || (count && !d_vals)) return SHD_ROUTE_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    if (hipMemsetAsync(d_out, 0xFF, sizeof(double), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    if (count == 0) return SHD_ROUTE_OK;
+    long long blocks = std::min<long long>((count + kBlock - 1) / kBlock, 2048);
+    hipLaunchKernelGGL(min_reduce_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, d_vals, (long long)count,
+                       (unsigned long long*)d_out);
+    return hip_check(hipGetLastError());
+}
+
+int shd_route_fw_async(shd_route_t* c, double* d_dist, void* stream) {
+    if (!c || !d_dist) return SHD_ROUTE_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    const int n = c->n;
+    const int nb = (n + kT - 1) / kT;
+    for (int kb = 0; kb < nb; kb++) {
+        const int k0 = kb * kT;
+        hipLaunchKernelGGL(fw_diag_kernel, dim3(1), dim3(kT * 8), 0, st, d_dist, n, k0);
+        if (nb > 1)
+            hipLaunchKernelGGL(fw_panel_kernel, dim3(nb - 1, 2), dim3(kT * 8), 0, st, d_dist, n, k0);
+        hipLaunchKernelGGL(fw_rest_kernel, dim3(nb, nb), dim3(kT * 8), 0, st, d_dist, n, k0);
+    }
+    return hip_check(hipGetLastError());
+}
+
+}  // extern "C"

@@ -48,6 +48,7 @@ class _Info(C.Structure):
         ("is_complete", C.c_int32), ("directed", C.c_int32), ("prefer_direct", C.c_int32),
         ("integer_weights", C.c_int32), ("multigraph", C.c_int32), ("device", C.c_int32),
         ("lds_resident", C.c_int32), ("device_bytes", C.c_uint64), ("min_edge_latency", C.c_double),
+        ("kernel", C.c_int32), ("dist_bound", C.c_int32), ("block", C.c_int32), ("reserved", C.c_int32),
     ]
 
 

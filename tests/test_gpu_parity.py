@@ -22,6 +22,16 @@ def route():
     return r
 
 
+@pytest.fixture(params=["auto", "f64"])
+def kernel(request, monkeypatch):
+    """Run a test on the auto-selected kernel and on the generic f64 kernel."""
+    if request.param == "f64":
+        monkeypatch.setenv("SHD_ROUTE_KERNEL", "f64")
+    else:
+        monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    return request.param
+
+
 def _check_rows(eng, og, oracle_mod, src, tgt, rel_exact=True):
     lat, rel, mn = eng.rows(src, tgt, dispatch=False)
     olat, orel, ouq, _ = og.source_rows(src, tgt, oracle_mod.TIE_MINKEY)
@@ -37,16 +47,17 @@ def _check_rows(eng, og, oracle_mod, src, tgt, rel_exact=True):
     return lat, rel
 
 
-def test_c2_rows_bitexact(route, oracle_mod):
+def test_c2_rows_bitexact(route, oracle_mod, kernel):
     g = config("c2")
     eng = route.RouteEngine(g)
     assert eng.info["lds_resident"] == 1
+    assert eng.info["kernel"] == (1 if kernel == "auto" else 0)
     og = oracle_mod.OracleGraph(g)
     src = np.arange(0, g.n, 13, dtype=np.int32)
     _check_rows(eng, og, oracle_mod, src, g.targets())
 
 
-def test_c2_vertex_loss_within_tol(route, oracle_mod):
+def test_c2_vertex_loss_within_tol(route, oracle_mod, kernel):
     g = config("c2", vloss=True)
     eng = route.RouteEngine(g)
     og = oracle_mod.OracleGraph(g)
@@ -117,7 +128,7 @@ def digests():
     return json.load(open(os.path.join(GOLD, "rows_digests.json")))
 
 
-def test_c2_full_table_matches_golden(route, digests):
+def test_c2_full_table_matches_golden(route, digests, kernel):
     g = config("c2")
     eng = route.RouteEngine(g)
     T = g.targets()
@@ -133,7 +144,7 @@ def test_c2_full_table_matches_golden(route, digests):
 
 
 @pytest.mark.parametrize("cfg", ["c3", "c4"])
-def test_sampled_rows_match_golden(route, digests, cfg):
+def test_sampled_rows_match_golden(route, digests, cfg, kernel):
     g = config(cfg)
     eng = route.RouteEngine(g)
     T = g.targets()
@@ -157,7 +168,7 @@ def test_bundled_topology_engine(route):
     assert mn.min() == exp["min_latency"] == 5.0
 
 
-def test_small_golden_tables_engine(route):
+def test_small_golden_tables_engine(route, kernel):
     z = np.load(os.path.join(GOLD, "small_tables.npz"))
     for name in z["names"]:
         p = f"{name}__"
@@ -178,6 +189,15 @@ def test_small_golden_tables_engine(route):
         np.testing.assert_allclose(E_rel[uq], z[p + "rel"][uq], rtol=REL_TOL, atol=0, err_msg=name)
         if not len(vl) or np.all(vl == 0):
             assert np.array_equal(E_rel[uq], z[p + "rel"][uq]), name
-        # raw rows against the golden raw rows too
-        assert np.array_equal(lat if not (g.prefer_direct or eng.info["is_complete"]) else z[p + "raw_lat"],
-                              z[p + "raw_lat"]) or g.prefer_direct or eng.info["is_complete"], name
+        if not (g.prefer_direct or eng.info["is_complete"]):
+            # raw SOURCE rows against the golden raw rows too
+            assert np.array_equal(lat, z[p + "raw_lat"]), name
+
+
+def test_kernel_selection(route):
+    g = config("c2")
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 1 and 0 < eng.info["dist_bound"] < 65535
+    g2 = internet_like(300, 2, seed=3)
+    g2.latency = g2.latency + 0.25  # fractional -> generic f64 kernel
+    assert route.RouteEngine(g2).info["kernel"] == 0

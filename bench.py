@@ -102,7 +102,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--verify", type=int, default=8, help="rows checked against the oracle after timing")
     ap.add_argument("--sources", type=int, default=0, help="limit sources per rank (0 = all)")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "f64"], help="force the generic f64 SSSP kernel")
     args = ap.parse_args()
+    if args.kernel == "f64":
+        os.environ["SHD_ROUTE_KERNEL"] = "f64"
 
     import torch
     import torch.distributed as dist
@@ -234,7 +237,8 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
             "traffic": load_traffic(args.config, ns),
-            "kernel": "sssp_rows_kernel", "bytes_per_source": b_src(n, nnz, nt),
+            "kernel": ("sssp_k32_kernel" if eng.info["kernel"] == 1 else "sssp_rows_kernel"),
+            "bytes_per_source": b_src(n, nnz, nt),
         },
         "verified_rows_vs_oracle": verified,
     }

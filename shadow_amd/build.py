@@ -25,6 +25,16 @@ def needs_build() -> bool:
     return any(os.path.getmtime(p) > t for p in deps)
 
 
+def build_diag(verbose: bool = False) -> str:
+    """Diagnostic build with per-phase s_memtime stamps (tools/stamps.py); never shipped."""
+    out = os.path.join(HERE, "libshd_route_diag.so")
+    cmd = [HIPCC, *FLAGS, "-DSHD_STAMPS", "-o", out, *SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if force or needs_build():
         cmd = [HIPCC, *FLAGS, "-o", OUT, *SOURCES]
@@ -35,4 +45,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose=True)
+    if "--diag" in sys.argv:
+        build_diag(verbose=True)
+    else:
+        build(force="--force" in sys.argv, verbose=True)

@@ -30,6 +30,7 @@ struct shd_route {
     ArcRec* d_arc = nullptr;
     uint16_t* d_k32_col_in = nullptr;
     double* d_k32_r_in = nullptr;
+    unsigned long long* d_dbg = nullptr;  // SHD_STAMPS builds: per-source phase stamps
     uint64_t device_bytes = 0;
     // host copies needed for lazy dense build
     std::vector<int32_t> e_src, e_dst;
@@ -428,6 +429,7 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         k.n = c->n; k.bound = c->k32_bound; k.row = c->d_row; k.arc = c->d_arc; k.row_in = c->d_k32_row_in;
         k.col_in = c->d_k32_col_in; k.r_in = c->d_k32_r_in; k.vf = c->d_vf; k.self_w = c->d_self_w;
         k.self_r = c->d_self_r;
+        k.dbg = c->d_dbg;
         const int grid = std::min(ns, 1 << 20);
         if (c->k32_block == 256)
             hipLaunchKernelGGL(sssp_k32_kernel<256>, dim3(grid), dim3(256), c->k32_lds, st, k, d_src, ns, d_tgt, nt,
@@ -582,3 +584,12 @@ int shd_route_fw_async(shd_route_t* c, double* d_dist, void* stream) {
 }
 
 }  // extern "C"
+
+#ifdef SHD_STAMPS
+// Diagnostic builds only (not part of include/shd_route.h): per-source phase stamps.
+extern "C" int shd_route_debug_buffer(shd_route_t* c, void* d_buf) {
+    if (!c) return SHD_ROUTE_EINVAL;
+    c->d_dbg = (unsigned long long*)d_buf;
+    return SHD_ROUTE_OK;
+}
+#endif

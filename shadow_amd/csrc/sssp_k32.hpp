@@ -36,7 +36,16 @@ struct DevK32 {
     const double* __restrict__ vf;
     const double* __restrict__ self_w;
     const double* __restrict__ self_r;
+    unsigned long long* dbg;             // SHD_STAMPS diagnostic builds only: 8 words per source
 };
+
+#ifdef SHD_STAMPS
+#define K32_STAMP(slot) do { if (tid == 0 && g.dbg) { g.dbg[(size_t)i * 8 + (slot)] = __builtin_amdgcn_s_memtime(); } } while (0)
+#define K32_COUNT(slot, x) do { if (g.dbg) atomicAdd(&g.dbg[(size_t)i * 8 + (slot)], (unsigned long long)(x)); } while (0)
+#else
+#define K32_STAMP(slot) do { } while (0)
+#define K32_COUNT(slot, x) do { } while (0)
+#endif
 
 struct K32Layout {
     size_t key, relv, par, bits, total;
@@ -54,36 +63,12 @@ struct K32Layout {
 
 template <int B>
 struct K32Small {
-    int off[B + 1];
-    int u[B];
-    int beg[B];
-    int wsum[B / 64];
+    unsigned char wflag[B / 64][64];  // per-wave arc-window start flags
     int qnext;
+    int cursor;
     int flag;
     unsigned long long rmin;
 };
-
-template <int B>
-__device__ inline int block_scan_b(int x, int* wsum, int* total) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int incl = x;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        int y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-    }
-    if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
-    int pre = 0, tot = 0;
-#pragma unroll
-    for (int k = 0; k < B / 64; k++) {
-        int s = wsum[k];
-        pre += (k < wv) ? s : 0;
-        tot += s;
-    }
-    *total = tot;
-    return pre + incl - x;
-}
 
 template <int B>
 __global__ __launch_bounds__(B) void sssp_k32_kernel(DevK32 g, const int* __restrict__ src, int ns,
@@ -95,6 +80,9 @@ __global__ __launch_bounds__(B) void sssp_k32_kernel(DevK32 g, const int* __rest
     K32Small<B>* sm = reinterpret_cast<K32Small<B>*>(smem);
     const int n = g.n;
     const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    unsigned char* wflag = sm->wflag[tid >> 6];
+    wflag[lane] = 0;
     const K32Layout L = K32Layout::make(n);
     char* base = smem + kSm;
     uint32_t* key = reinterpret_cast<uint32_t*>(base + L.key);
@@ -123,12 +111,22 @@ __global__ __launch_bounds__(B) void sssp_k32_kernel(DevK32 g, const int* __rest
         uint16_t* qn = q1;
         int qlen = 1;
         __syncthreads();
+        K32_STAMP(0);
 
         // ---- phase A: frontier Bellman-Ford on packed (dist, slot) keys ----------
+        // Each wave grabs 64 frontier vertices at a time (LDS cursor) and expands their
+        // arcs 64 at a time, load-balanced with no block barrier: wave scan of the
+        // degrees, then each arc lane finds its owner vertex from the window's
+        // start-position mask (ballot of LDS flags) and two popcounts.
         while (qlen > 0) {
-            if (tid == 0) sm->qnext = 0;
-            for (int c0 = 0; c0 < qlen; c0 += B) {
-                const int k = c0 + tid;
+            if (tid == 0) { sm->qnext = 0; sm->cursor = 0; }
+            __syncthreads();
+            for (;;) {
+                int start = 0;
+                if (lane == 0) start = atomicAdd(&sm->cursor, 64);
+                start = __shfl(start, 0, 64);
+                if (start >= qlen) break;
+                const int k = start + lane;
                 int u = 0, beg = 0, deg = 0;
                 if (k < qlen) {
                     u = qc[k];
@@ -136,39 +134,61 @@ __global__ __launch_bounds__(B) void sssp_k32_kernel(DevK32 g, const int* __rest
                     beg = g.row[u];
                     deg = g.row[u + 1] - beg;
                 }
-                int total;
-                const int off = block_scan_b<B>(deg, sm->wsum, &total);
-                const int cnt = min(B, qlen - c0);
-                sm->off[tid] = off;
-                sm->u[tid] = u;
-                sm->beg[tid] = beg;
-                __syncthreads();
-                for (int e = tid; e < total; e += B) {
-                    int lo = 0, hi = cnt;
-                    while (lo < hi) {
-                        const int mid = (lo + hi) >> 1;
-                        if (sm->off[mid] <= e) lo = mid + 1; else hi = mid;
-                    }
-                    const int o = lo - 1;
-                    const ArcRec rec = g.arc[sm->beg[o] + (e - sm->off[o])];
-                    const uint32_t nd = (key[sm->u[o]] >> 16) + rec.w;
-                    if (nd > bound) continue;  // cannot be final (all latencies <= bound)
-                    const uint32_t cand = (nd << 16) | rec.rslot;
-                    const int v = rec.col;
-                    if (cand < key[v]) {
-                        const uint32_t old = atomicMin(&key[v], cand);
-                        if (nd < (old >> 16)) {  // distance improved: (re)expand v
-                            const uint32_t m = 1u << (v & 31);
-                            if (!(atomicOr(&bits[v >> 5], m) & m)) qn[atomicAdd(&sm->qnext, 1)] = (uint16_t)v;
+                int incl = deg;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const int y = __shfl_up(incl, d, 64);
+                    if (lane >= d) incl += y;
+                }
+                const int total = __shfl(incl, 63, 64);
+                if (lane == 0) K32_COUNT(5, total);
+                const int excl = incl - deg;
+                const int boff = beg - excl;
+                const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+                for (int base = 0; base < total; base += 64) {
+                    const int pos = excl - base;
+                    if (deg > 0 && pos >= 0 && pos < 64) wflag[pos] = 1;
+                    __builtin_amdgcn_wave_barrier();
+                    const unsigned long long M = __ballot(wflag[lane] != 0);
+                    wflag[lane] = 0;
+                    const int l0 = __popcll(__ballot(incl <= base));
+                    const int o = (l0 + __popcll(M & upto) - (int)(M & 1ull)) & 63;
+                    const int ob = __shfl(boff, o, 64);
+                    const int ou = __shfl(u, o, 64);
+                    const int e = base + lane;
+                    bool push = false;
+                    int v = 0;
+                    if (e < total) {
+                        const ArcRec rec = g.arc[ob + e];
+                        const uint32_t nd = (key[ou] >> 16) + rec.w;
+                        v = rec.col;
+                        const uint32_t cand = (nd << 16) | rec.rslot;
+                        if (nd <= bound && cand < key[v]) {  // nd > bound can never be final
+                            const uint32_t old = atomicMin(&key[v], cand);
+                            if (nd < (old >> 16)) {  // distance improved: (re)expand v
+                                const uint32_t m = 1u << (v & 31);
+                                push = !(atomicOr(&bits[v >> 5], m) & m);
+                            }
                         }
                     }
+                    // wave-aggregated enqueue
+                    const unsigned long long pm = __ballot(push);
+                    if (pm) {
+                        int qb = 0;
+                        const int leader = __ffsll((long long)pm) - 1;
+                        if (lane == leader) qb = atomicAdd(&sm->qnext, __popcll(pm));
+                        qb = __shfl(qb, leader, 64);
+                        if (push) qn[qb + __popcll(pm & ((1ull << lane) - 1ull))] = (uint16_t)v;
+                    }
                 }
-                __syncthreads();
             }
+            __syncthreads();
             qlen = sm->qnext;
             uint16_t* t = qc; qc = qn; qn = t;
+            if (tid == 0) K32_COUNT(6, 1);
             __syncthreads();
         }
+        K32_STAMP(1);
 
         // ---- phase B: parent vertex from the slot; relv init (queues are dead) ----
         const double fs = g.vf[s];
@@ -182,6 +202,7 @@ __global__ __launch_bounds__(B) void sssp_k32_kernel(DevK32 g, const int* __rest
             relv[v] = (v == s) ? cs : -1.0;
         }
         __syncthreads();
+        K32_STAMP(2);
 
         // ---- phase C: reliability down the tree, level-synchronous, LDS only ------
         for (;;) {
@@ -203,7 +224,9 @@ __global__ __launch_bounds__(B) void sssp_k32_kernel(DevK32 g, const int* __rest
             const int again = sm->flag;
             __syncthreads();
             if (!again) break;
+            if (tid == 0) K32_COUNT(7, 1);
         }
+        K32_STAMP(3);
 
         // ---- phase D: row output + row min -----------------------------------
         if (tid == 0) sm->rmin = kInfBits;
@@ -249,6 +272,7 @@ __global__ __launch_bounds__(B) void sssp_k32_kernel(DevK32 g, const int* __rest
             if (tid == 0) row_min[i] = as_d(sm->rmin);
         }
         __syncthreads();
+        K32_STAMP(4);
     }
 }
 

@@ -14,7 +14,7 @@ import numpy as np
 from .graph import Graph
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libshd_route.so")
+LIB_PATH = os.environ.get("SHD_ROUTE_LIB") or os.path.join(_HERE, "libshd_route.so")
 
 OK = 0
 EINVAL = -1

@@ -65,7 +65,8 @@ def test_c2_vertex_loss_within_tol(route, oracle_mod, kernel):
     _check_rows(eng, og, oracle_mod, src, g.targets(), rel_exact=False)
 
 
-def test_hbm_resident_path(route, oracle_mod):
+def test_hbm_resident_path(route, oracle_mod, monkeypatch):
+    monkeypatch.setenv("SHD_ROUTE_KERNEL", "f64")
     g = internet_like(8000, 3, seed=5, name="hbm")
     eng = route.RouteEngine(g)
     assert eng.info["lds_resident"] == 0

@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Per-phase cycle breakdown of the K32 kernel from a diagnostic (SHD_STAMPS) build.
+Run on the GPU box:  SHD_ROUTE_LIB=shadow_amd/libshd_route_diag.so python tools/stamps.py --config c2"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("SHD_ROUTE_LIB", os.path.join(ROOT, "shadow_amd", "libshd_route_diag.so"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from shadow_amd import route  # noqa: E402
+from shadow_amd.graph import config  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="c2")
+ap.add_argument("--sources", type=int, default=0)
+a = ap.parse_args()
+g = config(a.config)
+eng = route.RouteEngine(g)
+L = route.load_library()
+T = g.targets()
+S = T if not a.sources else T[: a.sources]
+dev = torch.device("cuda", 0)
+d_src = torch.from_numpy(S.astype(np.int32)).to(dev)
+d_tgt = torch.from_numpy(T.astype(np.int32)).to(dev)
+lat = torch.empty((len(S), len(T)), dtype=torch.float64, device=dev)
+rel = torch.empty_like(lat)
+mn = torch.empty(len(S), dtype=torch.float64, device=dev)
+dbg = torch.zeros((len(S), 8), dtype=torch.int64, device=dev)
+L.shd_route_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
+L.shd_route_debug_buffer(eng._h, C.c_void_p(dbg.data_ptr()))
+for rep in range(3):
+    dbg.zero_()
+    eng.rows_async(d_src, d_tgt, lat, rel, mn)
+    eng.sync()
+d = dbg.cpu().numpy().astype(np.int64)
+ph = np.diff(d[:, :5], axis=1)
+names = ["A_bf", "B_parent", "C_rel", "D_out"]
+print(f"config {a.config} n={g.n} nnz={g.nnz} sources={len(S)} kernel={eng.info['kernel']} block={eng.info['block']}")
+for k, nm in enumerate(names):
+    print(f"  {nm:10s} mean {ph[:, k].mean():10.0f} cyc  p50 {np.median(ph[:, k]):10.0f}  max {ph[:, k].max():10.0f}")
+tot = d[:, 4] - d[:, 0]
+print(f"  total      mean {tot.mean():10.0f} cyc")
+print(f"  arcs expanded / nnz   {d[:, 5].mean() / g.nnz:.2f}")
+print(f"  BF rounds mean/max    {d[:, 6].mean():.1f} / {d[:, 6].max()}")
+print(f"  rel sweeps mean/max   {d[:, 7].mean():.1f} / {d[:, 7].max()}")
+t0 = d[:, 0] - d[:, 0].min()
+print(f"  start spread (cyc): p50 {np.median(t0):.0f} max {t0.max()}  end max {(d[:, 4] - d[:, 0].min()).max()}")

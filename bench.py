@@ -237,7 +237,8 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
             "traffic": load_traffic(args.config, ns),
-            "kernel": ("sssp_k32_kernel" if eng.info["kernel"] == 1 else "sssp_rows_kernel"),
+            "kernel": {0: "sssp_rows_kernel", 1: "sssp_k32_kernel",
+                       2: "sssp_batch_kernel+path_attr_kernel"}[eng.info["kernel"]],
             "bytes_per_source": b_src(n, nnz, nt),
         },
         "verified_rows_vs_oracle": verified,

@@ -2,6 +2,8 @@
 #include "common.hpp"
 #include "sssp_f64.hpp"
 #include "sssp_k32.hpp"
+#include "sssp_batch.hpp"
+#include "path_attr.hpp"
 #include "direct_fw.hpp"
 
 using namespace shd;
@@ -31,6 +33,14 @@ struct shd_route {
     uint16_t* d_k32_col_in = nullptr;
     double* d_k32_r_in = nullptr;
     unsigned long long* d_dbg = nullptr;  // SHD_STAMPS builds: per-source phase stamps
+    // KB batched kernel (sssp_batch.hpp) + K2 path attributes (path_attr.hpp)
+    int kb = 0, attr = 0, kb_nseg = 0, kb_nhub = 0, kb_npart = 0;
+    size_t kb_lds = 0, attr_lds = 0;
+    uint32_t* d_kb_arc = nullptr;
+    KBSeg* d_kb_seg = nullptr;
+    KBHub* d_kb_hub = nullptr;
+    uint32_t* d_keys = nullptr;     // key rows scratch (ns x n u32), grown on demand
+    size_t keys_cap = 0;
     uint64_t device_bytes = 0;
     // host copies needed for lazy dense build
     std::vector<int32_t> e_src, e_dst;
@@ -169,6 +179,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
     const int n = c->n;
     const char* force = getenv("SHD_ROUTE_KERNEL");
     if (force && !strcmp(force, "f64")) return SHD_ROUTE_OK;
+    if (force && !*force) force = nullptr;
     if (!c->integer_w || n > 65535 || c->multigraph) return SHD_ROUTE_OK;
     for (int a = 0; a < c->nnz; a++) if (w[a] > 65535.0) return SHD_ROUTE_OK;
     std::vector<int> indeg(n, 0);
@@ -186,7 +197,6 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
         int per_cu = (int)(kLdsBudget / tot);
         if (per_cu * (b / 64) >= 16 || b == 1024) { block = b; lds = tot; break; }
     }
-    if (!block) return SHD_ROUTE_OK;
     // in-rows: every out-arc a = (u -> v) appears in v's in-row
     std::vector<int> irow(n + 1, 0);
     for (int a = 0; a < c->nnz; a++) irow[col[a] + 1]++;
@@ -220,11 +230,53 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
     if (!rc) rc = upload(c, &c->d_k32_col_in, cin);
     if (!rc) rc = upload(c, &c->d_k32_r_in, rin);
     if (rc) return rc;
-    const void* fn = block == 256 ? (const void*)sssp_k32_kernel<256>
-                   : block == 512 ? (const void*)sssp_k32_kernel<512> : (const void*)sssp_k32_kernel<1024>;
-    rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    if (rc) return rc;
-    c->k32 = 1; c->k32_block = block; c->k32_lds = lds; c->k32_bound = (int)bound;
+    c->k32_bound = (int)bound;
+    const bool want_k32 = !force || !strcmp(force, "k32") || !strcmp(force, "auto");
+    const bool want_kb = !force || !strcmp(force, "kb") || !strcmp(force, "auto");
+    if (block && want_k32) {
+        const void* fn = block == 256 ? (const void*)sssp_k32_kernel<256>
+                       : block == 512 ? (const void*)sssp_k32_kernel<512> : (const void*)sssp_k32_kernel<1024>;
+        rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        if (rc) return rc;
+        c->k32 = 1; c->k32_block = block; c->k32_lds = lds;
+    }
+    // K2 path attributes: relv f64 + parent u16 per vertex in LDS
+    const AttrLayout AL = AttrLayout::make(n);
+    if (AL.total <= kLdsBudget) {
+        c->attr = 1;
+        c->attr_lds = AL.total;
+        rc = hip_check(hipFuncSetAttribute((const void*)path_attr_kernel<256>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)AL.total));
+        if (rc) return rc;
+    }
+    // KB batched kernel: segments of <= KB_SEG in-arcs, hub rows split
+    if (c->attr && want_kb) {
+        std::vector<KBSeg> segs;
+        std::vector<KBHub> hubs;
+        int npart = 0;
+        for (int v = 0; v < n; v++) {
+            const int a0 = irow[v], a1 = irow[v + 1];
+            if (a1 - a0 <= KB_SEG) { segs.push_back({v, a0, a1, -1}); continue; }
+            KBHub h{v, npart, 0, 0};
+            for (int a = a0; a < a1; a += KB_SEG) segs.push_back({v, a, std::min(a1, a + KB_SEG), npart++});
+            h.p1 = npart;
+            hubs.push_back(h);
+        }
+        const KBLayout KL = KBLayout::make(n, c->nnz, npart);
+        const size_t kbl = kKBSmall + KL.total;
+        if (kbl <= kLdsBudget) {
+            std::vector<uint32_t> packed(((size_t)c->nnz + 3) / 4 * 4, 0u);
+            for (int q = 0; q < c->nnz; q++) packed[q] = ((uint32_t)cin[q] << 16) | (uint32_t)w[order[q]];
+            rc = upload(c, &c->d_kb_arc, packed);
+            if (!rc) rc = upload(c, &c->d_kb_seg, segs);
+            if (!rc && !hubs.empty()) rc = upload(c, &c->d_kb_hub, hubs);
+            if (!rc) rc = hip_check(hipFuncSetAttribute((const void*)sssp_batch_kernel,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kbl));
+            if (rc) return rc;
+            c->kb = 1; c->kb_lds = kbl; c->kb_nseg = (int)segs.size(); c->kb_nhub = (int)hubs.size();
+            c->kb_npart = npart;
+        }
+    }
     return SHD_ROUTE_OK;
 }
 
@@ -384,6 +436,7 @@ int shd_route_create(shd_route_t** out, const shd_graph_t* g, int device) {
 void shd_route_destroy(shd_route_t* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    if (c->d_keys) (void)hipFree(c->d_keys);
     for (void* p : c->allocs) (void)hipFree(p);
     delete c;
 }
@@ -399,10 +452,10 @@ int shd_route_get_info(const shd_route_t* c, shd_route_info_t* info) {
     info->integer_weights = c->integer_w;
     info->multigraph = c->multigraph;
     info->device = c->device;
-    info->lds_resident = (c->lds || c->k32) ? 1 : 0;
-    info->kernel = c->k32 ? 1 : 0;
+    info->lds_resident = (c->lds || c->k32 || c->kb) ? 1 : 0;
+    info->kernel = c->kb ? 2 : c->k32 ? 1 : 0;
     info->dist_bound = c->k32_bound;
-    info->block = c->k32 ? c->k32_block : kBlock;
+    info->block = c->kb ? KB_BLOCK : c->k32 ? c->k32_block : kBlock;
     info->device_bytes = c->device_bytes;
     info->min_edge_latency = c->min_w;
     return SHD_ROUTE_OK;
@@ -424,6 +477,33 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         return hip_check(hipGetLastError());
     }
     const int dispatch = (flags & SHD_ROUTE_DISPATCH) ? 1 : 0;
+    if (c->kb && !(dispatch && c->prefer_direct)) {
+        // KB distances+parents for KB_SRC sources per workgroup -> key rows -> K2
+        const size_t need = (size_t)ns * c->n;
+        if (need > c->keys_cap) {
+            if (c->d_keys) (void)hipFree(c->d_keys);
+            c->d_keys = nullptr;
+            c->keys_cap = 0;
+            if (hipMalloc((void**)&c->d_keys, need * sizeof(uint32_t)) != hipSuccess) return SHD_ROUTE_ENOMEM;
+            c->keys_cap = need;
+        }
+        DevKB kb;
+        kb.n = c->n; kb.nnz = c->nnz; kb.nseg = c->kb_nseg; kb.nhub = c->kb_nhub; kb.npart = c->kb_npart;
+        kb.bound = c->k32_bound; kb.arc = c->d_kb_arc; kb.row_in = c->d_k32_row_in; kb.seg = c->d_kb_seg;
+        kb.hub = c->d_kb_hub;
+        const int gridb = std::min((ns + KB_SRC - 1) / KB_SRC, 1 << 20);
+        hipLaunchKernelGGL(sssp_batch_kernel, dim3(gridb), dim3(KB_BLOCK), c->kb_lds, st, kb, d_src, ns, c->d_keys,
+                           (long long)c->n, c->d_err);
+        int rc = hip_check(hipGetLastError());
+        if (rc) return rc;
+        DevAttr at;
+        at.n = c->n; at.row_in = c->d_k32_row_in; at.col_in = c->d_k32_col_in; at.r_in = c->d_k32_r_in;
+        at.vf = c->d_vf; at.self_w = c->d_self_w; at.self_r = c->d_self_r;
+        const int grida = std::min(ns, 1 << 20);
+        hipLaunchKernelGGL(path_attr_kernel<256>, dim3(grida), dim3(256), c->attr_lds, st, at, c->d_keys,
+                           (long long)c->n, d_src, ns, d_tgt, nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
+        return hip_check(hipGetLastError());
+    }
     if (c->k32 && !(dispatch && c->prefer_direct)) {
         DevK32 k;
         k.n = c->n; k.bound = c->k32_bound; k.row = c->d_row; k.arc = c->d_arc; k.row_in = c->d_k32_row_in;

@@ -22,13 +22,16 @@ def route():
     return r
 
 
-@pytest.fixture(params=["auto", "f64"])
+KERNEL_ID = {"f64": 0, "k32": 1, "kb": 2}
+
+
+@pytest.fixture(params=["auto", "k32", "f64"])
 def kernel(request, monkeypatch):
-    """Run a test on the auto-selected kernel and on the generic f64 kernel."""
-    if request.param == "f64":
-        monkeypatch.setenv("SHD_ROUTE_KERNEL", "f64")
-    else:
+    """Run a test on the auto-selected kernel and on each forced kernel."""
+    if request.param == "auto":
         monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    else:
+        monkeypatch.setenv("SHD_ROUTE_KERNEL", request.param)
     return request.param
 
 
@@ -51,7 +54,7 @@ def test_c2_rows_bitexact(route, oracle_mod, kernel):
     g = config("c2")
     eng = route.RouteEngine(g)
     assert eng.info["lds_resident"] == 1
-    assert eng.info["kernel"] == (1 if kernel == "auto" else 0)
+    assert eng.info["kernel"] == (2 if kernel == "auto" else KERNEL_ID[kernel])
     og = oracle_mod.OracleGraph(g)
     src = np.arange(0, g.n, 13, dtype=np.int32)
     _check_rows(eng, og, oracle_mod, src, g.targets())
@@ -198,7 +201,7 @@ def test_small_golden_tables_engine(route, kernel):
 def test_kernel_selection(route):
     g = config("c2")
     eng = route.RouteEngine(g)
-    assert eng.info["kernel"] == 1 and 0 < eng.info["dist_bound"] < 65535
+    assert eng.info["kernel"] == 2 and 0 < eng.info["dist_bound"] < 65535
     g2 = internet_like(300, 2, seed=3)
     g2.latency = g2.latency + 0.25  # fractional -> generic f64 kernel
     assert route.RouteEngine(g2).info["kernel"] == 0

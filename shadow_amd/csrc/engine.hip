@@ -262,6 +262,9 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
             h.p1 = npart;
             hubs.push_back(h);
         }
+        // equal-length segments side by side: a wave's lanes finish their rows together
+        std::stable_sort(segs.begin(), segs.end(),
+                         [](const KBSeg& x, const KBSeg& y) { return (x.a1 - x.a0) > (y.a1 - y.a0); });
         const KBLayout KL = KBLayout::make(n, c->nnz, npart);
         const size_t kbl = kKBSmall + KL.total;
         if (kbl <= kLdsBudget) {
@@ -491,6 +494,7 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         kb.n = c->n; kb.nnz = c->nnz; kb.nseg = c->kb_nseg; kb.nhub = c->kb_nhub; kb.npart = c->kb_npart;
         kb.bound = c->k32_bound; kb.arc = c->d_kb_arc; kb.row_in = c->d_k32_row_in; kb.seg = c->d_kb_seg;
         kb.hub = c->d_kb_hub;
+        kb.dbg = c->d_dbg ? c->d_dbg + (size_t)ns * 8 : nullptr;
         const int gridb = std::min((ns + KB_SRC - 1) / KB_SRC, 1 << 20);
         hipLaunchKernelGGL(sssp_batch_kernel, dim3(gridb), dim3(KB_BLOCK), c->kb_lds, st, kb, d_src, ns, c->d_keys,
                            (long long)c->n, c->d_err);
@@ -499,6 +503,7 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         DevAttr at;
         at.n = c->n; at.row_in = c->d_k32_row_in; at.col_in = c->d_k32_col_in; at.r_in = c->d_k32_r_in;
         at.vf = c->d_vf; at.self_w = c->d_self_w; at.self_r = c->d_self_r;
+        at.dbg = c->d_dbg;
         const int grida = std::min(ns, 1 << 20);
         hipLaunchKernelGGL(path_attr_kernel<256>, dim3(grida), dim3(256), c->attr_lds, st, at, c->d_keys,
                            (long long)c->n, d_src, ns, d_tgt, nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err);

@@ -10,6 +10,8 @@
 
 namespace shd {
 
+constexpr int AT_ILP = 8;  // independent elements per thread per loop trip
+
 struct DevAttr {
     int n;
     const int* __restrict__ row_in;      // in-CSR offsets, rows sorted by (-w, u, eid)
@@ -18,6 +20,7 @@ struct DevAttr {
     const double* __restrict__ vf;
     const double* __restrict__ self_w;
     const double* __restrict__ self_r;
+    unsigned long long* dbg;   // SHD_STAMPS builds: 8 words per source
 };
 
 struct AttrLayout {
@@ -54,32 +57,61 @@ __global__ __launch_bounds__(B) void path_attr_kernel(DevAttr g, const uint32_t*
             continue;
         }
         const uint32_t* krow = keys + (long long)i * kld;
+        if (tid == 0 && g.dbg) g.dbg[(size_t)i * 8 + 0] = __builtin_amdgcn_s_memtime();
         const double fs = g.vf[s];
         const double cs = isnan(fs) ? 1.0 : 1.0 * fs;
         // parent vertex + parent-arc reliability (stored negated: sign bit = pending)
-        for (int v = tid; v < n; v += B) {
-            const uint32_t kv = krow[v];
-            if (v == s) { par[v] = (uint16_t)s; relv[v] = cs; }
-            else if (kv == 0xFFFFFFFFu) { par[v] = 0xFFFFu; relv[v] = -1.0; }
-            else {
-                const int a = g.row_in[v] + (int)(kv & 0xFFFFu);
-                par[v] = g.col_in[a];
-                relv[v] = -g.r_in[a];
+        // blocked by AT_ILP vertices per thread so the dependent global gathers overlap
+        for (int v0 = tid; v0 < n; v0 += B * AT_ILP) {
+            uint32_t kv[AT_ILP];
+            int a[AT_ILP];
+#pragma unroll
+            for (int q = 0; q < AT_ILP; q++) {
+                const int v = v0 + q * B;
+                kv[q] = v < n ? krow[v] : 0xFFFFFFFFu;
+                a[q] = v < n ? g.row_in[v] : 0;
+            }
+            uint16_t pu[AT_ILP];
+            double pr[AT_ILP];
+#pragma unroll
+            for (int q = 0; q < AT_ILP; q++) {
+                const bool ok = kv[q] != 0xFFFFFFFFu;
+                const int aa = a[q] + (int)(kv[q] & 0xFFFFu);
+                pu[q] = ok ? g.col_in[aa] : (uint16_t)0xFFFFu;
+                pr[q] = ok ? g.r_in[aa] : 1.0;
+            }
+#pragma unroll
+            for (int q = 0; q < AT_ILP; q++) {
+                const int v = v0 + q * B;
+                if (v >= n) break;
+                if (v == s) { par[v] = (uint16_t)s; relv[v] = cs; }
+                else if (kv[q] == 0xFFFFFFFFu) { par[v] = 0xFFFFu; relv[v] = -1.0; }
+                else { par[v] = pu[q]; relv[v] = -pr[q]; }
             }
         }
         __syncthreads();
+        if (tid == 0 && g.dbg) g.dbg[(size_t)i * 8 + 1] = __builtin_amdgcn_s_memtime();
         // level-synchronous propagation down the tree (LDS only)
         for (;;) {
+            if (tid == 0 && g.dbg) g.dbg[(size_t)i * 8 + 5] += 1;
             if (tid == 0) *flag = 0;
             __syncthreads();
             int progressed = 0;
-            for (int v = tid; v < n; v += B) {
-                const double x = relv[v];
-                if (!signbit(x)) continue;
-                const uint16_t p = par[v];
-                if (p == 0xFFFFu) continue;
-                const double rp = relv[p];
-                if (!signbit(rp)) { relv[v] = rp * (-x); progressed = 1; }
+            for (int v0 = tid; v0 < n; v0 += B * AT_ILP) {
+                double x[AT_ILP], rp[AT_ILP];
+                uint16_t p[AT_ILP];
+#pragma unroll
+                for (int q = 0; q < AT_ILP; q++) {
+                    const int v = v0 + q * B;
+                    x[q] = v < n ? relv[v] : 0.0;
+                    p[q] = v < n ? par[v] : (uint16_t)0xFFFFu;
+                }
+#pragma unroll
+                for (int q = 0; q < AT_ILP; q++)
+                    rp[q] = (signbit(x[q]) && p[q] != 0xFFFFu) ? relv[p[q]] : -1.0;
+#pragma unroll
+                for (int q = 0; q < AT_ILP; q++)
+                    if (!signbit(rp[q])) { relv[v0 + q * B] = rp[q] * (-x[q]); progressed = 1; }
             }
             if (progressed) *flag = 1;
             __syncthreads();
@@ -89,31 +121,49 @@ __global__ __launch_bounds__(B) void path_attr_kernel(DevAttr g, const uint32_t*
         }
         if (tid == 0) *rmin = kInfBits;
         __syncthreads();
+        if (tid == 0 && g.dbg) g.dbg[(size_t)i * 8 + 2] = __builtin_amdgcn_s_memtime();
         double lmin = INFINITY;
         double* lrow = lat_out ? lat_out + (long long)i * ld : nullptr;
         double* rrow = rel_out ? rel_out + (long long)i * ld : nullptr;
-        for (int j = tid; j < nt; j += B) {
-            const int t = tgt[j];
-            double Lv, Rv;
-            if (t < 0 || t >= n) {
-                raise_err(err, SHD_ROUTE_EINVAL);
-                Lv = Rv = NAN;
-            } else if (t == s) {  // batch path [s]: one self-loop hop (topology.c:1471-1499)
-                const double w = g.self_w[s];
-                if (isnan(w)) { raise_err(err, SHD_ROUTE_ENOEDGE); Lv = Rv = NAN; }
-                else { Lv = 0.0 + w; Rv = cs * g.self_r[s]; }
-            } else {
-                const uint32_t kt = krow[t];
-                if (kt == 0xFFFFFFFFu) { raise_err(err, SHD_ROUTE_EUNREACH); Lv = Rv = NAN; }
-                else {
-                    Lv = (double)(kt >> 16);
-                    const double ft = g.vf[t];
-                    Rv = isnan(ft) ? relv[t] : relv[t] * ft;
-                }
+        for (int j0 = tid; j0 < nt; j0 += B * AT_ILP) {
+            int tq[AT_ILP];
+            uint32_t kt[AT_ILP];
+            double ft[AT_ILP];
+#pragma unroll
+            for (int q = 0; q < AT_ILP; q++) {
+                const int j = j0 + q * B;
+                tq[q] = j < nt ? tgt[j] : s;
             }
-            if (lrow) lrow[j] = Lv;
-            if (rrow) rrow[j] = Rv;
-            lmin = fmin(lmin, Lv);
+#pragma unroll
+            for (int q = 0; q < AT_ILP; q++) {
+                const bool ok = tq[q] >= 0 && tq[q] < n;
+                kt[q] = ok ? krow[tq[q]] : 0xFFFFFFFFu;
+                ft[q] = ok ? g.vf[tq[q]] : NAN;
+            }
+#pragma unroll
+            for (int q = 0; q < AT_ILP; q++) {
+                const int j = j0 + q * B;
+                if (j >= nt) break;
+                const int t = tq[q];
+                double Lv, Rv;
+                if (t < 0 || t >= n) {
+                    raise_err(err, SHD_ROUTE_EINVAL);
+                    Lv = Rv = NAN;
+                } else if (t == s) {  // batch path [s]: one self-loop hop (topology.c:1471-1499)
+                    const double w = g.self_w[s];
+                    if (isnan(w)) { raise_err(err, SHD_ROUTE_ENOEDGE); Lv = Rv = NAN; }
+                    else { Lv = 0.0 + w; Rv = cs * g.self_r[s]; }
+                } else if (kt[q] == 0xFFFFFFFFu) {
+                    raise_err(err, SHD_ROUTE_EUNREACH);
+                    Lv = Rv = NAN;
+                } else {
+                    Lv = (double)(kt[q] >> 16);
+                    Rv = isnan(ft[q]) ? relv[t] : relv[t] * ft[q];
+                }
+                if (lrow) lrow[j] = Lv;
+                if (rrow) rrow[j] = Rv;
+                lmin = fmin(lmin, Lv);
+            }
         }
         if (row_min) {
 #pragma unroll
@@ -123,6 +173,7 @@ __global__ __launch_bounds__(B) void path_attr_kernel(DevAttr g, const uint32_t*
             if (tid == 0) row_min[i] = as_d(*rmin);
         }
         __syncthreads();
+        if (tid == 0 && g.dbg) g.dbg[(size_t)i * 8 + 3] = __builtin_amdgcn_s_memtime();
     }
 }
 

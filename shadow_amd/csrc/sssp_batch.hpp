@@ -43,7 +43,15 @@ struct DevKB {
     const int* __restrict__ row_in;     // in-CSR offsets (n+1)
     const KBSeg* __restrict__ seg;
     const KBHub* __restrict__ hub;
+    unsigned long long* dbg;   // SHD_STAMPS builds: 8 words per workgroup
 };
+#ifdef SHD_STAMPS
+#define KB_STAMP(slot) do { if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + (slot)] += __builtin_amdgcn_s_memtime(); } while (0)
+#define KB_COUNT(slot) do { if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + (slot)] += 1; } while (0)
+#else
+#define KB_STAMP(slot) do { } while (0)
+#define KB_COUNT(slot) do { } while (0)
+#endif
 
 struct KBLayout {
     size_t arc, D, P, total;
@@ -99,6 +107,32 @@ __device__ inline u16x8 addsat8(const u16x8& a, us2 w) {
     return r;
 }
 
+__device__ inline us2 wsplat(uint32_t rec) {
+    const unsigned short w = (unsigned short)(rec & 0xFFFFu);
+    const us2 r = {w, w};
+    return r;
+}
+
+// min over arcs [a0, a1) of D[u] + w, four independent arc/distance reads in flight.
+__device__ inline u16x8 relax_row(const uint32_t* arc, const char* D, int a0, int a1) {
+    u16x8 acc = inf8();
+    int a = a0;
+    for (; a + 4 <= a1; a += 4) {
+        const uint32_t r0 = arc[a], r1 = arc[a + 1], r2 = arc[a + 2], r3 = arc[a + 3];
+        const u16x8 d0 = ld8(D + (size_t)16 * (r0 >> 16));
+        const u16x8 d1 = ld8(D + (size_t)16 * (r1 >> 16));
+        const u16x8 d2 = ld8(D + (size_t)16 * (r2 >> 16));
+        const u16x8 d3 = ld8(D + (size_t)16 * (r3 >> 16));
+        acc = min8(min8(acc, addsat8(d0, wsplat(r0))), addsat8(d1, wsplat(r1)));
+        acc = min8(min8(acc, addsat8(d2, wsplat(r2))), addsat8(d3, wsplat(r3)));
+    }
+    for (; a < a1; a++) {
+        const uint32_t r0 = arc[a];
+        acc = min8(acc, addsat8(ld8(D + (size_t)16 * (r0 >> 16)), wsplat(r0)));
+    }
+    return acc;
+}
+
 __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int* __restrict__ src, int ns,
                                                               uint32_t* __restrict__ keys, long long kld,
                                                               int* __restrict__ err) {
@@ -112,6 +146,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
     const int tid = threadIdx.x;
     const int n = g.n;
 
+    if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memtime();
     // stage the in-CSR into LDS once per workgroup (16-byte loads)
     {
         const int nq = (g.nnz + 3) / 4;
@@ -142,19 +177,16 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
         }
         __syncthreads();
 
+        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memtime();
         // ---- Gauss-Seidel pull sweeps to the fixed point -------------------------
         for (;;) {
+            KB_COUNT(4);
             if (tid == 0) *changed = 0;
             __syncthreads();
             int ch = 0;
             for (int k = tid; k < g.nseg; k += KB_BLOCK) {
                 const KBSeg sg = g.seg[k];
-                u16x8 acc = inf8();
-                for (int a = sg.a0; a < sg.a1; a++) {
-                    const uint32_t rec = arc[a];
-                    const us2 w = {(unsigned short)(rec & 0xFFFFu), (unsigned short)(rec & 0xFFFFu)};
-                    acc = min8(acc, addsat8(ld8(D + (size_t)16 * (rec >> 16)), w));
-                }
+                const u16x8 acc = relax_row(arc, D, sg.a0, sg.a1);
                 if (sg.p < 0) {
                     const u16x8 old = ld8(D + (size_t)16 * sg.v);
                     const u16x8 nw = min8(old, acc);
@@ -178,6 +210,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
             if (!again) break;
         }
 
+        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memtime();
         // ---- parents: first tight arc of each in-row, per source -----------------
         for (int k = tid; k < g.nseg; k += KB_BLOCK) {
             const KBSeg sg = g.seg[k];
@@ -186,14 +219,21 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
 #pragma unroll
             for (int b = 0; b < KB_SRC; b++) slot[b] = 0xFFFFu;
             const int r0 = g.row_in[sg.v];
-            for (int a = sg.a0; a < sg.a1; a++) {
-                const uint32_t rec = arc[a];
-                const us2 w = {(unsigned short)(rec & 0xFFFFu), (unsigned short)(rec & 0xFFFFu)};
-                const u16x8 c = addsat8(ld8(D + (size_t)16 * (rec >> 16)), w);
+            for (int a = sg.a0; a < sg.a1; a += 4) {
+                u16x8 c[4];
 #pragma unroll
-                for (int b = 0; b < KB_SRC; b++) {
-                    const unsigned short cb = c.h[b >> 1][b & 1], db = dv.h[b >> 1][b & 1];
-                    if (slot[b] == 0xFFFFu && db != 0xFFFFu && cb == db) slot[b] = (unsigned short)(a - r0);
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t rec = arc[min(a + q, sg.a1 - 1)];
+                    c[q] = addsat8(ld8(D + (size_t)16 * (rec >> 16)), wsplat(rec));
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (a + q >= sg.a1) break;
+#pragma unroll
+                    for (int b = 0; b < KB_SRC; b++) {
+                        const unsigned short cb = c[q].h[b >> 1][b & 1], db = dv.h[b >> 1][b & 1];
+                        if (slot[b] == 0xFFFFu && db != 0xFFFFu && cb == db) slot[b] = (unsigned short)(a + q - r0);
+                    }
                 }
             }
             if (sg.p < 0) {
@@ -232,6 +272,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
             }
         }
         __syncthreads();
+        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memtime();
     }
 }
 

@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc passes (tools/pmc_run.sh) into per-launch HBM bytes for the
+hot-path kernels, with the gfx950 corrections of MI355X_MICROARCH.md (HBM section):
+FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE counts half the bytes of a wide
+streaming read, so it is doubled.  Writes profiles/<round>_pmc_<cfg>.json for bench.py."""
+import collections
+import csv
+import json
+import os
+import sys
+
+HOT = ("sssp_batch_kernel", "path_attr_kernel", "sssp_k32_kernel", "sssp_rows_kernel", "sssp_k16")
+
+
+def load(path):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return agg
+
+
+def main(src_dir, out, cfg, sources):
+    fetch = load(os.path.join(src_dir, "fetch_counter_collection.csv"))
+    write = load(os.path.join(src_dir, "write_counter_collection.csv"))
+    per = {}
+    for k in set(fetch) | set(write):
+        if not any(h in k for h in HOT):
+            continue
+        f = fetch.get(k, {}).get("FETCH_SIZE", [0.0])
+        w = write.get(k, {}).get("WRITE_SIZE", [0.0])
+        name = k.split("(")[0].replace("void ", "")
+        per[name] = {"fetch_bytes": 2.0 * 1024 * sum(f) / len(f), "write_bytes": 1024 * sum(w) / len(w)}
+    tot = sum(v["fetch_bytes"] + v["write_bytes"] for v in per.values())
+    res = {"config": cfg, "sources_per_launch": sources, "hbm_bytes_per_launch": tot, "kernels": per,
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
+                     "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction)"}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]))

@@ -31,14 +31,28 @@ d_tgt = torch.from_numpy(T.astype(np.int32)).to(dev)
 lat = torch.empty((len(S), len(T)), dtype=torch.float64, device=dev)
 rel = torch.empty_like(lat)
 mn = torch.empty(len(S), dtype=torch.float64, device=dev)
-dbg = torch.zeros((len(S), 8), dtype=torch.int64, device=dev)
+nwg = (len(S) + 7) // 8
+dbg = torch.zeros((len(S) + nwg, 8), dtype=torch.int64, device=dev)
 L.shd_route_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
 L.shd_route_debug_buffer(eng._h, C.c_void_p(dbg.data_ptr()))
 for rep in range(3):
     dbg.zero_()
     eng.rows_async(d_src, d_tgt, lat, rel, mn)
     eng.sync()
-d = dbg.cpu().numpy().astype(np.int64)
+d_all = dbg.cpu().numpy().astype(np.int64)
+d = d_all[: len(S)]
+if eng.info["kernel"] == 2:
+    kb = d_all[len(S):]
+    print(f"config {a.config} n={g.n} nnz={g.nnz} sources={len(S)} kernel=KB+K2")
+    print(f"  KB stage   mean {np.mean(kb[:,1]-kb[:,0]):10.0f} cyc")
+    print(f"  KB sweeps  mean {np.mean(kb[:,2]-kb[:,1]):10.0f} cyc  max {np.max(kb[:,2]-kb[:,1])}  rounds mean {kb[:,4].mean():.1f} max {kb[:,4].max():.0f}")
+    print(f"  KB parents mean {np.mean(kb[:,3]-kb[:,2]):10.0f} cyc")
+    print(f"  K2 phaseB  mean {np.mean(d[:,1]-d[:,0]):10.0f} cyc")
+    print(f"  K2 sweeps  mean {np.mean(d[:,2]-d[:,1]):10.0f} cyc  sweeps mean {d[:,5].mean():.1f}")
+    print(f"  K2 output  mean {np.mean(d[:,3]-d[:,2]):10.0f} cyc")
+    t0 = d[:, 0] - d[:, 0].min()
+    print(f"  K2 start spread p50 {np.median(t0):.0f} max {t0.max()}")
+    sys.exit(0)
 ph = np.diff(d[:, :5], axis=1)
 names = ["A_bf", "B_parent", "C_rel", "D_out"]
 print(f"config {a.config} n={g.n} nnz={g.nnz} sources={len(S)} kernel={eng.info['kernel']} block={eng.info['block']}")

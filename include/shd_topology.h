@@ -1,0 +1,82 @@
+/*
+ * shd_topology.h -- C front end with the semantics of Shadow 1.14's
+ * src/main/routing/topology.c (mckerrigan/shadow), keyed by vertex index.
+ *
+ * Shadow's own topology.c keeps its public API (topology.h:17-28) and its
+ * Address->vertex map (virtualIP, topology.c:1388-1405); each public function then
+ * becomes a one-line call into this module.  Behind it:
+ *   - graphml loading with igraph_read_graph_graphml numbering (document order,
+ *     missing numeric attribute = NaN) and the validation of topology.c:565-1185;
+ *   - the Path cache as dense upper-triangle arrays over the attached vertices,
+ *     filled eagerly (ascending sources, first writer wins over both directions,
+ *     topology.c:1307-1336) by the HIP engine (include/shd_route.h) on the first
+ *     cache miss, optionally sharded over several GPUs;
+ *   - minimumPathLatency and the runahead it implies (topology.c:1374-1385,
+ *     master.c:148-159).
+ * Functions returning int use SHD_ROUTE_* codes; getters return -1 on error like
+ * topology_getLatency / topology_getReliability (topology.c:2065-2087).
+ */
+#ifndef SHD_TOPOLOGY_H
+#define SHD_TOPOLOGY_H
+
+#include <stdint.h>
+#include <stdio.h>
+
+#include "shd_route.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct shd_topology shd_topology_t;
+
+/* graphml -> igraph-numbered arrays (plain or .xz/.gz file).  On success the caller
+ * owns *out (release with shd_graphml_free). Validation as topology.c:565-1185;
+ * returns SHD_ROUTE_EINVAL with a message in errbuf on failure. */
+typedef struct shd_graphml {
+    shd_graph_t graph;         /* arrays owned by this struct */
+    char** vertex_ids;         /* graphml node id of each vertex */
+    double* bandwidth_down;    /* vertex attributes Shadow reads at attach time */
+    double* bandwidth_up;
+    int32_t has_vertex_packetloss;
+} shd_graphml_t;
+int shd_graphml_load(const char* path, shd_graphml_t* out, char* errbuf, size_t errlen);
+void shd_graphml_free(shd_graphml_t* g);
+
+/* topology_new (topology.c:2486-2510): load, validate, make one engine context per
+ * device in `devices` (NULL/0 -> device 0).  NULL on failure. */
+shd_topology_t* shd_topology_new(const char* graph_path, const int* devices, int ndev);
+shd_topology_t* shd_topology_new_from_graph(const shd_graph_t* g, const int* devices, int ndev);
+void shd_topology_free(shd_topology_t* top);  /* topology_free (topology.c:2441) */
+
+int32_t shd_topology_vertex_count(const shd_topology_t* top);
+int32_t shd_topology_find_vertex(const shd_topology_t* top, const char* graphml_id);
+
+/* topology_attach's effect on routing (topology.c:2371-2439): the vertex joins
+ * verticesWithAttachedHosts; detach never shrinks it (topology.c:2437). */
+int shd_topology_attach_vertex(shd_topology_t* top, int32_t vertex);
+int32_t shd_topology_attached_count(const shd_topology_t* top);
+
+/* Public accessors (topology.c:2053-2092); fill the cache on the first miss. */
+double shd_topology_get_latency(shd_topology_t* top, int32_t src, int32_t dst);
+double shd_topology_get_reliability(shd_topology_t* top, int32_t src, int32_t dst);
+int shd_topology_is_routable(shd_topology_t* top, int32_t src, int32_t dst);
+void shd_topology_increment_path_packet_counter(shd_topology_t* top, int32_t src, int32_t dst);
+uint64_t shd_topology_get_path_packet_count(shd_topology_t* top, int32_t src, int32_t dst);
+int shd_topology_is_direct_path(shd_topology_t* top, int32_t src, int32_t dst);
+
+/* minimumPathLatency over all cached Paths and the runahead it sets (ns). */
+double shd_topology_min_path_latency(shd_topology_t* top);
+uint64_t shd_topology_runahead_ns(shd_topology_t* top);
+
+/* Explicit eager fill (otherwise done by the first accessor); seconds spent in
+ * *elapsed_s (nullable), like shortestPathTotalTime (topology.c:1751-1788). */
+int shd_topology_fill(shd_topology_t* top, double* elapsed_s);
+
+/* _topology_logAllCachedPaths (topology.c:1929-1967): one line per cached Path. */
+int shd_topology_dump_paths(shd_topology_t* top, FILE* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHD_TOPOLOGY_H */

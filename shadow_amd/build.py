@@ -17,6 +17,22 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-f
          "-Wall", "-Wno-unused-result"]
 
 
+FRONT_SOURCES = [os.path.join(HERE, "csrc", "graphml.c"), os.path.join(HERE, "csrc", "topology_front.c")]
+FRONT_OUT = os.path.join(HERE, "libshd_topology.so")
+CC = os.environ.get("CC", "gcc")
+
+
+def build_front(verbose: bool = False) -> str:
+    """C front end (topology.c semantics + graphml loader), linked against the engine."""
+    cmd = [CC, "-O2", "-std=gnu11", "-fPIC", "-shared", "-Wall", "-I/usr/include/libxml2",
+           "-o", FRONT_OUT, *FRONT_SOURCES, "-L" + HERE, "-lshd_route", "-lxml2", "-lpthread", "-lm",
+           "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return FRONT_OUT
+
+
 def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
@@ -41,6 +57,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
+    front_deps = FRONT_SOURCES + [os.path.join(ROOT, "include", "shd_topology.h"), OUT]
+    if force or not os.path.exists(FRONT_OUT) or any(os.path.getmtime(p) > os.path.getmtime(FRONT_OUT)
+                                                     for p in front_deps):
+        build_front(verbose)
     return OUT
 
 

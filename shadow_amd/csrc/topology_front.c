@@ -1,0 +1,403 @@
+/*
+ * topology_front.c -- the Path cache and public accessors of Shadow 1.14's
+ * src/main/routing/topology.c, rebuilt over the HIP routing engine (shd_route.h).
+ *
+ * Reference behaviour kept (file:line in mckerrigan/shadow):
+ *   - one Path per unordered pair, first writer wins over both directions
+ *     (_topology_shouldStorePath, topology.c:1307-1336); lookups probe (s,d) then
+ *     (d,s) (topology.c:1987-1990, 2033-2037).  With the fill running over attached
+ *     sources in ascending order, the stored orientation of {s,t} is from min(s,t),
+ *     so the cache is one upper triangle over the attached vertices.
+ *   - dispatch complete / prefer-direct+adjacent -> direct path, else source paths
+ *     (topology.c:2019-2031), self entry = batch self-loop hop;
+ *   - minimumPathLatency over every stored Path (topology.c:1374-1385) and the
+ *     runahead it implies, truncated to whole ms (master.c:148-159, 10 ms default);
+ *   - -1 from the getters when a vertex has no attached host (topology.c:1973-1985);
+ *   - verticesWithAttachedHosts never shrinks on detach (topology.c:2437).
+ * What changes: the cache is dense (|A|(|A|+1)/2 latency + reliability doubles
+ * instead of a glib hash of 48-byte Paths), it is filled eagerly at the first miss
+ * by batched GPU rows (instead of one serialised igraph Dijkstra per missing source,
+ * topology.c:1747-1781), and the fill can shard sources over several GPUs.
+ */
+#define _GNU_SOURCE
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "../../include/shd_topology.h"
+
+typedef struct {
+    uint64_t* keys;  /* (i << 32 | j) + 1, 0 = empty */
+    uint64_t* vals;
+    size_t cap, len;
+} pcmap;
+
+struct shd_topology {
+    shd_graphml_t gml;   /* owns the arrays when loaded from a file */
+    shd_graph_t g;       /* view used by the engine */
+    int owns_copy;       /* arrays copied by shd_topology_new_from_graph */
+    int ndev;
+    shd_route_t** eng;
+    int32_t n;
+    int complete, directed, prefer_direct;
+    /* host adjacency for the prefer-direct isDirect flags */
+    int32_t* arow;
+    int32_t* acol;
+    /* attached set */
+    uint8_t* attached;
+    int32_t nattached;
+    /* dense cache over A (sorted attached vertices), upper triangle incl. diagonal */
+    int32_t na;
+    int32_t* A;
+    int32_t* cid;
+    double* lat;
+    double* rel;
+    int filled;
+    double min_lat;
+    double fill_seconds;
+    pthread_mutex_t lock;
+    pcmap pc;
+    pthread_mutex_t pclock;
+};
+
+static inline size_t tri(int32_t na, int32_t i, int32_t j) { /* i <= j */
+    return (size_t)i * (size_t)na - ((size_t)i * (size_t)(i - 1)) / 2 + (size_t)(j - i);
+}
+
+static int cmp_i32(const void* a, const void* b) {
+    int32_t x = *(const int32_t*)a, y = *(const int32_t*)b;
+    return (x > y) - (x < y);
+}
+
+static void build_adjacency(shd_topology_t* t) {
+    const shd_graph_t* g = &t->g;
+    int32_t n = g->n_vertices;
+    t->arow = calloc((size_t)n + 1, sizeof(int32_t));
+    for (int32_t e = 0; e < g->n_edges; e++) {
+        t->arow[g->edge_src[e] + 1]++;
+        if (!g->directed && g->edge_src[e] != g->edge_dst[e]) t->arow[g->edge_dst[e] + 1]++;
+    }
+    for (int32_t v = 0; v < n; v++) t->arow[v + 1] += t->arow[v];
+    t->acol = malloc(sizeof(int32_t) * ((size_t)t->arow[n] + 1));
+    int32_t* fill = malloc(sizeof(int32_t) * ((size_t)n + 1));
+    memcpy(fill, t->arow, sizeof(int32_t) * (size_t)n);
+    for (int32_t e = 0; e < g->n_edges; e++) {
+        int32_t a = g->edge_src[e], b = g->edge_dst[e];
+        t->acol[fill[a]++] = b;
+        if (!g->directed && a != b) t->acol[fill[b]++] = a;
+    }
+    free(fill);
+    for (int32_t v = 0; v < n; v++) qsort(t->acol + t->arow[v], (size_t)(t->arow[v + 1] - t->arow[v]), sizeof(int32_t), cmp_i32);
+}
+
+/* _topology_verticesAreAdjacent (topology.c:1248-1264) via get_eid semantics */
+static int adjacent(const shd_topology_t* t, int32_t s, int32_t d) {
+    int32_t lo = t->arow[s], hi = t->arow[s + 1];
+    while (lo < hi) {
+        int32_t mid = (lo + hi) / 2;
+        if (t->acol[mid] < d) lo = mid + 1;
+        else if (t->acol[mid] > d) hi = mid;
+        else return 1;
+    }
+    return 0;
+}
+
+static shd_topology_t* finish_new(shd_topology_t* t, const int* devices, int ndev) {
+    t->n = t->g.n_vertices;
+    t->ndev = ndev > 0 ? ndev : 1;
+    t->eng = calloc((size_t)t->ndev, sizeof(shd_route_t*));
+    for (int d = 0; d < t->ndev; d++) {
+        int dev = (devices && ndev > 0) ? devices[d] : 0;
+        if (shd_route_create(&t->eng[d], &t->g, dev) != SHD_ROUTE_OK) {
+            shd_topology_free(t);
+            return NULL;
+        }
+    }
+    shd_route_info_t info;
+    shd_route_get_info(t->eng[0], &info);
+    t->complete = info.is_complete;
+    t->directed = info.directed;
+    t->prefer_direct = info.prefer_direct;
+    t->attached = calloc((size_t)t->n, 1);
+    t->cid = malloc(sizeof(int32_t) * (size_t)t->n);
+    for (int32_t v = 0; v < t->n; v++) t->cid[v] = -1;
+    build_adjacency(t);
+    pthread_mutex_init(&t->lock, NULL);
+    pthread_mutex_init(&t->pclock, NULL);
+    return t;
+}
+
+shd_topology_t* shd_topology_new(const char* graph_path, const int* devices, int ndev) {
+    shd_topology_t* t = calloc(1, sizeof(*t));
+    char err[512];
+    if (shd_graphml_load(graph_path, &t->gml, err, sizeof(err)) != SHD_ROUTE_OK) {
+        fprintf(stderr, "shd_topology_new: %s\n", err);
+        free(t);
+        return NULL;
+    }
+    t->g = t->gml.graph;
+    return finish_new(t, devices, ndev);
+}
+
+shd_topology_t* shd_topology_new_from_graph(const shd_graph_t* g, const int* devices, int ndev) {
+    if (!g || g->n_vertices <= 0) return NULL;
+    shd_topology_t* t = calloc(1, sizeof(*t));
+    t->owns_copy = 1;
+    t->g = *g;
+    size_t m = (size_t)g->n_edges, n = (size_t)g->n_vertices;
+    int32_t* s = malloc(sizeof(int32_t) * (m + 1));
+    int32_t* d = malloc(sizeof(int32_t) * (m + 1));
+    double* l = malloc(sizeof(double) * (m + 1));
+    double* p = malloc(sizeof(double) * (m + 1));
+    memcpy(s, g->edge_src, sizeof(int32_t) * m); memcpy(d, g->edge_dst, sizeof(int32_t) * m);
+    memcpy(l, g->edge_latency, sizeof(double) * m); memcpy(p, g->edge_packetloss, sizeof(double) * m);
+    t->g.edge_src = s; t->g.edge_dst = d; t->g.edge_latency = l; t->g.edge_packetloss = p;
+    if (g->vertex_packetloss) {
+        double* vl = malloc(sizeof(double) * n);
+        memcpy(vl, g->vertex_packetloss, sizeof(double) * n);
+        t->g.vertex_packetloss = vl;
+    }
+    return finish_new(t, devices, ndev);
+}
+
+void shd_topology_free(shd_topology_t* t) {
+    if (!t) return;
+    if (t->eng) for (int d = 0; d < t->ndev; d++) if (t->eng[d]) shd_route_destroy(t->eng[d]);
+    free(t->eng);
+    if (t->owns_copy) {
+        free((void*)t->g.edge_src); free((void*)t->g.edge_dst); free((void*)t->g.edge_latency);
+        free((void*)t->g.edge_packetloss); free((void*)t->g.vertex_packetloss);
+    }
+    shd_graphml_free(&t->gml);
+    free(t->arow); free(t->acol); free(t->attached); free(t->A); free(t->cid);
+    free(t->lat); free(t->rel);
+    free(t->pc.keys); free(t->pc.vals);
+    free(t);
+}
+
+int32_t shd_topology_vertex_count(const shd_topology_t* t) { return t ? t->n : -1; }
+
+int32_t shd_topology_find_vertex(const shd_topology_t* t, const char* id) {
+    if (!t || !id || !t->gml.vertex_ids) return -1;
+    for (int32_t v = 0; v < t->n; v++)
+        if (!strcmp(t->gml.vertex_ids[v], id)) return v;
+    return -1;
+}
+
+int shd_topology_attach_vertex(shd_topology_t* t, int32_t v) {
+    if (!t || v < 0 || v >= t->n) return SHD_ROUTE_EINVAL;
+    pthread_mutex_lock(&t->lock);
+    if (!t->attached[v]) {
+        t->attached[v] = 1;
+        t->nattached++;
+        t->filled = 0;  /* the next lookup refills over the grown attached set */
+    }
+    pthread_mutex_unlock(&t->lock);
+    return SHD_ROUTE_OK;
+}
+
+int32_t shd_topology_attached_count(const shd_topology_t* t) { return t ? t->nattached : -1; }
+
+typedef struct {
+    shd_topology_t* t;
+    int dev;
+    int rc;
+} fill_job;
+
+/* Row chunks are dealt round-robin over the devices; chunk c covers sources
+ * A[c*R, (c+1)*R) and targets A[c*R, na) (the upper triangle it stores). */
+#define FILL_ROWS 256
+
+static void* fill_worker(void* arg) {
+    fill_job* job = arg;
+    shd_topology_t* t = job->t;
+    const int32_t na = t->na;
+    double* lbuf = malloc(sizeof(double) * (size_t)FILL_ROWS * (size_t)na);
+    double* rbuf = malloc(sizeof(double) * (size_t)FILL_ROWS * (size_t)na);
+    if (!lbuf || !rbuf) { job->rc = SHD_ROUTE_ENOMEM; free(lbuf); free(rbuf); return NULL; }
+    const int32_t nchunks = (na + FILL_ROWS - 1) / FILL_ROWS;
+    for (int32_t c = job->dev; c < nchunks && !job->rc; c += t->ndev) {
+        const int32_t i0 = c * FILL_ROWS;
+        const int32_t rows = (na - i0) < FILL_ROWS ? (na - i0) : FILL_ROWS;
+        const int32_t nt = na - i0;
+        int rc = shd_route_rows(t->eng[job->dev], t->A + i0, rows, t->A + i0, nt, SHD_ROUTE_DISPATCH,
+                                lbuf, rbuf, NULL);
+        if (rc) { job->rc = rc; break; }
+        for (int32_t r = 0; r < rows; r++) {
+            const int32_t i = i0 + r;
+            const size_t base = tri(na, i, i);
+            /* row i stores targets j >= i: offsets (j - i0) in the returned row */
+            memcpy(t->lat + base, lbuf + (size_t)r * nt + r, sizeof(double) * (size_t)(na - i));
+            memcpy(t->rel + base, rbuf + (size_t)r * nt + r, sizeof(double) * (size_t)(na - i));
+        }
+    }
+    free(lbuf); free(rbuf);
+    return NULL;
+}
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static int fill_locked(shd_topology_t* t) {
+    if (t->filled) return SHD_ROUTE_OK;
+    const double t0 = now_s();
+    free(t->A); free(t->lat); free(t->rel);
+    t->A = NULL; t->lat = t->rel = NULL;
+    t->na = 0;
+    t->A = malloc(sizeof(int32_t) * ((size_t)t->nattached + 1));
+    for (int32_t v = 0; v < t->n; v++) {
+        t->cid[v] = -1;
+        if (t->attached[v]) { t->cid[v] = t->na; t->A[t->na++] = v; }
+    }
+    const size_t ntri = (size_t)t->na * ((size_t)t->na + 1) / 2;
+    t->lat = malloc(sizeof(double) * (ntri ? ntri : 1));
+    t->rel = malloc(sizeof(double) * (ntri ? ntri : 1));
+    if (!t->lat || !t->rel) return SHD_ROUTE_ENOMEM;
+    int rc = SHD_ROUTE_OK;
+    if (t->na) {
+        pthread_t th[64];
+        fill_job jobs[64];
+        const int nd = t->ndev < 64 ? t->ndev : 64;
+        for (int d = 0; d < nd; d++) {
+            jobs[d].t = t; jobs[d].dev = d; jobs[d].rc = 0;
+            pthread_create(&th[d], NULL, fill_worker, &jobs[d]);
+        }
+        for (int d = 0; d < nd; d++) {
+            pthread_join(th[d], NULL);
+            if (jobs[d].rc && !rc) rc = jobs[d].rc;
+        }
+    }
+    if (rc) return rc;
+    double mn = 0;
+    for (size_t k = 0; k < ntri; k++)  /* topology.c:1375: minLat == 0 means unset */
+        if (mn == 0 || t->lat[k] < mn) mn = t->lat[k];
+    t->min_lat = mn;
+    t->fill_seconds += now_s() - t0;
+    __atomic_store_n(&t->filled, 1, __ATOMIC_RELEASE);
+    return SHD_ROUTE_OK;
+}
+
+int shd_topology_fill(shd_topology_t* t, double* elapsed_s) {
+    if (!t) return SHD_ROUTE_EINVAL;
+    pthread_mutex_lock(&t->lock);
+    int rc = fill_locked(t);
+    pthread_mutex_unlock(&t->lock);
+    if (elapsed_s) *elapsed_s = t->fill_seconds;
+    return rc;
+}
+
+/* _topology_getPathEntry (topology.c:1969-2051) -> index into the triangle, or -1 */
+static int64_t entry(shd_topology_t* t, int32_t s, int32_t d) {
+    if (!t || s < 0 || d < 0 || s >= t->n || d >= t->n) return -1;
+    if (!__atomic_load_n(&t->filled, __ATOMIC_ACQUIRE)) {
+        pthread_mutex_lock(&t->lock);
+        int rc = fill_locked(t);
+        pthread_mutex_unlock(&t->lock);
+        if (rc) return -1;
+    }
+    const int32_t i = t->cid[s], j = t->cid[d];
+    if (i < 0 || j < 0) return -1;  /* address not connected to the topology */
+    return (int64_t)(i <= j ? tri(t->na, i, j) : tri(t->na, j, i));
+}
+
+double shd_topology_get_latency(shd_topology_t* t, int32_t s, int32_t d) {
+    int64_t k = entry(t, s, d);
+    return k < 0 ? -1.0 : t->lat[k];
+}
+
+double shd_topology_get_reliability(shd_topology_t* t, int32_t s, int32_t d) {
+    int64_t k = entry(t, s, d);
+    return k < 0 ? -1.0 : t->rel[k];
+}
+
+int shd_topology_is_routable(shd_topology_t* t, int32_t s, int32_t d) {
+    return shd_topology_get_latency(t, s, d) > -1;  /* topology.c:2089-2092 */
+}
+
+int shd_topology_is_direct_path(shd_topology_t* t, int32_t s, int32_t d) {
+    if (entry(t, s, d) < 0) return -1;
+    const int32_t a = s < d ? s : d, b = s < d ? d : s;  /* stored orientation: min -> max */
+    return t->complete || (t->prefer_direct && adjacent(t, a, b));
+}
+
+static uint64_t* pc_slot(pcmap* m, uint64_t key) {
+    if (m->len * 2 + 2 > m->cap) {
+        size_t nc = m->cap ? m->cap * 2 : 4096;
+        uint64_t* nk = calloc(nc, sizeof(uint64_t));
+        uint64_t* nv = calloc(nc, sizeof(uint64_t));
+        for (size_t i = 0; i < m->cap; i++)
+            if (m->keys[i]) {
+                size_t j = (m->keys[i] * 0x9E3779B97F4A7C15ull) & (nc - 1);
+                while (nk[j]) j = (j + 1) & (nc - 1);
+                nk[j] = m->keys[i]; nv[j] = m->vals[i];
+            }
+        free(m->keys); free(m->vals);
+        m->keys = nk; m->vals = nv; m->cap = nc;
+    }
+    size_t j = (key * 0x9E3779B97F4A7C15ull) & (m->cap - 1);
+    while (m->keys[j] && m->keys[j] != key) j = (j + 1) & (m->cap - 1);
+    if (!m->keys[j]) { m->keys[j] = key; m->len++; }
+    return &m->vals[j];
+}
+
+void shd_topology_increment_path_packet_counter(shd_topology_t* t, int32_t s, int32_t d) {
+    int64_t k = entry(t, s, d);
+    if (k < 0) return;
+    pthread_mutex_lock(&t->pclock);
+    (*pc_slot(&t->pc, (uint64_t)k + 1))++;
+    pthread_mutex_unlock(&t->pclock);
+}
+
+uint64_t shd_topology_get_path_packet_count(shd_topology_t* t, int32_t s, int32_t d) {
+    int64_t k = entry(t, s, d);
+    if (k < 0) return 0;
+    pthread_mutex_lock(&t->pclock);
+    uint64_t v = *pc_slot(&t->pc, (uint64_t)k + 1);
+    pthread_mutex_unlock(&t->pclock);
+    return v;
+}
+
+double shd_topology_min_path_latency(shd_topology_t* t) {
+    if (!t) return -1;
+    if (shd_topology_fill(t, NULL) != SHD_ROUTE_OK) return -1;
+    return t->min_lat;
+}
+
+uint64_t shd_topology_runahead_ns(shd_topology_t* t) {
+    double m = shd_topology_min_path_latency(t);
+    uint64_t ns = m > 0 ? ((uint64_t)m) * 1000000ull : 0;  /* master.c:153 */
+    return ns > 0 ? ns : 10ull * 1000000ull;              /* master.c:138 */
+}
+
+int shd_topology_dump_paths(shd_topology_t* t, FILE* out) {
+    if (!t || !out) return SHD_ROUTE_EINVAL;
+    int rc = shd_topology_fill(t, NULL);
+    if (rc) return rc;
+    for (int32_t i = 0; i < t->na; i++)
+        for (int32_t j = i; j < t->na; j++) {
+            const size_t k = tri(t->na, i, j);
+            const int32_t a = t->A[i], b = t->A[j];
+            const char* ia = t->gml.vertex_ids ? t->gml.vertex_ids[a] : NULL;
+            const char* ib = t->gml.vertex_ids ? t->gml.vertex_ids[b] : NULL;
+            char na_[32], nb_[32];
+            if (!ia) { snprintf(na_, sizeof na_, "%d", a); ia = na_; }
+            if (!ib) { snprintf(nb_, sizeof nb_, "%d", b); ib = nb_; }
+            uint64_t pc = 0;
+            pthread_mutex_lock(&t->pclock);
+            if (t->pc.cap) pc = *pc_slot(&t->pc, (uint64_t)k + 1);
+            pthread_mutex_unlock(&t->pclock);
+            /* path_toString (path.c:62-74) inside _topology_logAllCachedPathsHelper2 */
+            fprintf(out, "Found path %s%s%s in cache: SourceIndex=%d DestinationIndex=%d Latency=%f "
+                         "Reliability=%f PacketCount=%llu isDirect=%s\n",
+                    ia, t->directed ? "->" : "<->", ib, a, b, t->lat[k], t->rel[k], (unsigned long long)pc,
+                    (t->complete || (t->prefer_direct && adjacent(t, a, b))) ? "True" : "False");
+        }
+    return SHD_ROUTE_OK;
+}

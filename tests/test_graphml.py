@@ -1,0 +1,112 @@
+"""CPU: the C graphml loader (igraph numbering, NaN-absent, topology.c validation)."""
+import lzma
+import math
+import os
+
+import numpy as np
+import pytest
+
+from shadow_amd.graph import Graph, internet_like, to_graphml
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def topo():
+    from shadow_amd import build, topology
+    build.build()
+    topology.load_library()
+    return topology
+
+
+def _bundled():
+    z = np.load(os.path.join(HERE, "golden", "bundled_topology.npz"))
+    return Graph(n=int(z["n"]), src=z["src"], dst=z["dst"], latency=z["latency"], packetloss=z["packetloss"],
+                 vertex_packetloss=z["vertex_packetloss"], directed=bool(z["directed"]), ids=list(z["ids"]))
+
+
+def test_roundtrip_xz_bundled(topo, tmp_path):
+    g = _bundled()
+    p = tmp_path / "topology.graphml.xml"
+    to_graphml(g, str(p))
+    pxz = tmp_path / "topology.graphml.xml.xz"
+    pxz.write_bytes(lzma.compress(p.read_bytes()))
+    h = topo.load_graphml(str(pxz))
+    assert h.n == 183 and h.m == 16836 and not h.directed
+    assert np.array_equal(h.src, g.src) and np.array_equal(h.dst, g.dst)
+    assert np.array_equal(h.latency, g.latency) and np.array_equal(h.packetloss, g.packetloss)
+    assert np.array_equal(h.vertex_packetloss, g.vertex_packetloss)
+    assert h.ids == g.ids
+
+
+def test_reference_style_config_topology(topo, tmp_path):
+    # the embedded graph of src/test/tcp/tcp-blocking-lossy.test.shadow.config.xml (no vertex packetloss key)
+    txt = """<graphml xmlns="http://graphml.graphdrawing.org/xmlns">
+  <key attr.name="packetloss" attr.type="double" for="edge" id="d4" />
+  <key attr.name="latency" attr.type="double" for="edge" id="d3" />
+  <key attr.name="bandwidthup" attr.type="int" for="node" id="d2" />
+  <key attr.name="bandwidthdown" attr.type="int" for="node" id="d1" />
+  <key attr.name="countrycode" attr.type="string" for="node" id="d0" />
+  <graph edgedefault="undirected">
+    <node id="poi-1"><data key="d0">US</data><data key="d1">10240</data><data key="d2">10240</data></node>
+    <edge source="poi-1" target="poi-1"><data key="d3">50.0</data><data key="d4">0.25</data></edge>
+  </graph>
+</graphml>"""
+    p = tmp_path / "t.xml"
+    p.write_text(txt)
+    g = topo.load_graphml(str(p))
+    assert g.n == 1 and g.m == 1 and g.vertex_packetloss is None
+    assert g.latency[0] == 50.0 and g.packetloss[0] == 0.25 and g.ids == ["poi-1"]
+
+
+def _write(tmp_path, body, keys=None):
+    keys = keys or """<key attr.name="packetloss" attr.type="double" for="edge" id="el" />
+  <key attr.name="latency" attr.type="double" for="edge" id="lt" />
+  <key attr.name="bandwidthup" attr.type="int" for="node" id="bu" />
+  <key attr.name="bandwidthdown" attr.type="int" for="node" id="bd" />
+  <key attr.name="packetloss" attr.type="double" for="node" id="vl" />"""
+    p = tmp_path / "g.xml"
+    p.write_text(f'<graphml xmlns="http://graphml.graphdrawing.org/xmlns">{keys}<graph edgedefault="undirected">{body}</graph></graphml>')
+    return str(p)
+
+
+N = '<node id="{0}"><data key="bd">1</data><data key="bu">1</data>{1}</node>'
+
+
+def test_missing_vertex_loss_is_nan_and_order(topo, tmp_path):
+    body = N.format("b", '<data key="vl">0.1</data>') + N.format("a", "") + \
+        '<edge source="a" target="b"><data key="lt">3</data><data key="el">0</data></edge>'
+    g = topo.load_graphml(_write(tmp_path, body))
+    assert g.ids == ["b", "a"] and g.src.tolist() == [1] and g.dst.tolist() == [0]
+    assert g.vertex_packetloss[0] == pytest.approx(0.1) and math.isnan(g.vertex_packetloss[1])
+
+
+@pytest.mark.parametrize("bad", [
+    '<edge source="a" target="b"><data key="lt">0</data><data key="el">0</data></edge>',     # latency > 0
+    '<edge source="a" target="b"><data key="lt">5</data><data key="el">1.5</data></edge>',   # loss in [0,1]
+    '<edge source="a" target="b"><data key="lt">5</data></edge>',                             # loss missing
+])
+def test_edge_validation(topo, tmp_path, bad):
+    body = N.format("a", "") + N.format("b", "") + bad
+    with pytest.raises(ValueError):
+        topo.load_graphml(_write(tmp_path, body))
+
+
+def test_vertex_validation_and_types(topo, tmp_path):
+    body = '<node id="a"><data key="bd">0</data><data key="bu">1</data></node>'
+    with pytest.raises(ValueError, match="bandwidth"):
+        topo.load_graphml(_write(tmp_path, body))
+    keys = """<key attr.name="packetloss" attr.type="string" for="edge" id="el" />
+  <key attr.name="latency" attr.type="double" for="edge" id="lt" />
+  <key attr.name="bandwidthup" attr.type="int" for="node" id="bu" />
+  <key attr.name="bandwidthdown" attr.type="int" for="node" id="bd" />"""
+    with pytest.raises(ValueError, match="type"):
+        topo.load_graphml(_write(tmp_path, N.format("a", ""), keys))
+
+
+def test_prefer_direct_attribute(topo, tmp_path):
+    g = internet_like(20, 2, seed=3, prefer_direct=True)
+    p = tmp_path / "pd.xml"
+    to_graphml(g, str(p))
+    h = topo.load_graphml(str(p))
+    assert h.prefer_direct and np.array_equal(h.latency, g.latency)

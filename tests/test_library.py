@@ -47,3 +47,15 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".c", ".cpp", ".h")):
                 txt = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in txt.replace("oracle/", "").lower() or f == "__init__.py", f
+
+
+def test_front_end_exports():
+    import re
+    from shadow_amd import build, topology
+    build.build()
+    text = open(os.path.join(ROOT, "include", "shd_topology.h")).read()
+    declared = sorted(set(re.findall(r"\b(shd_(?:topology|graphml)_[a-z_]+)\s*\(", text)))
+    assert sorted(topology.EXPORTS) == declared
+    lib = ctypes.CDLL(topology.LIB_PATH)
+    for sym in declared:
+        assert hasattr(lib, sym), sym

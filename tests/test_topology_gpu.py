@@ -1,0 +1,123 @@
+"""GPU: the C front end (topology.c semantics) end to end over the HIP engine."""
+import json
+import lzma
+import os
+
+import numpy as np
+import pytest
+
+from shadow_amd.graph import Graph, config, example_one_vertex, internet_like, to_graphml
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+
+
+@pytest.fixture(scope="module")
+def topo():
+    from shadow_amd import topology
+    topology.load_library()
+    return topology
+
+
+def _small(name):
+    z = np.load(os.path.join(GOLD, "small_tables.npz"))
+    p = f"{name}__"
+    vl = z[p + "vertex_packetloss"]
+    g = Graph(n=int(z[p + "n"]), src=z[p + "src"], dst=z[p + "dst"], latency=z[p + "latency"],
+              packetloss=z[p + "packetloss"], vertex_packetloss=vl if len(vl) else None,
+              directed=bool(z[p + "directed"]), prefer_direct=bool(z[p + "prefer_direct"]))
+    return g, z, p
+
+
+@pytest.mark.parametrize("name", ["ba60", "ba80_prefer", "k24", "ba100_attached", "dir40", "ba90_frac"])
+def test_cache_matches_golden_eager_table(topo, name):
+    g, z, p = _small(name)
+    A = z[p + "attached"]
+    t = topo.Topology.from_graph(g)
+    t.attach_all(A)
+    lat, rel = t.table(A)
+    assert np.array_equal(lat, z[p + "lat"]), name
+    uq = z[p + "unique"]
+    assert np.array_equal(rel[uq], z[p + "rel"][uq]), name
+    assert t.min_path_latency() == float(z[p + "min_latency"])
+    isd = np.array([[t.is_direct(a, b) for b in A] for a in A], bool)
+    assert np.array_equal(isd, z[p + "is_direct"]), name
+
+
+def test_example_config_graphml_kat(topo, tmp_path):
+    # resource/examples/shadow.config.xml: 2 hosts on the single vertex
+    g = example_one_vertex(0.0, 0.01, 50.0)
+    pth = tmp_path / "ex.graphml.xml"
+    to_graphml(g, str(pth))
+    t = topo.Topology.new(str(pth))
+    t.attach(0)
+    assert t.get_latency(0, 0) == 50.0 and t.get_reliability(0, 0) == 0.99
+    assert t.is_routable(0, 0) and t.is_direct(0, 0) == 1
+    assert t.runahead_ns() == 50_000_000
+
+
+def test_bundled_topology_xz(topo, tmp_path):
+    z = np.load(os.path.join(GOLD, "bundled_topology.npz"))
+    g = Graph(n=int(z["n"]), src=z["src"], dst=z["dst"], latency=z["latency"], packetloss=z["packetloss"],
+              vertex_packetloss=z["vertex_packetloss"], directed=bool(z["directed"]), ids=list(z["ids"]))
+    pth = tmp_path / "topology.graphml.xml"
+    to_graphml(g, str(pth))
+    pxz = tmp_path / "topology.graphml.xml.xz"
+    pxz.write_bytes(lzma.compress(pth.read_bytes()))
+    t = topo.Topology.new(str(pxz))
+    assert t.find_vertex("poi-112") == 0
+    t.attach_all(range(g.n))
+    lat, rel = t.table(range(g.n))
+    w = {}
+    for a, b, L in zip(g.src, g.dst, g.latency):
+        w[(a, b)] = w[(b, a)] = L
+    assert all(lat[s, d] == w[(s, d)] for s in range(0, g.n, 13) for d in range(g.n))
+    assert np.all(rel == 1.0 - 0.005)
+    assert t.min_path_latency() == 5.0 and t.runahead_ns() == 5_000_000
+
+
+def test_unattached_and_counters(topo):
+    g = internet_like(50, 2, seed=8)
+    t = topo.Topology.from_graph(g)
+    t.attach_all([1, 5, 9])
+    assert t.get_latency(1, 2) == -1.0 and not t.is_routable(2, 1)
+    for _ in range(3):
+        t.increment_path_packet_counter(5, 9)
+    t.increment_path_packet_counter(9, 5)  # same cached Path (reverse lookup)
+    assert t.packet_count(5, 9) == 4 and t.packet_count(9, 5) == 4
+    # attaching later refills over the grown set
+    t.attach(2)
+    assert t.get_latency(1, 2) > 0
+
+
+def test_multi_context_fill_equals_single(topo):
+    g = config("c2")
+    A = np.arange(0, g.n, 3)
+    t1 = topo.Topology.from_graph(g)
+    t2 = topo.Topology.from_graph(g, devices=(0, 0, 0))  # rows sharded over 3 contexts
+    t1.attach_all(A); t2.attach_all(A)
+    t1.fill(); t2.fill()
+    sel = A[::17]
+    l1, r1 = t1.table(sel)
+    l2, r2 = t2.table(sel)
+    assert np.array_equal(l1, l2) and np.array_equal(r1, r2)
+    assert t1.min_path_latency() == t2.min_path_latency()
+
+
+def test_dump_paths(topo, tmp_path):
+    import ctypes
+    g = internet_like(12, 2, seed=2)
+    t = topo.Topology.from_graph(g)
+    t.attach_all(range(g.n))
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    out = tmp_path / "paths.txt"
+    fp = libc.fopen(str(out).encode(), b"w")
+    assert topo.load_library().shd_topology_dump_paths(t._h, fp) == 0
+    libc.fclose(fp)
+    lines = out.read_text().splitlines()
+    assert len(lines) == g.n * (g.n + 1) // 2
+    assert lines[0].startswith("Found path 0<->0 in cache: SourceIndex=0 DestinationIndex=0 Latency=")

@@ -102,10 +102,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--verify", type=int, default=8, help="rows checked against the oracle after timing")
     ap.add_argument("--sources", type=int, default=0, help="limit sources per rank (0 = all)")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "f64"], help="force the generic f64 SSSP kernel")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "f64", "k32", "kb", "k16"], help="force an SSSP kernel")
     args = ap.parse_args()
-    if args.kernel == "f64":
-        os.environ["SHD_ROUTE_KERNEL"] = "f64"
+    if args.kernel != "auto":
+        os.environ["SHD_ROUTE_KERNEL"] = args.kernel
 
     import torch
     import torch.distributed as dist
@@ -130,11 +130,12 @@ def main():
     all_sources = targets.copy()
     if args.sources:
         all_sources = all_sources[: args.sources]
+    from shadow_amd.shard import allgather_rows, runahead_min, shard_range
     if weak or world == 1:
         my_sources = all_sources
     else:
-        blk = (len(all_sources) + world - 1) // world
-        my_sources = all_sources[rank * blk:(rank + 1) * blk]
+        lo, hi = shard_range(len(all_sources), world, rank)
+        my_sources = all_sources[lo:hi]
     ns, nt = len(my_sources), len(targets)
 
     eng = RouteEngine(g, device=local)
@@ -146,10 +147,6 @@ def main():
     d_rel = torch.empty((max(ns, 1), nt), dtype=torch.float64, device=dev)
     d_rmin = torch.empty(max(ns, 1), dtype=torch.float64, device=dev)
     d_min = torch.empty(1, dtype=torch.float64, device=dev)
-    gather = None
-    if not weak and world > 1 and args.allgather:
-        blk = (len(all_sources) + world - 1) // world
-        gather = [torch.empty((blk, nt), dtype=torch.float64, device=dev) for _ in range(world)]
     torch.cuda.synchronize()
 
     k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -163,11 +160,9 @@ def main():
             k_end[t].record(stream)
         eng.min_reduce_async(d_rmin, d_min, stream=sh)
         if world > 1 and not weak:
-            dist.all_reduce(d_min, op=dist.ReduceOp.MIN)
-            if gather is not None:
-                buf = d_lat if d_lat.shape[0] == gather[0].shape[0] else torch.nn.functional.pad(
-                    d_lat, (0, 0, 0, gather[0].shape[0] - d_lat.shape[0]))
-                dist.all_gather(gather, buf)
+            runahead_min(d_min, dist)                         # RCCL all-reduce MIN
+            if args.allgather:                                # full latency table on every GPU
+                allgather_rows(d_lat[:ns], len(all_sources), dist)
 
     for _ in range(args.warmup):
         step()
@@ -238,7 +233,7 @@ def main():
             "bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
             "traffic": load_traffic(args.config, ns),
             "kernel": {0: "sssp_rows_kernel", 1: "sssp_k32_kernel",
-                       2: "sssp_batch_kernel+path_attr_kernel"}[eng.info["kernel"]],
+                       2: "sssp_batch_kernel+path_attr_kernel", 3: "sssp_k16_kernel"}[eng.info["kernel"]],
             "bytes_per_source": b_src(n, nnz, nt),
         },
         "verified_rows_vs_oracle": verified,

@@ -4,6 +4,7 @@
 #include "sssp_k32.hpp"
 #include "sssp_batch.hpp"
 #include "path_attr.hpp"
+#include "sssp_k16.hpp"
 #include "direct_fw.hpp"
 
 using namespace shd;
@@ -41,6 +42,11 @@ struct shd_route {
     KBHub* d_kb_hub = nullptr;
     uint32_t* d_keys = nullptr;     // key rows scratch (ns x n u32), grown on demand
     size_t keys_cap = 0;
+    // K16 large-graph kernel (sssp_k16.hpp)
+    int k16 = 0, k16_slots = 0;
+    size_t k16_lds = 0, k16_stride = 0;
+    uint32_t* d_k16_oarc = nullptr;
+    char* d_k16_ws = nullptr;
     uint64_t device_bytes = 0;
     // host copies needed for lazy dense build
     std::vector<int32_t> e_src, e_dst;
@@ -232,6 +238,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
     if (rc) return rc;
     c->k32_bound = (int)bound;
     const bool want_k32 = !force || !strcmp(force, "k32") || !strcmp(force, "auto");
+    (void)0;
     const bool want_kb = !force || !strcmp(force, "kb") || !strcmp(force, "auto");
     if (block && want_k32) {
         const void* fn = block == 256 ? (const void*)sssp_k32_kernel<256>
@@ -248,6 +255,30 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
         rc = hip_check(hipFuncSetAttribute((const void*)path_attr_kernel<256>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)AL.total));
         if (rc) return rc;
+    }
+    // packed in-arcs (u << 16 | w), rows sorted by (-w, u, eid): KB and K16
+    {
+        std::vector<uint32_t> packed(((size_t)c->nnz + 3) / 4 * 4, 0u);
+        for (int q = 0; q < c->nnz; q++) packed[q] = ((uint32_t)cin[q] << 16) | (uint32_t)w[order[q]];
+        rc = upload(c, &c->d_kb_arc, packed);
+        if (rc) return rc;
+    }
+    // K16: u16 distances in LDS, one 1024-thread workgroup per source
+    const bool want_k16 = !force || !strcmp(force, "k16") || !strcmp(force, "auto");
+    if (want_k16 && k16_lds_bytes(n) <= kLdsBudget) {
+        std::vector<uint32_t> oarc(c->nnz);
+        for (int a = 0; a < c->nnz; a++) oarc[a] = ((uint32_t)col[a] << 16) | (uint32_t)w[a];
+        rc = upload(c, &c->d_k16_oarc, oarc);
+        if (rc) return rc;
+        c->k16_stride = k16_ws_stride(n);
+        c->k16_slots = 256;  // one 1024-thread workgroup per CU
+        if (hipMalloc((void**)&c->d_k16_ws, c->k16_stride * (size_t)c->k16_slots) != hipSuccess) return SHD_ROUTE_ENOMEM;
+        c->allocs.push_back(c->d_k16_ws);
+        c->k16_lds = k16_lds_bytes(n);
+        rc = hip_check(hipFuncSetAttribute((const void*)sssp_k16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)c->k16_lds));
+        if (rc) return rc;
+        c->k16 = 1;
     }
     // KB batched kernel: segments of <= KB_SEG in-arcs, hub rows split
     if (c->attr && want_kb) {
@@ -268,10 +299,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
         const KBLayout KL = KBLayout::make(n, c->nnz, npart);
         const size_t kbl = kKBSmall + KL.total;
         if (kbl <= kLdsBudget) {
-            std::vector<uint32_t> packed(((size_t)c->nnz + 3) / 4 * 4, 0u);
-            for (int q = 0; q < c->nnz; q++) packed[q] = ((uint32_t)cin[q] << 16) | (uint32_t)w[order[q]];
-            rc = upload(c, &c->d_kb_arc, packed);
-            if (!rc) rc = upload(c, &c->d_kb_seg, segs);
+            rc = upload(c, &c->d_kb_seg, segs);
             if (!rc && !hubs.empty()) rc = upload(c, &c->d_kb_hub, hubs);
             if (!rc) rc = hip_check(hipFuncSetAttribute((const void*)sssp_batch_kernel,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kbl));
@@ -456,9 +484,9 @@ int shd_route_get_info(const shd_route_t* c, shd_route_info_t* info) {
     info->multigraph = c->multigraph;
     info->device = c->device;
     info->lds_resident = (c->lds || c->k32 || c->kb) ? 1 : 0;
-    info->kernel = c->kb ? 2 : c->k32 ? 1 : 0;
+    info->kernel = c->kb ? 2 : c->k32 ? 1 : c->k16 ? 3 : 0;
     info->dist_bound = c->k32_bound;
-    info->block = c->kb ? KB_BLOCK : c->k32 ? c->k32_block : kBlock;
+    info->block = info->kernel == 2 ? KB_BLOCK : info->kernel == 3 ? K16_BLOCK : c->k32 ? c->k32_block : kBlock;
     info->device_bytes = c->device_bytes;
     info->min_edge_latency = c->min_w;
     return SHD_ROUTE_OK;
@@ -507,6 +535,15 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         const int grida = std::min(ns, 1 << 20);
         hipLaunchKernelGGL(path_attr_kernel<256>, dim3(grida), dim3(256), c->attr_lds, st, at, c->d_keys,
                            (long long)c->n, d_src, ns, d_tgt, nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
+        return hip_check(hipGetLastError());
+    }
+    if (c->k16 && !c->k32 && !(dispatch && c->prefer_direct)) {
+        DevK16 k;
+        k.n = c->n; k.bound = c->k32_bound; k.row = c->d_row; k.oarc = c->d_k16_oarc; k.row_in = c->d_k32_row_in;
+        k.iarc = c->d_kb_arc; k.r_in = c->d_k32_r_in; k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r;
+        const int grid = std::min(ns, c->k16_slots);
+        hipLaunchKernelGGL(sssp_k16_kernel, dim3(grid), dim3(K16_BLOCK), c->k16_lds, st, k, d_src, ns, d_tgt, nt,
+                           (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_k16_ws, c->k16_stride);
         return hip_check(hipGetLastError());
     }
     if (c->k32 && !(dispatch && c->prefer_direct)) {

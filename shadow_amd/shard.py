@@ -1,0 +1,44 @@
+"""Multi-GPU sharding of source rows (one process per GPU, torch.distributed).
+
+Source rows are independent: attached sources are split into contiguous
+blocks, one per rank; the only exchange step is the runahead minimum (all-reduce MIN
+of one double) and, where a device-resident full table is needed, an all-gather of
+the row shards (RCCL over xGMI with backend "nccl"; gloo on CPU for tests).
+"""
+from __future__ import annotations
+
+import math
+
+
+def shard_range(n_items: int, world: int, rank: int):
+    """Contiguous block [lo, hi) of rank `rank` (blocks of ceil(n/world))."""
+    blk = math.ceil(n_items / world) if world > 0 else n_items
+    lo = min(n_items, rank * blk)
+    hi = min(n_items, lo + blk)
+    return lo, hi
+
+
+def block_rows(n_items: int, world: int) -> int:
+    return math.ceil(n_items / world) if world > 0 else n_items
+
+
+def runahead_min(local_min, dist, group=None):
+    """All-reduce MIN of the per-rank minimum path latency (tensor of shape [1])."""
+    if dist is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(local_min, op=dist.ReduceOp.MIN, group=group)
+    return local_min
+
+
+def allgather_rows(local_rows, n_total: int, dist, group=None):
+    """All-gather row shards (each [rows_r, nt]) into the full [n_total, nt] table.
+    Shards are padded to the common block size for the collective."""
+    import torch
+    world = dist.get_world_size(group) if dist is not None and dist.is_initialized() else 1
+    if world == 1:
+        return local_rows
+    blk = block_rows(n_total, world)
+    pad = blk - local_rows.shape[0]
+    send = local_rows if pad == 0 else torch.nn.functional.pad(local_rows, (0, 0, 0, pad))
+    out = [torch.empty_like(send) for _ in range(world)]
+    dist.all_gather(out, send.contiguous(), group=group)
+    return torch.cat(out, 0)[:n_total]

@@ -102,7 +102,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--verify", type=int, default=8, help="rows checked against the oracle after timing")
     ap.add_argument("--sources", type=int, default=0, help="limit sources per rank (0 = all)")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "f64", "k32", "kb", "k16"], help="force an SSSP kernel")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "f64", "k32", "kb", "k16", "kd"], help="force an SSSP kernel")
     args = ap.parse_args()
     if args.kernel != "auto":
         os.environ["SHD_ROUTE_KERNEL"] = args.kernel
@@ -233,7 +233,8 @@ def main():
             "bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
             "traffic": load_traffic(args.config, ns),
             "kernel": {0: "sssp_rows_kernel", 1: "sssp_k32_kernel",
-                       2: "sssp_batch_kernel+path_attr_kernel", 3: "sssp_k16_kernel"}[eng.info["kernel"]],
+                       2: "sssp_batch_kernel+path_attr_kernel", 3: "sssp_k16_kernel",
+                       4: "sssp_delta_kernel"}[eng.info["kernel"]],
             "bytes_per_source": b_src(n, nnz, nt),
         },
         "verified_rows_vs_oracle": verified,

@@ -11,7 +11,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 SOURCES = [os.path.join(HERE, "csrc", "engine.hip")]
-HEADERS = [os.path.join(HERE, "csrc", f) for f in ("common.hpp", "sssp_f64.hpp", "sssp_k32.hpp", "sssp_batch.hpp", "path_attr.hpp", "sssp_k16.hpp", "direct_fw.hpp")]
+HEADERS = [os.path.join(HERE, "csrc", f) for f in ("common.hpp", "sssp_f64.hpp", "sssp_k32.hpp", "sssp_batch.hpp", "path_attr.hpp", "sssp_k16.hpp", "sssp_delta.hpp", "direct_fw.hpp")]
 OUT = os.path.join(HERE, "libshd_route.so")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
          "-Wall", "-Wno-unused-result"]

@@ -5,6 +5,7 @@
 #include "sssp_batch.hpp"
 #include "path_attr.hpp"
 #include "sssp_k16.hpp"
+#include "sssp_delta.hpp"
 #include "direct_fw.hpp"
 
 using namespace shd;
@@ -47,6 +48,12 @@ struct shd_route {
     size_t k16_lds = 0, k16_stride = 0;
     uint32_t* d_k16_oarc = nullptr;
     char* d_k16_ws = nullptr;
+    // KD delta-stepping kernel (sssp_delta.hpp)
+    int kd = 0, kd_block = 1024, kd_slots = 0, kd_delta = 1, kd_qcap = 0;
+    size_t kd_lds = 0, kd_stride = 0;
+    int* d_kd_lstart = nullptr;
+    char* d_kd_ws = nullptr;
+    int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD
     uint64_t device_bytes = 0;
     // host copies needed for lazy dense build
     std::vector<int32_t> e_src, e_dst;
@@ -264,12 +271,14 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
         if (rc) return rc;
     }
     // K16: u16 distances in LDS, one 1024-thread workgroup per source
-    const bool want_k16 = !force || !strcmp(force, "k16") || !strcmp(force, "auto");
-    if (want_k16 && k16_lds_bytes(n) <= kLdsBudget) {
+    const bool want_k16 = force && !strcmp(force, "k16");
+    {
         std::vector<uint32_t> oarc(c->nnz);
         for (int a = 0; a < c->nnz; a++) oarc[a] = ((uint32_t)col[a] << 16) | (uint32_t)w[a];
         rc = upload(c, &c->d_k16_oarc, oarc);
         if (rc) return rc;
+    }
+    if (want_k16 && k16_lds_bytes(n) <= kLdsBudget) {
         c->k16_stride = k16_ws_stride(n);
         c->k16_slots = 256;  // one 1024-thread workgroup per CU
         if (hipMalloc((void**)&c->d_k16_ws, c->k16_stride * (size_t)c->k16_slots) != hipSuccess) return SHD_ROUTE_ENOMEM;
@@ -279,6 +288,55 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                                            (int)c->k16_lds));
         if (rc) return rc;
         c->k16 = 1;
+    }
+    // KD delta-stepping: bucket width ~ the 6th percentile of arc latencies (>= 1), so
+    // ~6% of arcs are light; light in-arcs are the tail of each (-w)-sorted in-row
+    const bool want_kd = !force || !strcmp(force, "kd") || !strcmp(force, "auto");
+    if (want_kd && c->nnz > 0) {
+        int delta = 1;
+        if (const char* e = getenv("SHD_ROUTE_DELTA")) delta = std::max(1, atoi(e));
+        else {
+            std::vector<int> ws(c->nnz);
+            for (int a = 0; a < c->nnz; a++) ws[a] = (int)w[a];
+            const size_t k = (size_t)c->nnz * 6 / 100;
+            std::nth_element(ws.begin(), ws.begin() + k, ws.end());
+            delta = std::max(1, ws[k]);
+        }
+        const int blk = n > 16384 ? 1024 : n > 4096 ? 512 : 256;
+        const size_t base = blk == 1024 ? kd_lds_bytes<1024>(n, 0) : blk == 512 ? kd_lds_bytes<512>(n, 0)
+                                                                               : kd_lds_bytes<256>(n, 0);
+        if (base + 2 * 512 <= kLdsBudget) {
+            // queue: the rest of the CU's LDS at one workgroup per CU (large n), else enough
+            // for a few workgroups per CU
+            int qcap;
+            if (blk == 1024) qcap = (int)std::min<size_t>((size_t)n, (kLdsBudget - base - 16) / 2);
+            else qcap = std::min(n, std::max(512, n / 2));
+            if (const char* e = getenv("SHD_ROUTE_QCAP")) qcap = std::min(qcap, std::max(64, atoi(e)));
+            qcap &= ~7;
+            const size_t lds = base + a16(2 * (size_t)qcap);
+            if (lds <= kLdsBudget) {
+                std::vector<int> lst(n);
+                for (int v = 0; v < n; v++) {
+                    int q = irow[v];
+                    if (!c->directed)
+                        while (q < irow[v + 1] && (int)w[order[q]] >= delta) q++;
+                    lst[v] = q;
+                }
+                rc = upload(c, &c->d_kd_lstart, lst);
+                if (rc) return rc;
+                const int per_cu = std::max(1, std::min((int)(kLdsBudget / lds), 2048 / blk));
+                c->kd_slots = 256 * per_cu;
+                c->kd_stride = kd_ws_stride(n);
+                if (hipMalloc((void**)&c->d_kd_ws, c->kd_stride * (size_t)c->kd_slots) != hipSuccess)
+                    return SHD_ROUTE_ENOMEM;
+                c->allocs.push_back(c->d_kd_ws);
+                const void* fn = blk == 1024 ? (const void*)sssp_delta_kernel<1024>
+                               : blk == 512 ? (const void*)sssp_delta_kernel<512> : (const void*)sssp_delta_kernel<256>;
+                rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                if (rc) return rc;
+                c->kd = 1; c->kd_block = blk; c->kd_lds = lds; c->kd_delta = delta; c->kd_qcap = qcap;
+            }
+        }
     }
     // KB batched kernel: segments of <= KB_SEG in-arcs, hub rows split
     if (c->attr && want_kb) {
@@ -308,6 +366,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
             c->kb_npart = npart;
         }
     }
+    c->sel = c->kb ? 2 : c->kd ? 4 : c->k32 ? 1 : c->k16 ? 3 : 0;
     return SHD_ROUTE_OK;
 }
 
@@ -483,10 +542,12 @@ int shd_route_get_info(const shd_route_t* c, shd_route_info_t* info) {
     info->integer_weights = c->integer_w;
     info->multigraph = c->multigraph;
     info->device = c->device;
-    info->lds_resident = (c->lds || c->k32 || c->kb) ? 1 : 0;
-    info->kernel = c->kb ? 2 : c->k32 ? 1 : c->k16 ? 3 : 0;
+    info->lds_resident = (c->lds || c->sel) ? 1 : 0;
+    info->kernel = c->sel;
     info->dist_bound = c->k32_bound;
-    info->block = info->kernel == 2 ? KB_BLOCK : info->kernel == 3 ? K16_BLOCK : c->k32 ? c->k32_block : kBlock;
+    info->block = c->sel == 2 ? KB_BLOCK : c->sel == 3 ? K16_BLOCK : c->sel == 4 ? c->kd_block
+                : c->sel == 1 ? c->k32_block : kBlock;
+    info->reserved = c->sel == 4 ? c->kd_delta : 0;
     info->device_bytes = c->device_bytes;
     info->min_edge_latency = c->min_w;
     return SHD_ROUTE_OK;
@@ -508,7 +569,7 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         return hip_check(hipGetLastError());
     }
     const int dispatch = (flags & SHD_ROUTE_DISPATCH) ? 1 : 0;
-    if (c->kb && !(dispatch && c->prefer_direct)) {
+    if (c->sel == 2 && !(dispatch && c->prefer_direct)) {
         // KB distances+parents for KB_SRC sources per workgroup -> key rows -> K2
         const size_t need = (size_t)ns * c->n;
         if (need > c->keys_cap) {
@@ -537,7 +598,26 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
                            (long long)c->n, d_src, ns, d_tgt, nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
         return hip_check(hipGetLastError());
     }
-    if (c->k16 && !c->k32 && !(dispatch && c->prefer_direct)) {
+    if (c->sel == 4 && !(dispatch && c->prefer_direct)) {
+        DevDelta k;
+        k.n = c->n; k.nw = (c->n + 63) / 64; k.bound = c->k32_bound; k.delta = c->kd_delta;
+        k.fused = c->directed ? 0 : 1; k.qcap = c->kd_qcap;
+        k.row = c->d_row; k.oarc = c->d_k16_oarc; k.r_out = c->d_r; k.row_in = c->d_k32_row_in;
+        k.lstart = c->d_kd_lstart; k.iarc = c->d_kb_arc; k.r_in = c->d_k32_r_in;
+        k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;
+        const int grid = std::min(ns, c->kd_slots);
+        if (c->kd_block == 1024)
+            hipLaunchKernelGGL(sssp_delta_kernel<1024>, dim3(grid), dim3(1024), c->kd_lds, st, k, d_src, ns, d_tgt,
+                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kd_ws, c->kd_stride);
+        else if (c->kd_block == 512)
+            hipLaunchKernelGGL(sssp_delta_kernel<512>, dim3(grid), dim3(512), c->kd_lds, st, k, d_src, ns, d_tgt,
+                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kd_ws, c->kd_stride);
+        else
+            hipLaunchKernelGGL(sssp_delta_kernel<256>, dim3(grid), dim3(256), c->kd_lds, st, k, d_src, ns, d_tgt,
+                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kd_ws, c->kd_stride);
+        return hip_check(hipGetLastError());
+    }
+    if (c->sel == 3 && !(dispatch && c->prefer_direct)) {
         DevK16 k;
         k.n = c->n; k.bound = c->k32_bound; k.row = c->d_row; k.oarc = c->d_k16_oarc; k.row_in = c->d_k32_row_in;
         k.iarc = c->d_kb_arc; k.r_in = c->d_k32_r_in; k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r;
@@ -546,7 +626,7 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
                            (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_k16_ws, c->k16_stride);
         return hip_check(hipGetLastError());
     }
-    if (c->k32 && !(dispatch && c->prefer_direct)) {
+    if (c->sel == 1 && !(dispatch && c->prefer_direct)) {
         DevK32 k;
         k.n = c->n; k.bound = c->k32_bound; k.row = c->d_row; k.arc = c->d_arc; k.row_in = c->d_k32_row_in;
         k.col_in = c->d_k32_col_in; k.r_in = c->d_k32_r_in; k.vf = c->d_vf; k.self_w = c->d_self_w;

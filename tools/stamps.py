@@ -53,6 +53,19 @@ if eng.info["kernel"] == 2:
     t0 = d[:, 0] - d[:, 0].min()
     print(f"  K2 start spread p50 {np.median(t0):.0f} max {t0.max()}")
     sys.exit(0)
+if eng.info["kernel"] == 4:
+    ph = np.diff(d[:, :5], axis=1)
+    print(f"config {a.config} n={g.n} nnz={g.nnz} sources={len(S)} kernel=KD block={eng.info['block']} delta={eng.info['reserved']}")
+    for k, nm in enumerate(["A_delta", "B_fixup", "C_lat+par+rel", "D_out"]):
+        print(f"  {nm:14s} mean {ph[:, k].mean():10.0f} cyc  p50 {np.median(ph[:, k]):10.0f}  max {ph[:, k].max():10.0f}")
+    tot = d[:, 4] - d[:, 0]
+    print(f"  total          mean {tot.mean():10.0f} cyc")
+    print(f"  sweeps mean/max        {d[:, 5].mean():.1f} / {d[:, 5].max()}")
+    print(f"  queued vertices / n    {d[:, 6].mean() / g.n:.3f}")
+    print(f"  arcs expanded / nnz    {d[:, 7].mean() / g.nnz:.3f}")
+    t0 = d[:, 0] - d[:, 0].min()
+    print(f"  start spread (cyc): p50 {np.median(t0):.0f} max {t0.max()}  end max {(d[:, 4] - d[:, 0].min()).max()}")
+    sys.exit(0)
 ph = np.diff(d[:, :5], axis=1)
 names = ["A_bf", "B_parent", "C_rel", "D_out"]
 print(f"config {a.config} n={g.n} nnz={g.nnz} sources={len(S)} kernel={eng.info['kernel']} block={eng.info['block']}")

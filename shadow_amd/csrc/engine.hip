@@ -51,7 +51,11 @@ struct shd_route {
     // KD delta-stepping kernel (sssp_delta.hpp)
     int kd = 0, kd_block = 1024, kd_slots = 0, kd_delta = 1, kd_qcap = 0;
     size_t kd_lds = 0, kd_stride = 0;
-    int* d_kd_lstart = nullptr;
+    int* d_kd_lstart = nullptr;   // light in-CSR offsets (n+1)
+    uint32_t* d_kd_orec = nullptr;  // out-arc records (2 x u32 per arc)
+    uint32_t* d_kd_lrec = nullptr;  // light in-arc records (2 x u32 per arc)
+    double* d_kd_rtab = nullptr;    // distinct reliabilities
+    int kd_nlight = 0, kd_nrtab = 1;
     char* d_kd_ws = nullptr;
     int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD
     uint64_t device_bytes = 0;
@@ -308,22 +312,66 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
         if (base + 2 * 512 <= kLdsBudget) {
             // queue: the rest of the CU's LDS at one workgroup per CU (large n), else enough
             // for a few workgroups per CU
+            // work queue: the rest of the CU's LDS at one workgroup per CU (large n), else
+            // enough for a few workgroups per CU
             int qcap;
-            if (blk == 1024) qcap = (int)std::min<size_t>((size_t)n, (kLdsBudget - base - 16) / 2);
-            else qcap = std::min(n, std::max(512, n / 2));
+            if (blk == 1024) qcap = (int)std::min<size_t>((size_t)n, (kLdsBudget - base - 64) / 2);
+            else qcap = std::min(n, std::max(1024, n / 2));
             if (const char* e = getenv("SHD_ROUTE_QCAP")) qcap = std::min(qcap, std::max(64, atoi(e)));
             qcap &= ~7;
-            const size_t lds = base + a16(2 * (size_t)qcap);
-            if (lds <= kLdsBudget) {
-                std::vector<int> lst(n);
-                for (int v = 0; v < n; v++) {
-                    int q = irow[v];
-                    if (!c->directed)
-                        while (q < irow[v + 1] && (int)w[order[q]] >= delta) q++;
-                    lst[v] = q;
+            const size_t lds = blk == 1024 ? kd_lds_bytes<1024>(n, qcap) : blk == 512 ? kd_lds_bytes<512>(n, qcap)
+                                                                           : kd_lds_bytes<256>(n, qcap);
+            int maxdeg = 0;
+            for (int v = 0; v < n; v++) maxdeg = std::max(maxdeg, row[v + 1] - row[v]);
+            // reliability table: every distinct 1-loss value (exact bits), indexed by u16
+            std::vector<double> rtab;
+            std::vector<uint16_t> ridx_out(c->nnz);
+            bool rtab_ok = true;
+            {
+                std::vector<std::pair<uint64_t, int>> keyed(c->nnz);
+                for (int a = 0; a < c->nnz; a++) {
+                    uint64_t bits;
+                    std::memcpy(&bits, &c->e_rel[eid[a]], 8);
+                    keyed[a] = {bits, a};
                 }
-                rc = upload(c, &c->d_kd_lstart, lst);
+                std::sort(keyed.begin(), keyed.end());
+                for (int q = 0; q < c->nnz && rtab_ok; q++) {
+                    if (q == 0 || keyed[q].first != keyed[q - 1].first) {
+                        double x;
+                        std::memcpy(&x, &keyed[q].first, 8);
+                        rtab.push_back(x);
+                        if (rtab.size() > 65535) rtab_ok = false;
+                    }
+                    ridx_out[keyed[q].second] = (uint16_t)(rtab.size() - 1);
+                }
+            }
+            if (lds <= kLdsBudget && maxdeg <= 65535 && rtab_ok) {
+                // out-arc records {v | w << 16, ridx}; light in-CSR records {u | w << 16, ridx}
+                // (light = w < delta; directed graphs: every in-arc, fused parents are off)
+                std::vector<uint32_t> orec(2 * (size_t)c->nnz);
+                for (int a = 0; a < c->nnz; a++) {
+                    orec[2 * (size_t)a] = (uint32_t)col[a] | ((uint32_t)w[a] << 16);
+                    orec[2 * (size_t)a + 1] = ridx_out[a];
+                }
+                std::vector<int> lrow(n + 1, 0);
+                std::vector<uint32_t> lrec;
+                for (int v = 0; v < n; v++) {
+                    for (int q = irow[v]; q < irow[v + 1]; q++) {
+                        const int a = order[q];
+                        if (!c->directed && (int)w[a] >= delta) continue;
+                        lrec.push_back((uint32_t)cin[q] | ((uint32_t)w[a] << 16));
+                        lrec.push_back(ridx_out[a]);
+                    }
+                    lrow[v + 1] = (int)(lrec.size() / 2);
+                }
+                if (lrec.empty()) lrec.assign(2, 0u);
+                rc = upload(c, &c->d_kd_lstart, lrow);
+                if (!rc) rc = upload(c, &c->d_kd_orec, orec);
+                if (!rc) rc = upload(c, &c->d_kd_lrec, lrec);
+                if (!rc) rc = upload(c, &c->d_kd_rtab, rtab);
                 if (rc) return rc;
+                c->kd_nlight = lrow[n];
+                c->kd_nrtab = std::max<int>(1, (int)rtab.size());
                 const int per_cu = std::max(1, std::min((int)(kLdsBudget / lds), 2048 / blk));
                 c->kd_slots = 256 * per_cu;
                 c->kd_stride = kd_ws_stride(n);
@@ -366,7 +414,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
             c->kb_npart = npart;
         }
     }
-    c->sel = c->kb ? 2 : c->kd ? 4 : c->k32 ? 1 : c->k16 ? 3 : 0;
+    c->sel = c->kb ? 2 : c->k32 ? 1 : c->kd ? 4 : c->k16 ? 3 : 0;  // K32 still beats KD on C3-class graphs
     return SHD_ROUTE_OK;
 }
 
@@ -601,9 +649,10 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
     if (c->sel == 4 && !(dispatch && c->prefer_direct)) {
         DevDelta k;
         k.n = c->n; k.nw = (c->n + 63) / 64; k.bound = c->k32_bound; k.delta = c->kd_delta;
-        k.fused = c->directed ? 0 : 1; k.qcap = c->kd_qcap;
-        k.row = c->d_row; k.oarc = c->d_k16_oarc; k.r_out = c->d_r; k.row_in = c->d_k32_row_in;
-        k.lstart = c->d_kd_lstart; k.iarc = c->d_kb_arc; k.r_in = c->d_k32_r_in;
+        k.fused = c->directed ? 0 : 1; k.rc = c->kd_qcap;
+        k.row = c->d_row; k.orec = reinterpret_cast<const uint2*>(c->d_kd_orec);
+        k.lrow = c->d_kd_lstart; k.lrec = reinterpret_cast<const uint2*>(c->d_kd_lrec); k.nlight = c->kd_nlight;
+        k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab;
         k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;
         const int grid = std::min(ns, c->kd_slots);
         if (c->kd_block == 1024)

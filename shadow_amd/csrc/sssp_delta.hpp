@@ -8,115 +8,168 @@
 // A  Delta-stepping.  Bucket k holds pending vertices with dist in [k*D, (k+1)*D).
 //    Pending vertices are a bitmask (u64 word per 64 vertices) plus, per word, a
 //    conservative lower bound of the pending distances (wmin), so a sweep opens only
-//    words that can hold bucket work.  Each sweep: (1) gather -- one thread per word
-//    moves the pending vertices with dist < T into a dense LDS queue (no atomics:
-//    nothing else runs), (2) expand -- each wave takes 64 queued vertices and walks
-//    their out-arcs with a wave-level load-balanced scan, 64 arcs per step, P steps of
-//    arc loads in flight; an improvement is a 32-bit CAS on the word holding two u16
-//    distances (there is no 16-bit LDS atomic) followed by set-pending + wmin update.
-//    On BA topologies with U[1,250] ms edges D = 16 expands each vertex ~1.03 times
-//    (frontier Bellman-Ford: 5.7 times) in ~45 sweeps.
+//    words that can hold bucket work.  Each sweep:
+//      gather  one thread per word moves the pending vertices with dist < T into a
+//              dense LDS queue (no atomics: nothing else runs);
+//      prep    one thread per queue entry loads its CSR row bounds (all loads in
+//              flight at once, so a sweep pays one global latency for them);
+//      expand  each wave takes a 64-entry slice (strided over the queue, so the BA
+//              hubs -- low ids, gathered first -- spread over all slices) and walks the
+//              slice's out-arcs with a wave-level load-balanced scan: KD_P steps of 64
+//              arcs at a time, owners found for all steps with one marker write, all
+//              arc loads in flight together, all dist reads batched.
+//    An improvement is a 32-bit CAS on the word holding two u16 distances (there is no
+//    16-bit LDS atomic), then set-pending + wmin update.  On BA topologies with
+//    U[1,250] ms edges D = 15 expands each vertex ~1.03 times (frontier Bellman-Ford:
+//    5.7 times).
 //
 //    Fused parents (undirected graphs): when u is expanded, its out-arcs are its in-arcs,
 //    so the same dist[v] reads find the tight in-arcs (dist[v] + w == dist[u]).  The
 //    engine tie rule takes the tight arc with the largest w, then smallest (u, eid).  A
 //    tight HEAVY arc (w >= D) comes from an earlier bucket, which is final when u's last
 //    expansion runs, so a heavy winner seen at the last expansion is the final parent:
-//    no light arc can beat it and no heavy arc can appear later.  Only vertices whose
-//    winner is light (or absent) are marked for a pull fix-up over the light tail of
-//    their (-w, u, eid)-sorted in-row (phase B).  Directed graphs fix up every vertex.
+//    no light arc can beat it and no heavy arc can appear later.  Vertices whose winner
+//    is light or absent (45% on C4: shortest-path trees favour short arcs) are marked
+//    for a pull fix-up over the light tail of their (-w, u, eid)-sorted in-row (phase
+//    B, ~6% of the arcs).  Directed graphs fix up every vertex over its whole in-row.
 //
-// B  lat row out (dist is exact: integer latencies, bound < 0xFFFF) + fix-ups.
-// C  reliability down the tree, level-synchronous, relv f64 in a per-workgroup HBM slice
-//    (8n bytes do not fit LDS at this size), parents u16 in LDS over the dead distances.
-// D  rel row out, row min.
+// B  fix-ups (four vertices and four tail arcs each in flight per thread; long tails one
+//    wave per vertex), lat row out (dist is exact: integer latencies, bound < 0xFFFF).
+// C  reliability down the tree: parents u16 in LDS over the dead distances, relv f64 in
+//    a per-workgroup HBM slice (8n bytes do not fit LDS at this size).  Level sweeps
+//    over a pending bitmask: a vertex is ready when its parent left the pending set in
+//    an earlier sweep; ready vertices load relv[parent] and their own -r together.
+// D  rel row out, row min.  Output rows are non-temporal stores (written once, never
+//    re-read here) so they do not evict the CSR from L2.
+//
+// Measured on MI355X under a full-chip load (tools/micro/lat_probe.hip): a dependent
+// L2 gather costs ~2.4k cycles, a random 4-8 B gather into a 16-64 MB array is line-
+// traffic bound at ~0.3-0.5 per CU-cycle, and because gfx9 counts loads and stores in ONE
+// in-order vmcnt, a load consumed after a store waits ~5-15k cycles for that store.  So:
+//  * arc records carry everything a parent needs: out-arcs {v | w << 16, ridx} where
+//    ridx indexes the table of distinct reliabilities (101 entries on C4), so the winning
+//    parent (vertex, ridx) comes out of the expansion itself, no gather;
+//  * fix-ups read a compact light in-CSR (6% of the arcs, L2-resident);
+//  * loads are straight-line (clamped addresses, no branches around them) and stores are
+//    deferred: a slice records each winner in LDS, the next sweep flushes the records
+//    (wpr, one u32 per vertex) before its only global loads.
 #include "common.hpp"
 
 namespace shd {
 
-constexpr int KD_P = 8;  // arc steps (64 arcs each) with loads in flight per wave
+constexpr int KD_P = 4;  // arc steps (64 arcs each) with loads in flight per wave
+constexpr int KD_TAIL = 4;  // light-tail arcs per fix-up vertex loaded speculatively
+constexpr uint32_t KD_NONE = 0xFFFFFFFFu;      // no parent recorded
+constexpr uint32_t KD_SRC_MARK = 0xFFFFFFFEu;  // parent record of the source itself
 
 struct DevDelta {
     int n, nw;
+    int nlight;                         // light in-arcs
     int bound;
     int delta;                          // bucket width; arcs with w >= delta are heavy
     int fused;                          // undirected: parents found during expansion
-    int qcap;                           // LDS queue capacity (vertices)
+    int rc;                             // LDS work-queue capacity per bucket round (vertices)
     const int* __restrict__ row;        // out-CSR offsets (n+1)
-    const uint32_t* __restrict__ oarc;  // out-arcs (v << 16 | w), rows sorted by (v, eid)
-    const double* __restrict__ r_out;   // 1 - loss per out-arc
-    const int* __restrict__ row_in;     // in-CSR offsets (n+1), rows sorted by (-w, u, eid)
-    const int* __restrict__ lstart;     // first light in-arc of each row (directed: row start)
-    const uint32_t* __restrict__ iarc;  // in-arcs (u << 16 | w)
-    const double* __restrict__ r_in;    // 1 - loss per in-arc
+    const uint2* __restrict__ orec;     // out-arcs {v | w << 16, ridx}, rows sorted by (v, eid)
+    const int* __restrict__ lrow;       // light in-CSR offsets (n+1)
+    const uint2* __restrict__ lrec;     // light in-arcs {u | w << 16, ridx}, rows by (-w, u, eid)
+                                        // (directed graphs: every in-arc)
+    const double* __restrict__ rtab;    // distinct 1 - loss values, indexed by ridx
+    int nrtab;
     const double* __restrict__ vf;
     const double* __restrict__ self_w;
     const double* __restrict__ self_r;
-    unsigned long long* dbg;            // SHD_STAMPS builds: 8 words per source
+    unsigned long long* dbg;            // SHD_STAMPS builds: 32 words per source
 };
 
 #ifdef SHD_STAMPS
-#define KD_STAMP(slot) do { if (tid == 0 && g.dbg) g.dbg[(size_t)i * 8 + (slot)] = __builtin_amdgcn_s_memtime(); } while (0)
-#define KD_COUNT(slot, x) do { if (g.dbg && lane == 0) atomicAdd(&g.dbg[(size_t)i * 8 + (slot)], (unsigned long long)(x)); } while (0)
+// 32 words per source: 0-4 phase stamps, 5 sweeps, 6 queued, 7 arcs, 8-11 summed sweep
+// parts, 12-15 phase C (sweeps, compute, store drain, barriers), 16-19 phase B parts
+// accumulated in LDS (sm->acc) and written out once per source: a global read-modify-
+// write inside the timed regions would drain the wave's vmcnt and distort them
+#define KD_STAMP(slot) do { if (tid == 0) sm->acc[slot] = __builtin_amdgcn_s_memtime(); } while (0)
+#define KD_COUNT(slot, x) do { if (lane == 0 && (x)) atomicAdd(&sm->acc[slot], (unsigned long long)(x)); } while (0)
+#define KD_MARK() do { if (tid == 0) kd_t = __builtin_amdgcn_s_memtime(); } while (0)
+#define KD_ACC(slot) do { if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[slot] += t_ - kd_t; kd_t = t_; } } while (0)
+#define KD_FLUSH() do { lds_barrier(); if (g.dbg) for (int q_ = tid; q_ < 32; q_ += B) g.dbg[(size_t)i * 32 + q_] = sm->acc[q_]; lds_barrier(); if (tid < 32) sm->acc[tid] = 0; lds_barrier(); } while (0)
 #else
 #define KD_STAMP(slot) do { } while (0)
 #define KD_COUNT(slot, x) do { } while (0)
+#define KD_MARK() do { } while (0)
+#define KD_ACC(slot) do { } while (0)
+#define KD_FLUSH() do { } while (0)
 #endif
 
 struct KDSmall {
-    unsigned gmin[2];   // min pending distance seen at the start of a sweep (by parity)
-    int qtail[2];       // queue length
-    int qcur[2];        // next queue slice to expand
-    int flag;
-    int pad;
+    unsigned gmin[2];   // min pending distance at the start of a bucket round (by parity)
+    int head, tail;     // work queue of this bucket round: grabbed / reserved
+    int busy;           // compute waves holding a grabbed slice
+    int nexit;          // compute waves that left the async loop
+    int rtail, rdone;   // parent-record ring: reserved / consumed by the writer wave
+    int qtail[2];       // phase B/C list lengths (by parity)
+    int qcur[2];        // phase B long-tail list lengths
     unsigned long long rmin;
+#ifdef SHD_STAMPS
+    unsigned long long acc[32];
+#endif
 };
 
+// LDS: per-wave scratch | dist u16[n+1] | pend, inq, fix u64[nw] | wmin u32[nw] | work.
+// work holds the bucket work queue (u16 x rc) + the parent-record ring (uint2 x rr) in
+// phase A, and the phase B/C vertex lists (u16 x qcap + i32 x qcap) afterwards.
 template <int B>
 struct KDLayout {
-    size_t wflag, wkey, dist, pend, wmin, fix, queue, total;
-    __host__ __device__ static KDLayout make(int n, int qcap) {
+    size_t wmark, wkey, dist, pend, inq, fix, wmin, work, ring, rrec, qv, qbeg, total;
+    int qcap;
+    __host__ __device__ static KDLayout make(int n, int rc, int rr) {
         KDLayout L;
         const size_t nw = (size_t)(n + 63) / 64;
         size_t o = a16(sizeof(KDSmall));
-        L.wflag = o; o += (size_t)(B / 64) * 64;
+        L.wmark = o; o += (size_t)(B / 64) * 64 * KD_P;
         L.wkey = o;  o += (size_t)(B / 64) * 64 * 8;
         L.dist = o;  o += a16(sizeof(uint16_t) * (size_t)(n + 1));
         L.pend = o;  o += a16(8 * nw);
-        L.wmin = o;  o += a16(4 * nw);
+        L.inq = o;   o += a16(8 * nw);
         L.fix = o;   o += a16(8 * nw);
-        L.queue = o; o += a16(sizeof(uint16_t) * (size_t)qcap);
+        L.wmin = o;  o += a16(4 * nw);
+        L.work = o;
+        const size_t wbytes = a16(2 * (size_t)rc) + 8 * (size_t)rr;
+        L.ring = o;
+        L.rrec = o + a16(2 * (size_t)rc);
+        L.qcap = (int)((wbytes - 16) / 6) & ~7;
+        L.qv = o;
+        L.qbeg = o + a16(2 * (size_t)L.qcap);
+        o += wbytes;
         L.total = o;
         return L;
     }
 };
+constexpr int KD_RR = 1024;  // parent-record ring slots
 
-// per-workgroup HBM slice: relv f64[n] | parent u16[n]
-__host__ __device__ inline size_t kd_ws_stride(int n) { return a16(sizeof(double) * n) + a16(sizeof(uint16_t) * n) + 256; }
+// per-workgroup HBM slice: relv f64[n] | wpr u32[n], the parent record of every vertex:
+// parent << 16 | ridx of the parent arc (KD_SRC_MARK for the source)
+__host__ __device__ inline size_t kd_ws_stride(int n) { return a16(sizeof(double) * n) + a16(sizeof(uint32_t) * n) + 256; }
 
 // LDS-only workgroup barrier: outstanding global stores (output rows) stay in flight.
 __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ inline void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// lower the u16 at d[v] to nd if smaller; true if this call lowered it
-__device__ inline bool kd_lower(uint16_t* d, int v, unsigned nd) {
-    uint32_t* wp = reinterpret_cast<uint32_t*>(d) + (v >> 1);
-    const int sh = (v & 1) * 16;
-    uint32_t old = *wp;
-    for (;;) {
-        const unsigned cur = (old >> sh) & 0xFFFFu;
-        if (nd >= cur) return false;
-        const uint32_t nw = (old & ~(0xFFFFu << sh)) | (nd << sh);
-        const uint32_t prev = atomicCAS(wp, old, nw);
-        if (prev == old) return true;
-        old = prev;
-    }
-}
-
 __device__ inline unsigned kd_wave_min(unsigned x) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) x = min(x, (unsigned)__shfl_xor((int)x, d, 64));
     return x;
+}
+
+__device__ inline unsigned ld16(const uint16_t* d, int v) { return d[v]; }
+
+// pop up to four set bits of *b (lowest first) into v[] as vertex ids of word k (-1 = none)
+__device__ inline void pop4(unsigned long long* b, int k, int v[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const unsigned long long x = *b;
+        v[q] = x ? (k << 6) + __ffsll((long long)x) - 1 : -1;
+        *b = x & (x - 1);
+    }
 }
 
 template <int B>
@@ -127,21 +180,34 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                                                        char* __restrict__ ws, size_t ws_stride) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int n = g.n, nw = g.nw;
-    const KDLayout<B> L = KDLayout<B>::make(n, g.qcap);
+    const KDLayout<B> L = KDLayout<B>::make(n, g.rc, KD_RR);
     KDSmall* sm = reinterpret_cast<KDSmall*>(smem);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    unsigned char* wflag = reinterpret_cast<unsigned char*>(smem + L.wflag) + wid * 64;
+    unsigned char* wmark = reinterpret_cast<unsigned char*>(smem + L.wmark) + wid * 64 * KD_P;
     unsigned long long* wkey = reinterpret_cast<unsigned long long*>(smem + L.wkey) + wid * 64;
     uint16_t* dist = reinterpret_cast<uint16_t*>(smem + L.dist);
     unsigned long long* pend = reinterpret_cast<unsigned long long*>(smem + L.pend);
     unsigned* wmin = reinterpret_cast<unsigned*>(smem + L.wmin);
     unsigned long long* fix = reinterpret_cast<unsigned long long*>(smem + L.fix);
-    uint16_t* queue = reinterpret_cast<uint16_t*>(smem + L.queue);
+    unsigned long long* inq = reinterpret_cast<unsigned long long*>(smem + L.inq);
+    uint16_t* ring = reinterpret_cast<uint16_t*>(smem + L.ring);
+    uint2* rrec = reinterpret_cast<uint2*>(smem + L.rrec);
+    uint16_t* qv = reinterpret_cast<uint16_t*>(smem + L.qv);
+    int* qbeg = reinterpret_cast<int*>(smem + L.qbeg);
     const unsigned bound = (unsigned)g.bound;
     const unsigned delta = (unsigned)g.delta;
+    const int qcap = L.qcap;
+    const int rc = g.rc;
+    constexpr int NW = B / 64;
+    const bool writer = wid == NW - 1;  // drains parent records; never waits on a global load
     double* relv = reinterpret_cast<double*>(ws + (size_t)blockIdx.x * ws_stride);
-    uint16_t* wpar = reinterpret_cast<uint16_t*>(ws + (size_t)blockIdx.x * ws_stride + a16(sizeof(double) * n));
-    wflag[lane] = 0;
+    uint32_t* wpr = reinterpret_cast<uint32_t*>(ws + (size_t)blockIdx.x * ws_stride + a16(sizeof(double) * n));
+    for (int q = lane; q < 64 * KD_P; q += 64) wmark[q] = 0;
+#ifdef SHD_STAMPS
+    if (tid < 32) sm->acc[tid] = 0;
+    __syncthreads();
+#endif
+    const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
 
     for (int i = blockIdx.x; i < ns; i += gridDim.x) {
         const int s = src[i];
@@ -153,13 +219,12 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
         const double fs = g.vf[s];
         const double cs = isnan(fs) ? 1.0 : 1.0 * fs;
         for (int v = tid; v < (n + 2) / 2; v += B) reinterpret_cast<uint32_t*>(dist)[v] = 0xFFFFFFFFu;
-        for (int k = tid; k < nw; k += B) { pend[k] = 0ull; wmin[k] = 0xFFFFFFFFu; fix[k] = 0ull; }
+        for (int k = tid; k < nw; k += B) { pend[k] = 0ull; inq[k] = 0ull; wmin[k] = 0xFFFFFFFFu; fix[k] = 0ull; }
+        for (int q = tid; q < KD_RR; q += B) rrec[q] = make_uint2(0u, 0xFFFFFFFFu);  // phases B/C reuse the area
         if (tid == 0) {
             sm->gmin[0] = sm->gmin[1] = 0xFFFFFFFFu;
-            sm->qtail[0] = sm->qtail[1] = 0;
-            sm->qcur[0] = sm->qcur[1] = 0;
-            wpar[s] = (uint16_t)s;
-            relv[s] = cs;
+            sm->rtail = sm->rdone = 0;
+            wpr[s] = KD_SRC_MARK;
         }
         lds_barrier();
         if (tid == 0) {
@@ -169,9 +234,21 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
         }
         lds_barrier();
 
-        // ---- A: delta-stepping ----------------------------------------------------
+        // ---- A: delta-stepping, asynchronous inside a bucket ------------------------
+        // Bucket round: (1) T from the min pending distance; (2) gather the pending vertices
+        // with dist < T into the work queue; (3) compute waves pull 64-entry slices from the
+        // queue and push every vertex they improve below T straight back (deduplicated by
+        // the inq bits), so a bucket's light-arc chains need no barriers; far improvements
+        // and queue overflow go to the pending bitmask.  The last wave is the writer: it
+        // drains the slices' parent records into wpr (HBM) so compute waves never wait on a
+        // store.  A round ends when no wave holds a slice and the queue is empty.
         unsigned T = delta;
         int par = 0;
+        const int ncomp = NW - 1;
+#ifdef SHD_STAMPS
+        unsigned long long kd_t = 0;
+#endif
+        KD_MARK();
         for (;;) {
             KD_COUNT(5, tid == 0 ? 1 : 0);
             {
@@ -180,12 +257,14 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                 const unsigned wm = kd_wave_min(m0);
                 if (lane == 0 && wm != 0xFFFFFFFFu) atomicMin(&sm->gmin[par], wm);
             }
+            for (int q = tid; q < rc; q += B) ring[q] = 0xFFFFu;
+            if (tid == 0) { sm->gmin[par ^ 1] = 0xFFFFFFFFu; sm->head = sm->tail = 0; sm->busy = 0; sm->nexit = 0; }
             lds_barrier();
             const unsigned m = sm->gmin[par];
             if (m == 0xFFFFFFFFu) break;
             if (m >= T) T = (m / delta + 1) * delta;
-            if (tid == 0) { sm->gmin[par ^ 1] = 0xFFFFFFFFu; sm->qtail[par ^ 1] = 0; sm->qcur[par ^ 1] = 0; }
-            // gather: move pending vertices with dist < T into the queue (one thread per word)
+            KD_ACC(11);
+            // gather: pending vertices with dist < T into the queue (one thread per word)
             for (int k0 = 0; k0 < nw; k0 += B) {
                 const int k = k0 + tid;
                 unsigned long long bits = 0ull, take = 0ull;
@@ -194,12 +273,18 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                 if (act) {
                     bits = pend[k];
                     unsigned long long b = bits;
-                    while (b) {
-                        const int bi = __ffsll((long long)b) - 1;
-                        b &= b - 1;
-                        const unsigned du = dist[(k << 6) + bi];
-                        if (du < T) take |= 1ull << bi;
-                        else rest = min(rest, du);
+                    while (b) {  // four bits per trip: independent LDS reads in flight
+                        int v4[4];
+                        pop4(&b, k, v4);
+                        unsigned d4[4];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) d4[q] = ld16(dist, v4[q] >= 0 ? v4[q] : n);
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            if (v4[q] < 0) continue;
+                            if (d4[q] < T) take |= 1ull << (v4[q] & 63);
+                            else rest = min(rest, d4[q]);
+                        }
                     }
                 }
                 const int cnt = __popcll(take);
@@ -210,7 +295,7 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                     if (lane >= d) incl += y;
                 }
                 int base = 0;
-                if (lane == 63 && incl) base = atomicAdd(&sm->qtail[par], incl);
+                if (lane == 63 && incl) base = atomicAdd(&sm->tail, incl);
                 base = __shfl(base, 63, 64);
                 int pos = base + incl - cnt;
                 if (act) {
@@ -219,126 +304,398 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                         const int bi = __ffsll((long long)b) - 1;
                         b &= b - 1;
                         const int u = (k << 6) + bi;
-                        if (pos < g.qcap) queue[pos] = (uint16_t)u;
+                        if (pos < rc) ring[pos] = (uint16_t)u;
                         else { take &= ~(1ull << bi); rest = min(rest, (unsigned)dist[u]); }
                         pos++;
                     }
                     pend[k] = bits & ~take;
+                    inq[k] = take;
                     wmin[k] = rest;
                 }
             }
             lds_barrier();
-            const int qn = min(sm->qtail[par], g.qcap);
-            KD_COUNT(6, tid == 0 ? qn : 0);
-            bool stored = false;
-            // expand: waves take 64-vertex slices of the queue
-            for (;;) {
-                int sl = 0;
-                if (lane == 0) sl = atomicAdd(&sm->qcur[par], 1);
-                sl = __shfl(sl, 0, 64);
-                const int nsl = (qn + 63) >> 6;
-                if (sl >= nsl) break;
-                const int j = sl + nsl * lane;  // strided: the hubs (low ids, gathered first) spread over slices
-                const bool act = j < qn;
-                const int u = act ? (int)queue[j] : 0;
-                const unsigned du = act ? (unsigned)dist[u] : 0u;
-                int beg = 0, deg = 0;
-                if (act) { beg = g.row[u]; deg = g.row[u + 1] - beg; }
-                int incl = deg;
+            if (tid == 0) sm->tail = min(sm->tail, rc);
+            lds_barrier();
+            KD_ACC(8);
+            if (!writer) {
+                // ---- compute wave: pull slices until the round drains ----------------
+                int spins = 0;
+                for (;;) {
+                    int h = 0, nn = 0;
+                    if (lane == 0) {
+                        // idle waves only read: busy is raised just around a real grab, so an
+                        // idle wave never hides the all-idle state from the others
+                        if (__hip_atomic_load(&sm->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >
+                            __hip_atomic_load(&sm->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                            atomicAdd(&sm->busy, 1);
+                            h = __hip_atomic_load(&sm->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            const int t = __hip_atomic_load(&sm->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            nn = min(64, t - h);
+                            if (nn > 0 && atomicCAS(&sm->head, h, h + nn) != h) nn = 0;
+                            if (nn <= 0) { nn = 0; atomicSub(&sm->busy, 1); }
+                        }
+                    }
+                    nn = __builtin_amdgcn_readfirstlane(nn);
+                    h = __builtin_amdgcn_readfirstlane(h);
+                    if (nn == 0) {
+                        int fin = 0;
+                        if (lane == 0) {
+                            const int bz = __hip_atomic_load(&sm->busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            const int t = __hip_atomic_load(&sm->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            const int hh = __hip_atomic_load(&sm->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            fin = bz == 0 && hh == t;
+                        }
+                        if (__builtin_amdgcn_readfirstlane(fin)) break;
+                        if (++spins > (1 << 22)) { if (lane == 0) raise_err(err, SHD_ROUTE_EDEVICE); break; }
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    spins = 0;
+                    // the slice: queue entries [h, h+nn), written right after reservation
+                    const bool act = lane < nn;
+                    int u = 0;
+                    if (act) {
+                        volatile uint16_t* slot = ring + h + lane;
+                        unsigned x = *slot;
+                        for (int w8 = 0; x == 0xFFFFu && w8 < (1 << 22); w8++) { __builtin_amdgcn_s_sleep(1); x = *slot; }
+                        if (x == 0xFFFFu) raise_err(err, SHD_ROUTE_EDEVICE);
+                        u = x == 0xFFFFu ? s : (int)x;
+                        atomicAnd(&inq[u >> 6], ~(1ull << (u & 63)));
+                    }
+                    const unsigned du = act ? ld16(dist, u) : 0u;
+                    int beg = 0, deg = 0;
+                    {
+                        const int r0 = g.row[u], r1 = g.row[u + 1];
+                        if (act) { beg = r0; deg = r1 - r0; }
+                    }
+                    int incl = deg;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const int y = __shfl_up(incl, d, 64);
+                        if (lane >= d) incl += y;
+                    }
+                    const int total = __shfl(incl, 63, 64);
+                    const int excl = incl - deg;
+                    const int boff = beg - excl;
+                    if (g.fused) wkey[lane] = ~0ull;
+                    for (int base0 = 0; base0 < total; base0 += 64 * KD_P) {
+                        // owners: each lane whose row starts inside the window marks its start
+                        const int pos = excl - base0;
+                        const bool mark = deg > 0 && pos >= 0 && pos < 64 * KD_P;
+                        if (mark) wmark[pos] = (unsigned char)(lane + 1);
+                        __builtin_amdgcn_wave_barrier();
+                        int fl[KD_P];
+#pragma unroll
+                        for (int p = 0; p < KD_P; p++) fl[p] = wmark[64 * p + lane];
+                        uint2 rec[KD_P];
+                        unsigned od[KD_P];
+                        int oo[KD_P], aa[KD_P], ps[KD_P];
+                        // staged so the cross-lane reads of all steps issue back to back
+                        int pp[KD_P], cl[KD_P];
+                        bool bel[KD_P];
+#pragma unroll
+                        for (int p = 0; p < KD_P; p++) {
+                            const int base = base0 + 64 * p;
+                            const unsigned long long M = __ballot(fl[p] != 0);
+                            const unsigned long long carry_m = __ballot(deg > 0 && excl < base && incl > base);
+                            const unsigned long long below = M & upto;
+                            bel[p] = below != 0ull;
+                            pp[p] = bel[p] ? 63 - __clzll((long long)below) : 0;
+                            cl[p] = carry_m ? __ffsll((long long)carry_m) - 1 : 0;
+                        }
+                        int via[KD_P];
+#pragma unroll
+                        for (int p = 0; p < KD_P; p++) via[p] = __builtin_amdgcn_ds_bpermute(pp[p] << 2, fl[p]) - 1;
+#pragma unroll
+                        for (int p = 0; p < KD_P; p++) oo[p] = bel[p] ? via[p] : cl[p];
+                        int ob[KD_P], ox[KD_P];
+#pragma unroll
+                        for (int p = 0; p < KD_P; p++) {
+                            ob[p] = __builtin_amdgcn_ds_bpermute(oo[p] << 2, boff);
+                            od[p] = (unsigned)__builtin_amdgcn_ds_bpermute(oo[p] << 2, (int)du);
+                            ox[p] = __builtin_amdgcn_ds_bpermute(oo[p] << 2, excl);
+                        }
+#pragma unroll
+                        for (int p = 0; p < KD_P; p++) {
+                            const int e = base0 + 64 * p + lane;
+                            ps[p] = e - ox[p];  // position in the owner's row
+                            aa[p] = e < total ? ob[p] + e : -1;
+                            rec[p] = g.orec[e < total ? ob[p] + e : 0];
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        if (mark) wmark[pos] = 0;
+                        // relax: all dist words read, all CAS attempts issued, then results checked
+                        uint32_t* dist32 = reinterpret_cast<uint32_t*>(dist);
+                        uint32_t wd[KD_P];
+#pragma unroll
+                        for (int p = 0; p < KD_P; p++) wd[p] = dist32[(rec[p].x & 0xFFFFu) >> 1];
+                        unsigned dv[KD_P], nd[KD_P];
+                        bool want[KD_P];
+#pragma unroll
+                        for (int p = 0; p < KD_P; p++) {
+                            const unsigned v = rec[p].x & 0xFFFFu;
+                            dv[p] = (wd[p] >> ((v & 1u) * 16)) & 0xFFFFu;
+                            nd[p] = od[p] + (rec[p].x >> 16);
+                            want[p] = aa[p] >= 0 && nd[p] < dv[p] && nd[p] <= bound;
+                        }
+                        uint32_t prev[KD_P];
+#pragma unroll
+                        for (int p = 0; p < KD_P; p++) {
+                            const unsigned v = rec[p].x & 0xFFFFu, sh = (v & 1u) * 16;
+                            prev[p] = want[p] ? atomicCAS(&dist32[v >> 1], wd[p], (wd[p] & ~(0xFFFFu << sh)) | (nd[p] << sh))
+                                              : wd[p];
+                        }
+                        bool push[KD_P];
+#pragma unroll
+                        for (int p = 0; p < KD_P; p++) {
+                            push[p] = false;
+                            if (!want[p]) continue;
+                            const unsigned v = rec[p].x & 0xFFFFu, sh = (v & 1u) * 16;
+                            bool won = prev[p] == wd[p];
+                            uint32_t old = prev[p];
+                            while (!won) {  // lost a race on the word: retry while still an improvement
+                                if (nd[p] >= ((old >> sh) & 0xFFFFu)) break;
+                                const uint32_t got = atomicCAS(&dist32[v >> 1], old, (old & ~(0xFFFFu << sh)) | (nd[p] << sh));
+                                won = got == old;
+                                old = got;
+                            }
+                            if (!won) continue;
+                            const unsigned long long bit = 1ull << (v & 63);
+                            if (nd[p] < T) {
+                                push[p] = !(atomicOr(&inq[v >> 6], bit) & bit);
+                                if (push[p]) atomicAnd(&pend[v >> 6], ~bit);  // one copy: the queue's
+                            }
+                            else { atomicOr(&pend[v >> 6], bit); atomicMin(&wmin[v >> 6], nd[p]); }
+                        }
+                        // one queue reservation for all the group's pushes
+                        int cpre[KD_P], ctot = 0;
+#pragma unroll
+                        for (int p = 0; p < KD_P; p++) { cpre[p] = ctot; ctot += __popcll(__ballot(push[p])); }
+                        if (ctot) {
+                            int qb = 0, qk = 0;
+                            if (lane == 0) {
+                                for (;;) {
+                                    const int t = __hip_atomic_load(&sm->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    qk = min(ctot, rc - t);
+                                    if (qk <= 0) { qk = 0; break; }
+                                    if (atomicCAS(&sm->tail, t, t + qk) == t) { qb = t; break; }
+                                }
+                            }
+                            qb = __builtin_amdgcn_readfirstlane(qb);
+                            qk = __builtin_amdgcn_readfirstlane(qk);
+#pragma unroll
+                            for (int p = 0; p < KD_P; p++) {
+                                const unsigned long long bm = __ballot(push[p]);
+                                if (!push[p]) continue;
+                                const int rk = cpre[p] + __popcll(bm & (upto >> 1));
+                                const unsigned v = rec[p].x & 0xFFFFu;
+                                if (rk < qk) ring[qb + rk] = (uint16_t)v;
+                                else {  // queue full: back to the pending bitmask
+                                    atomicAnd(&inq[v >> 6], ~(1ull << (v & 63)));
+                                    atomicOr(&pend[v >> 6], 1ull << (v & 63));
+                                    atomicMin(&wmin[v >> 6], nd[p]);
+                                }
+                            }
+                        }
+#pragma unroll
+                        for (int p = 0; p < KD_P; p++) {
+                            // tie rule: largest w, then smallest (parent, eid) = row position
+                            const unsigned w = rec[p].x >> 16;
+                            if (g.fused && aa[p] >= 0 && dv[p] + w == od[p])
+                                atomicMin(&wkey[oo[p]], ((unsigned long long)(0xFFFFu - w) << 48) |
+                                                            ((unsigned long long)ps[p] << 32) |
+                                                            ((rec[p].x & 0xFFFFu) << 16) | (rec[p].y & 0xFFFFu));
+                        }
+                    }
+                    KD_COUNT(7, total);
+                    KD_COUNT(6, nn);
+                    __builtin_amdgcn_wave_barrier();
+                    // parent records {winner, u | du << 16} to the writer's ring
+                    const bool hasrec = act && u != s;
+                    uint32_t prec = KD_NONE;
+                    if (g.fused && hasrec) {
+                        const unsigned long long kk = wkey[lane];
+                        if (kk != ~0ull && (0xFFFFu - (unsigned)(kk >> 48)) >= delta) prec = (uint32_t)kk;
+                    }
+                    const unsigned long long rm = __ballot(hasrec);
+                    const int nr = __popcll(rm);
+                    if (nr) {
+                        int rb = 0;
+                        if (lane == 0) {
+                            rb = atomicAdd(&sm->rtail, nr);
+                            for (int w8 = 0; rb + nr - __hip_atomic_load(&sm->rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > KD_RR
+                                             && w8 < (1 << 22); w8++)
+                                __builtin_amdgcn_s_sleep(1);
+                        }
+                        rb = __builtin_amdgcn_readfirstlane(rb);
+                        if (hasrec) {  // one 64-bit LDS write: the writer never sees half a record
+                            const int slot = (rb + __popcll(rm & (upto >> 1))) & (KD_RR - 1);
+                            *reinterpret_cast<volatile unsigned long long*>(&rrec[slot]) =
+                                (unsigned long long)prec | ((unsigned long long)((uint32_t)u | (du << 16)) << 32);
+                        }
+                    }
+                    if (lane == 0) atomicSub(&sm->busy, 1);
+                }
+                if (lane == 0) atomicAdd(&sm->nexit, 1);
+            } else {
+                // ---- writer wave: parent records -> wpr (HBM) + fix bits -------------
+                int rd = __hip_atomic_load(&sm->rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                int spins = 0;
+                for (;;) {
+                    const int rt = __hip_atomic_load(&sm->rtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (rt > rd) {
+                        const int k = min(64, rt - rd);
+                        if (lane < k) {
+                            const int slot = (rd + lane) & (KD_RR - 1);
+                            volatile unsigned long long* sp = reinterpret_cast<volatile unsigned long long*>(&rrec[slot]);
+                            unsigned long long rv = *sp;
+                            for (int w8 = 0; (rv >> 32) == 0xFFFFFFFFull && w8 < (1 << 22); w8++) {
+                                __builtin_amdgcn_s_sleep(1);
+                                rv = *sp;
+                            }
+                            const uint32_t x = (uint32_t)rv, y = (uint32_t)(rv >> 32);
+                            *sp = 0xFFFFFFFF00000000ull;
+                            const int u = (int)(y & 0xFFFFu);
+                            if (y != 0xFFFFFFFFu && ld16(dist, u) == (y >> 16)) {  // from u's latest expansion
+                                const unsigned long long bit = 1ull << (u & 63);
+                                if (x != KD_NONE) { wpr[u] = x; atomicAnd(&fix[u >> 6], ~bit); }
+                                else atomicOr(&fix[u >> 6], bit);
+                            }
+                        }
+                        rd += k;
+                        __builtin_amdgcn_wave_barrier();
+                        if (lane == 0) __hip_atomic_store(&sm->rdone, rd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        spins = 0;
+                        continue;
+                    }
+                    if (__hip_atomic_load(&sm->nexit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == ncomp &&
+                        __hip_atomic_load(&sm->rtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == rd)
+                        break;
+                    if (++spins > (1 << 22)) { if (lane == 0) raise_err(err, SHD_ROUTE_EDEVICE); break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            par ^= 1;
+            lds_barrier();
+            KD_ACC(10);
+        }
+        wait_stores();  // the writer's records land before phase B rewrites fixed-up vertices
+        lds_barrier();
+        KD_STAMP(1);
+        KD_MARK();
+
+        // ---- B: fix-ups (first tight arc of the light in-row tail) ---------------------
+        // rounds over a compacted list (qv) so all threads share the work evenly; per entry
+        // the row bounds and KD_TAIL tail arcs are loaded straight-line, long tails are
+        // re-queued (qbeg) for one wave per vertex
+        const int last_arc = g.nlight > 0 ? g.nlight - 1 : 0;
+        if (tid == 0) {
+            fix[s >> 6] &= ~(1ull << (s & 63));
+            sm->qtail[0] = sm->qtail[1] = 0;
+            sm->qcur[0] = sm->qcur[1] = 0;
+        }
+        for (int rnd = 0;; rnd ^= 1) {
+            if (tid == 0) { sm->qtail[rnd ^ 1] = 0; sm->qcur[rnd ^ 1] = 0; }
+            lds_barrier();
+            for (int k0 = 0; k0 < nw; k0 += B) {
+                const int k = k0 + tid;
+                unsigned long long bits = k < nw ? fix[k] : 0ull;
+                const int cnt = __popcll(bits);
+                int incl = cnt;
 #pragma unroll
                 for (int d = 1; d < 64; d <<= 1) {
                     const int y = __shfl_up(incl, d, 64);
                     if (lane >= d) incl += y;
                 }
-                const int total = __shfl(incl, 63, 64);
-                const int excl = incl - deg;
-                const int boff = beg - excl;
-                if (g.fused) wkey[lane] = ~0ull;
-                const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-                for (int base0 = 0; base0 < total; base0 += 64 * KD_P) {
-                    uint32_t rec[KD_P];
-                    unsigned od[KD_P];
-                    int oo[KD_P], aa[KD_P];
-#pragma unroll
-                    for (int p = 0; p < KD_P; p++) {
-                        const int base = base0 + 64 * p;
-                        rec[p] = 0u; od[p] = 0u; oo[p] = 0; aa[p] = -1;
-                        if (base < total) {
-                            // owner of arc position base+lane = last lane starting at or before it
-                            const int pos = excl - base;
-                            if (deg > 0 && pos >= 0 && pos < 64) wflag[pos] = (unsigned char)(lane + 1);
-                            __builtin_amdgcn_wave_barrier();
-                            const int fl = wflag[lane];
-                            const unsigned long long M = __ballot(fl != 0);
-                            wflag[lane] = 0;
-                            const unsigned long long carry_m = __ballot(deg > 0 && excl < base && incl > base);
-                            const unsigned long long below = M & upto;
-                            const int pp = below ? 63 - __clzll((long long)below) : 0;
-                            const int via = __shfl(fl, pp, 64) - 1;
-                            const int o = below ? via : (carry_m ? __ffsll((long long)carry_m) - 1 : 0);
-                            const int ob = __shfl(boff, o, 64);
-                            od[p] = (unsigned)__shfl((int)du, o, 64);
-                            oo[p] = o;
-                            const int e = base + lane;
-                            if (e < total) { aa[p] = ob + e; rec[p] = g.oarc[ob + e]; }
-                        }
-                    }
-#pragma unroll
-                    for (int p = 0; p < KD_P; p++) {
-                        if (aa[p] < 0) continue;
-                        const int v = (int)(rec[p] >> 16);
-                        const unsigned w = rec[p] & 0xFFFFu;
-                        const unsigned nd = od[p] + w;
-                        const unsigned dv = dist[v];
-                        if (nd < dv && nd <= bound && kd_lower(dist, v, nd)) {
-                            atomicOr(&pend[v >> 6], 1ull << (v & 63));
-                            atomicMin(&wmin[v >> 6], nd);
-                        }
-                        if (g.fused && dv + w == od[p])
-                            atomicMin(&wkey[oo[p]], ((unsigned long long)(0xFFFFu - w) << 32) | (unsigned)aa[p]);
-                    }
+                int base = 0;
+                if (lane == 63 && incl) base = atomicAdd(&sm->qtail[rnd], incl);
+                base = __shfl(base, 63, 64);
+                int pos = base + incl - cnt;
+                unsigned long long b = bits, listed = 0ull;
+                while (b && pos < qcap) {
+                    const int bi = __ffsll((long long)b) - 1;
+                    b &= b - 1;
+                    qv[pos++] = (uint16_t)((k << 6) + bi);
+                    listed |= 1ull << bi;
                 }
-                KD_COUNT(7, lane == 0 ? total : 0);
-                __builtin_amdgcn_wave_barrier();
-                if (act && u != s) {
-                    bool heavy = false;
-                    if (g.fused) {
-                        const unsigned long long kk = wkey[lane];
-                        if (kk != ~0ull && (0xFFFFu - (unsigned)(kk >> 32)) >= delta) {
-                            heavy = true;
-                            const int a = (int)(kk & 0xFFFFFFFFull);
-                            wpar[u] = (uint16_t)(g.oarc[a] >> 16);
-                            relv[u] = -g.r_out[a];
-                            stored = true;
-                        }
-                    }
-                    if (heavy) atomicAnd(&fix[u >> 6], ~(1ull << (u & 63)));
-                    else atomicOr(&fix[u >> 6], 1ull << (u & 63));
-                }
+                if (listed) fix[k] = bits & ~listed;
             }
-            // a later expansion of the same vertex (next sweeps, another wave) must land after this one
-            if (stored) wait_stores();
-            par ^= 1;
             lds_barrier();
-        }
-        KD_STAMP(1);
-
-        // ---- B: fix-ups (parents over light in-arcs) + lat row --------------------
-        for (int v = tid; v < n; v += B) {
-            if (v == s || !((fix[v >> 6] >> (v & 63)) & 1ull)) continue;
-            const unsigned dv = dist[v];
-            const int r1 = g.row_in[v + 1];
-            int found = -1;
-            for (int a = g.lstart[v]; a < r1; a++) {
-                const uint32_t rec = g.iarc[a];
-                if ((unsigned)dist[rec >> 16] + (rec & 0xFFFFu) == dv) { found = a; break; }
+            const int cnt = min(sm->qtail[rnd], qcap);
+            if (cnt == 0) break;
+            for (int j0 = 0; j0 < cnt; j0 += B * 4) {
+                int v4[4], a4[4], r4[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int j = j0 + q * B + tid;
+                    v4[q] = j < cnt ? (int)qv[j] : -1;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int vv = v4[q] >= 0 ? v4[q] : 0;
+                    a4[q] = g.lrow[vv];
+                    r4[q] = g.lrow[vv + 1];
+                }
+                uint2 rc[4][KD_TAIL];
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+#pragma unroll
+                    for (int e = 0; e < KD_TAIL; e++) rc[q][e] = g.lrec[min(a4[q] + e, last_arc)];
+                unsigned dt[4][KD_TAIL], d4[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    d4[q] = ld16(dist, v4[q] >= 0 ? v4[q] : 0);
+#pragma unroll
+                    for (int e = 0; e < KD_TAIL; e++) dt[q][e] = ld16(dist, (int)(rc[q][e].x & 0xFFFFu));
+                }
+                uint32_t out_a[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    int f = -1;
+#pragma unroll
+                    for (int e = KD_TAIL - 1; e >= 0; e--)
+                        if (a4[q] + e < r4[q] && dt[q][e] + (rc[q][e].x >> 16) == d4[q]) f = e;
+                    uint32_t fr = rc[q][0].x << 16 | (rc[q][0].y & 0xFFFFu);
+#pragma unroll
+                    for (int e = 1; e < KD_TAIL; e++)
+                        if (f == e) fr = rc[q][e].x << 16 | (rc[q][e].y & 0xFFFFu);
+                    out_a[q] = f >= 0 ? fr : KD_NONE;
+                    if (v4[q] >= 0 && f < 0) {
+                        if (r4[q] - a4[q] > KD_TAIL) {  // long tail: one wave per vertex below
+                            const int at = atomicAdd(&sm->qcur[rnd], 1);
+                            qbeg[at] = v4[q];  // at < cnt <= qcap
+                            v4[q] = -1;
+                        } else raise_err(err, SHD_ROUTE_EUNREACH);
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (v4[q] >= 0) wpr[v4[q]] = out_a[q];
             }
-            if (found < 0) { raise_err(err, SHD_ROUTE_EUNREACH); wpar[v] = 0xFFFFu; relv[v] = -1.0; }
-            else { wpar[v] = (uint16_t)(g.iarc[found] >> 16); relv[v] = -g.r_in[found]; }
+            lds_barrier();
+            const int nlong = sm->qcur[rnd];
+            for (int j = wid; j < nlong; j += B / 64) {
+                const int v = qbeg[j];
+                const unsigned dv = ld16(dist, v);
+                const int r1 = g.lrow[v + 1];
+                uint32_t fr = KD_NONE;
+                for (int a0 = g.lrow[v] + KD_TAIL; a0 < r1 && fr == KD_NONE; a0 += 64) {
+                    const int a = a0 + lane;
+                    const uint2 rc = g.lrec[min(a, last_arc)];
+                    const bool tight = a < r1 && ld16(dist, (int)(rc.x & 0xFFFFu)) + (rc.x >> 16) == dv;
+                    const unsigned long long tm = __ballot(tight);
+                    const uint32_t mine = rc.x << 16 | (rc.y & 0xFFFFu);
+                    if (tm) fr = (uint32_t)__shfl((int)mine, __ffsll((long long)tm) - 1, 64);
+                }
+                if (lane == 0) {
+                    if (fr == KD_NONE) raise_err(err, SHD_ROUTE_EUNREACH);
+                    wpr[v] = fr;
+                }
+            }
         }
+        KD_ACC(16);
+        KD_ACC(17);
         KD_STAMP(2);
-        wait_stores();
-        __syncthreads();
         double* lrow = lat_out ? lat_out + (long long)i * ld : nullptr;
         double* rrow = rel_out ? rel_out + (long long)i * ld : nullptr;
         double lmin = INFINITY;
@@ -354,57 +711,146 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
             else { Lv = (double)dist[t]; lmin = fmin(lmin, Lv); }
             if (lrow) __builtin_nontemporal_store(Lv, lrow + j);
         }
-        lds_barrier();
-        // dist is dead: its LDS becomes the parent array
-        uint16_t* parv = dist;
-        for (int v = tid; v < n; v += B) parv[v] = wpar[v];
+        wait_stores();  // wpr of phase B visible to the whole workgroup
         __syncthreads();
+        KD_ACC(18);
+        // dist is dead: its LDS becomes the parent array; wpr decodes into (parent, -r)
+        uint16_t* parv = dist;
+        for (int v0 = tid; v0 < n; v0 += B * 8) {
+            uint32_t pr[8];
+            double rr[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) pr[q] = wpr[min(v0 + q * B, n - 1)];
+#pragma unroll
+            for (int q = 0; q < 8; q++) rr[q] = g.rtab[pr[q] >= KD_SRC_MARK ? 0 : min((int)(pr[q] & 0xFFFFu), g.nrtab - 1)];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int v = v0 + q * B;
+                if (v >= n) continue;
+                const bool src_v = pr[q] == KD_SRC_MARK;
+                parv[v] = src_v ? (uint16_t)v : (uint16_t)(pr[q] >> 16);
+                relv[v] = src_v ? cs : -rr[q];
+            }
+        }
+        for (int k = tid; k < nw; k += B) {
+            unsigned long long mk = (k == nw - 1 && (n & 63)) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+            if (k == (s >> 6)) mk &= ~(1ull << (s & 63));
+            pend[k] = mk;
+            fix[k] = 0ull;
+        }
+        wait_stores();
+        __syncthreads();
+        KD_ACC(19);
 
-        // ---- C: reliability down the tree (relv in the HBM slice) -----------------
-        for (;;) {
-            if (tid == 0) sm->flag = 0;
-            __syncthreads();
-            int progressed = 0;
-            for (int v0 = tid; v0 < n; v0 += B * 4) {
-                double x[4], rp[4];
-                uint16_t p[4];
+        if (tid == 0) sm->qtail[0] = sm->qtail[1] = 0;
+        lds_barrier();
+        // ---- C: reliability down the tree ------------------------------------------
+        // per level: pending vertices whose parent is done are compacted into qv, then one
+        // thread per listed vertex loads relv[parent] and its own -r and stores the product
+        for (int c = 0;; c ^= 1) {
+            KD_COUNT(12, tid == 0 ? 1 : 0);
+            if (tid == 0) sm->qtail[c ^ 1] = 0;
+            for (int k0 = 0; k0 < nw; k0 += B) {
+                const int k = k0 + tid;
+                unsigned long long b = k < nw ? pend[k] : 0ull, ready = 0ull;
+                while (b) {  // ready = pending vertices whose parent is done (LDS only)
+                    int v4[4];
+                    pop4(&b, k, v4);
+                    int p4[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) p4[q] = (int)parv[v4[q] >= 0 ? v4[q] : 0];
+                    unsigned long long pw[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) pw[q] = pend[p4[q] >> 6];
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        if (v4[q] >= 0 && !((pw[q] >> (p4[q] & 63)) & 1ull)) ready |= 1ull << (v4[q] & 63);
+                }
+                const int cnt = __popcll(ready);
+                int incl = cnt;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const int y = __shfl_up(incl, d, 64);
+                    if (lane >= d) incl += y;
+                }
+                int base = 0;
+                if (lane == 63 && incl) base = atomicAdd(&sm->qtail[c], incl);
+                base = __shfl(base, 63, 64);
+                int pos = base + incl - cnt;
+                unsigned long long listed = 0ull;
+                b = ready;
+                while (b && pos < qcap) {
+                    const int bi = __ffsll((long long)b) - 1;
+                    b &= b - 1;
+                    qv[pos++] = (uint16_t)((k << 6) + bi);
+                    listed |= 1ull << bi;
+                }
+                if (k < nw) fix[k] = listed;
+            }
+            lds_barrier();
+            KD_ACC(13);
+            const int cnt = min(sm->qtail[c], qcap);
+            if (cnt == 0) break;
+            for (int j0 = 0; j0 < cnt; j0 += B * 4) {
+                int v4[4], p4[4];
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
-                    const int v = v0 + q * B;
-                    x[q] = v < n ? relv[v] : 0.0;
-                    p[q] = v < n ? parv[v] : (uint16_t)0xFFFFu;
+                    const int j = j0 + q * B + tid;
+                    v4[q] = j < cnt ? (int)qv[j] : -1;
+                    p4[q] = (int)parv[v4[q] >= 0 ? v4[q] : 0];
+                }
+                double xp[4], xv[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    xp[q] = relv[p4[q]];
+                    xv[q] = relv[v4[q] >= 0 ? v4[q] : 0];
                 }
 #pragma unroll
                 for (int q = 0; q < 4; q++)
-                    rp[q] = (signbit(x[q]) && p[q] != 0xFFFFu) ? relv[p[q]] : -1.0;
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    if (!signbit(rp[q])) { relv[v0 + q * B] = rp[q] * (-x[q]); progressed = 1; }
+                    if (v4[q] >= 0) relv[v4[q]] = xp[q] * (-xv[q]);
             }
-            if (progressed) sm->flag = 1;
-            __syncthreads();
-            const int again = sm->flag;
-            __syncthreads();
-            if (!again) break;
+            wait_stores();  // this level's relv visible before its vertices count as done
+            KD_ACC(14);
+            lds_barrier();
+            for (int k = tid; k < nw; k += B) {
+                const unsigned long long r = fix[k];
+                if (r) pend[k] &= ~r;
+            }
+            lds_barrier();
+            KD_ACC(15);
         }
-        wait_stores();  // relv must land before phase D reads it and the next source rewrites it
         KD_STAMP(3);
 
         // ---- D: rel row out + row min ----------------------------------------------
         if (tid == 0) sm->rmin = kInfBits;
         __syncthreads();
         if (rrow) {
-            for (int j = tid; j < nt; j += B) {
-                const int t = tgt[j];
-                double Rv = NAN;
-                if (t >= 0 && t < n) {
-                    if (t == s) Rv = isnan(g.self_w[s]) ? NAN : cs * g.self_r[s];
-                    else {
-                        const double ft = g.vf[t];
-                        Rv = isnan(ft) ? relv[t] : relv[t] * ft;
-                    }
+            for (int j0 = tid; j0 < nt; j0 += B * 4) {
+                int t4[4];
+                double x4[4], f4[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int j = j0 + q * B;
+                    t4[q] = j < nt ? tgt[j] : s;
                 }
-                __builtin_nontemporal_store(Rv, rrow + j);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int t = (t4[q] >= 0 && t4[q] < n) ? t4[q] : s;
+                    x4[q] = relv[t];
+                    f4[q] = g.vf[t];
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int j = j0 + q * B;
+                    if (j >= nt) continue;
+                    const int t = t4[q];
+                    double Rv = NAN;
+                    if (t >= 0 && t < n) {
+                        if (t == s) Rv = isnan(g.self_w[s]) ? NAN : cs * g.self_r[s];
+                        else Rv = isnan(f4[q]) ? x4[q] : x4[q] * f4[q];
+                    }
+                    __builtin_nontemporal_store(Rv, rrow + j);
+                }
             }
         }
         if (row_min) {
@@ -416,10 +862,11 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
         }
         lds_barrier();
         KD_STAMP(4);
+        KD_FLUSH();
     }
 }
 
 template <int B>
-inline size_t kd_lds_bytes(int n, int qcap) { return KDLayout<B>::make(n, qcap).total; }
+inline size_t kd_lds_bytes(int n, int rc) { return KDLayout<B>::make(n, rc, KD_RR).total; }
 
 }  // namespace shd

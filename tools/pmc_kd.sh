@@ -1,0 +1,23 @@
+#!/bin/bash
+# PMC passes for the KD kernel on C4 (one counter group per rocprofv3 run).
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/pmc_kd
+run() {
+  local name=$1; shift
+  timeout -s KILL 90 rocprofv3 --pmc "$@" -d gpurun_out/pmc_kd/${name} -o run --output-format csv \
+    -- python3 bench.py --config c4 --sources 2048 --steps 1 --warmup 1 --no-cpu-baseline --verify 0 > gpurun_out/pmc_kd/${name}.log 2>&1 || echo "pass $name failed"
+}
+run sq1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU
+run sq2 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE
+run sq3 SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_FLAT SQ_INSTS_FLAT SQ_WAVES
+python3 - <<'PY'
+import csv, collections, glob
+for f in sorted(glob.glob("gpurun_out/pmc_kd/*/*counter_collection.csv")):
+    agg = collections.defaultdict(float)
+    for r in csv.DictReader(open(f)):
+        if "sssp_delta" in r["Kernel_Name"]:
+            agg[r["Counter_Name"]] += float(r["Counter_Value"])
+    for k, v in sorted(agg.items()):
+        print(f"{k:28s} {v:16.0f}")
+PY

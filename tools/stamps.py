@@ -32,14 +32,14 @@ lat = torch.empty((len(S), len(T)), dtype=torch.float64, device=dev)
 rel = torch.empty_like(lat)
 mn = torch.empty(len(S), dtype=torch.float64, device=dev)
 nwg = (len(S) + 7) // 8
-dbg = torch.zeros((len(S) + nwg, 8), dtype=torch.int64, device=dev)
+dbg = torch.zeros((len(S) + nwg) * 32, dtype=torch.int64, device=dev)
 L.shd_route_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
 L.shd_route_debug_buffer(eng._h, C.c_void_p(dbg.data_ptr()))
 for rep in range(3):
     dbg.zero_()
     eng.rows_async(d_src, d_tgt, lat, rel, mn)
     eng.sync()
-d_all = dbg.cpu().numpy().astype(np.int64)
+d_all = dbg.cpu().numpy().astype(np.int64).reshape(-1, 32 if eng.info["kernel"] == 4 else 8)
 d = d_all[: len(S)]
 if eng.info["kernel"] == 2:
     kb = d_all[len(S):]
@@ -60,9 +60,12 @@ if eng.info["kernel"] == 4:
         print(f"  {nm:14s} mean {ph[:, k].mean():10.0f} cyc  p50 {np.median(ph[:, k]):10.0f}  max {ph[:, k].max():10.0f}")
     tot = d[:, 4] - d[:, 0]
     print(f"  total          mean {tot.mean():10.0f} cyc")
-    print(f"  sweeps mean/max        {d[:, 5].mean():.1f} / {d[:, 5].max()}")
+    print(f"  sweeps mean/max        {d[:, 5].mean():.1f} / {d[:, 5].max()}   C sweeps {d[:, 12].mean():.1f}")
     print(f"  queued vertices / n    {d[:, 6].mean() / g.n:.3f}")
     print(f"  arcs expanded / nnz    {d[:, 7].mean() / g.nnz:.3f}")
+    for k, nm in [(11, "minreduce"), (8, "gather"), (9, "prep"), (10, "expand"), (16, "B.short"), (17, "B.long"),
+                  (18, "lat row+drain"), (19, "par copy"), (13, "C.compute"), (14, "C.drain"), (15, "C.barrier")]:
+        print(f"  A.{nm:10s} mean {d[:, k].mean():10.0f} cyc  ({d[:, k].mean() / max(d[:, 5].mean(), 1):.0f}/sweep)")
     t0 = d[:, 0] - d[:, 0].min()
     print(f"  start spread (cyc): p50 {np.median(t0):.0f} max {t0.max()}  end max {(d[:, 4] - d[:, 0].min()).max()}")
     sys.exit(0)

@@ -52,7 +52,8 @@ struct shd_route {
     int kd = 0, kd_block = 1024, kd_slots = 0, kd_delta = 1, kd_qcap = 0;
     size_t kd_lds = 0, kd_stride = 0;
     int* d_kd_lstart = nullptr;   // light in-CSR offsets (n+1)
-    uint32_t* d_kd_orec = nullptr;  // out-arc records (2 x u32 per arc)
+    uint32_t* d_kd_orec = nullptr;  // out-arc records v | w << 16
+    uint16_t* d_kd_oridx = nullptr; // rtab index per out-arc
     uint32_t* d_kd_lrec = nullptr;  // light in-arc records (2 x u32 per arc)
     double* d_kd_rtab = nullptr;    // distinct reliabilities
     int kd_nlight = 0, kd_nrtab = 1;
@@ -348,11 +349,8 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
             if (lds <= kLdsBudget && maxdeg <= 65535 && rtab_ok) {
                 // out-arc records {v | w << 16, ridx}; light in-CSR records {u | w << 16, ridx}
                 // (light = w < delta; directed graphs: every in-arc, fused parents are off)
-                std::vector<uint32_t> orec(2 * (size_t)c->nnz);
-                for (int a = 0; a < c->nnz; a++) {
-                    orec[2 * (size_t)a] = (uint32_t)col[a] | ((uint32_t)w[a] << 16);
-                    orec[2 * (size_t)a + 1] = ridx_out[a];
-                }
+                std::vector<uint32_t> orec(c->nnz);
+                for (int a = 0; a < c->nnz; a++) orec[a] = (uint32_t)col[a] | ((uint32_t)w[a] << 16);
                 std::vector<int> lrow(n + 1, 0);
                 std::vector<uint32_t> lrec;
                 for (int v = 0; v < n; v++) {
@@ -367,6 +365,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 if (lrec.empty()) lrec.assign(2, 0u);
                 rc = upload(c, &c->d_kd_lstart, lrow);
                 if (!rc) rc = upload(c, &c->d_kd_orec, orec);
+                if (!rc) rc = upload(c, &c->d_kd_oridx, ridx_out);
                 if (!rc) rc = upload(c, &c->d_kd_lrec, lrec);
                 if (!rc) rc = upload(c, &c->d_kd_rtab, rtab);
                 if (rc) return rc;
@@ -650,7 +649,7 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         DevDelta k;
         k.n = c->n; k.nw = (c->n + 63) / 64; k.bound = c->k32_bound; k.delta = c->kd_delta;
         k.fused = c->directed ? 0 : 1; k.rc = c->kd_qcap;
-        k.row = c->d_row; k.orec = reinterpret_cast<const uint2*>(c->d_kd_orec);
+        k.row = c->d_row; k.orec = c->d_kd_orec; k.oridx = c->d_kd_oridx;
         k.lrow = c->d_kd_lstart; k.lrec = reinterpret_cast<const uint2*>(c->d_kd_lrec); k.nlight = c->kd_nlight;
         k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab;
         k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;

@@ -57,10 +57,13 @@
 
 namespace shd {
 
-constexpr int KD_P = 4;  // arc steps (64 arcs each) with loads in flight per wave
+constexpr int KD_P = 8;  // arc steps (64 arcs each) with loads in flight per wave
 constexpr int KD_TAIL = 4;  // light-tail arcs per fix-up vertex loaded speculatively
+constexpr int KD_W = 8;      // bitmask words per wave step in the gather / readiness scans
+constexpr int KD_IMP = 192;  // per-wave list of improving arcs (v | nd << 16), flushed past 128
 constexpr uint32_t KD_NONE = 0xFFFFFFFFu;      // no parent recorded
 constexpr uint32_t KD_SRC_MARK = 0xFFFFFFFEu;  // parent record of the source itself
+constexpr uint32_t KD_LIGHT = 0x80000000u;     // parent record = light in-arc index | KD_LIGHT
 
 struct DevDelta {
     int n, nw;
@@ -70,7 +73,8 @@ struct DevDelta {
     int fused;                          // undirected: parents found during expansion
     int rc;                             // LDS work-queue capacity per bucket round (vertices)
     const int* __restrict__ row;        // out-CSR offsets (n+1)
-    const uint2* __restrict__ orec;     // out-arcs {v | w << 16, ridx}, rows sorted by (v, eid)
+    const uint32_t* __restrict__ orec;  // out-arcs v | w << 16, rows sorted by (v, eid)
+    const uint16_t* __restrict__ oridx; // rtab index of each out-arc
     const int* __restrict__ lrow;       // light in-CSR offsets (n+1)
     const uint2* __restrict__ lrec;     // light in-arcs {u | w << 16, ridx}, rows by (-w, u, eid)
                                         // (directed graphs: every in-arc)
@@ -114,12 +118,12 @@ struct KDSmall {
 #endif
 };
 
-// LDS: per-wave scratch | dist u16[n+1] | pend, inq, fix u64[nw] | wmin u32[nw] | work.
+// LDS: per-wave scratch | dist u16[n+1] | pend, fix u64[nw] | wmin u32[nw] | work.
 // work holds the bucket work queue (u16 x rc) + the parent-record ring (uint2 x rr) in
 // phase A, and the phase B/C vertex lists (u16 x qcap + i32 x qcap) afterwards.
 template <int B>
 struct KDLayout {
-    size_t wmark, wkey, dist, pend, inq, fix, wmin, work, ring, rrec, qv, qbeg, total;
+    size_t wmark, wkey, wimp, dist, pend, fix, wmin, work, ring, rrec, qv, qbeg, total;
     int qcap;
     __host__ __device__ static KDLayout make(int n, int rc, int rr) {
         KDLayout L;
@@ -127,9 +131,9 @@ struct KDLayout {
         size_t o = a16(sizeof(KDSmall));
         L.wmark = o; o += (size_t)(B / 64) * 64 * KD_P;
         L.wkey = o;  o += (size_t)(B / 64) * 64 * 8;
+        L.wimp = o;  o += (size_t)(B / 64) * KD_IMP * 4;
         L.dist = o;  o += a16(sizeof(uint16_t) * (size_t)(n + 1));
         L.pend = o;  o += a16(8 * nw);
-        L.inq = o;   o += a16(8 * nw);
         L.fix = o;   o += a16(8 * nw);
         L.wmin = o;  o += a16(4 * nw);
         L.work = o;
@@ -160,6 +164,19 @@ __device__ inline unsigned kd_wave_min(unsigned x) {
     return x;
 }
 
+// wave-wide min of a u32 with DPP row shifts/broadcasts (VALU only, no LDS round trips)
+__device__ inline unsigned kd_wave_min_dpp(unsigned x) {
+    int v = (int)x;
+    const int inf = (int)0xFFFFFFFFu;
+    v = (int)min((unsigned)v, (unsigned)__builtin_amdgcn_update_dpp(inf, v, 0x111, 0xF, 0xF, false));  // row_shr:1
+    v = (int)min((unsigned)v, (unsigned)__builtin_amdgcn_update_dpp(inf, v, 0x112, 0xF, 0xF, false));  // row_shr:2
+    v = (int)min((unsigned)v, (unsigned)__builtin_amdgcn_update_dpp(inf, v, 0x114, 0xF, 0xF, false));  // row_shr:4
+    v = (int)min((unsigned)v, (unsigned)__builtin_amdgcn_update_dpp(inf, v, 0x118, 0xF, 0xF, false));  // row_shr:8
+    v = (int)min((unsigned)v, (unsigned)__builtin_amdgcn_update_dpp(inf, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    v = (int)min((unsigned)v, (unsigned)__builtin_amdgcn_update_dpp(inf, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return (unsigned)__builtin_amdgcn_readlane(v, 63);
+}
+
 __device__ inline unsigned ld16(const uint16_t* d, int v) { return d[v]; }
 
 // pop up to four set bits of *b (lowest first) into v[] as vertex ids of word k (-1 = none)
@@ -170,6 +187,53 @@ __device__ inline void pop4(unsigned long long* b, int k, int v[4]) {
         v[q] = x ? (k << 6) + __ffsll((long long)x) - 1 : -1;
         *b = x & (x - 1);
     }
+}
+
+// Relax the wave's list of improving arcs {v | nd << 16}: a CAS on the u32 word holding
+// dist[v] (retry while still an improvement), then below T -> work queue (one reservation
+// for the whole pass), else -> pending bitmask.  Entries may repeat a vertex; the CAS sorts
+// them out.  Called by a whole wave (ballots); `cnt` is wave-uniform.
+__device__ inline void kd_relax_list(const uint32_t* wimp, int cnt, int lane, unsigned long long upto,
+                                     uint32_t* dist32, unsigned long long* pend, unsigned* wmin, uint16_t* ring,
+                                     int* tail, int rc, unsigned T) {
+    __builtin_amdgcn_wave_barrier();
+    for (int b0 = 0; b0 < cnt; b0 += 64) {
+        const bool act = b0 + lane < cnt;
+        const uint32_t e = act ? wimp[b0 + lane] : 0u;
+        const unsigned v = e & 0xFFFFu, nd = e >> 16, sh = (v & 1u) << 4;
+        bool won = false;
+        if (act) {
+            uint32_t old = dist32[v >> 1];
+            for (;;) {
+                if (nd >= ((old >> sh) & 0xFFFFu)) break;
+                const uint32_t got = atomicCAS(&dist32[v >> 1], old, (old & ~(0xFFFFu << sh)) | (nd << sh));
+                if (got == old) { won = true; break; }
+                old = got;
+            }
+        }
+        const bool push = won && nd < T;
+        if (won && nd >= T) { atomicOr(&pend[v >> 6], 1ull << (v & 63)); atomicMin(&wmin[v >> 6], nd); }
+        const unsigned long long pm = __ballot(push);
+        if (pm) {
+            const int ctot = __popcll(pm);
+            int qb = 0, qk = 0;
+            if (lane == 0) {
+                for (;;) {
+                    const int t = __hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    qk = min(ctot, rc - t);
+                    if (qk <= 0) { qk = 0; break; }
+                    if (atomicCAS(tail, t, t + qk) == t) { qb = t; break; }
+                }
+            }
+            qb = __builtin_amdgcn_readfirstlane(qb);
+            qk = __builtin_amdgcn_readfirstlane(qk);
+            const int rk = __popcll(pm & (upto >> 1));
+            // one copy of the vertex: the queue's (else the pending bitmask)
+            if (push && rk < qk) { ring[qb + rk] = (uint16_t)v; atomicAnd(&pend[v >> 6], ~(1ull << (v & 63))); }
+            if (push && rk >= qk) { atomicOr(&pend[v >> 6], 1ull << (v & 63)); atomicMin(&wmin[v >> 6], nd); }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
 }
 
 template <int B>
@@ -185,11 +249,11 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     unsigned char* wmark = reinterpret_cast<unsigned char*>(smem + L.wmark) + wid * 64 * KD_P;
     unsigned long long* wkey = reinterpret_cast<unsigned long long*>(smem + L.wkey) + wid * 64;
+    uint32_t* wimp = reinterpret_cast<uint32_t*>(smem + L.wimp) + wid * KD_IMP;
     uint16_t* dist = reinterpret_cast<uint16_t*>(smem + L.dist);
     unsigned long long* pend = reinterpret_cast<unsigned long long*>(smem + L.pend);
     unsigned* wmin = reinterpret_cast<unsigned*>(smem + L.wmin);
     unsigned long long* fix = reinterpret_cast<unsigned long long*>(smem + L.fix);
-    unsigned long long* inq = reinterpret_cast<unsigned long long*>(smem + L.inq);
     uint16_t* ring = reinterpret_cast<uint16_t*>(smem + L.ring);
     uint2* rrec = reinterpret_cast<uint2*>(smem + L.rrec);
     uint16_t* qv = reinterpret_cast<uint16_t*>(smem + L.qv);
@@ -219,7 +283,7 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
         const double fs = g.vf[s];
         const double cs = isnan(fs) ? 1.0 : 1.0 * fs;
         for (int v = tid; v < (n + 2) / 2; v += B) reinterpret_cast<uint32_t*>(dist)[v] = 0xFFFFFFFFu;
-        for (int k = tid; k < nw; k += B) { pend[k] = 0ull; inq[k] = 0ull; wmin[k] = 0xFFFFFFFFu; fix[k] = 0ull; }
+        for (int k = tid; k < nw; k += B) { pend[k] = 0ull; wmin[k] = 0xFFFFFFFFu; fix[k] = 0ull; }
         for (int q = tid; q < KD_RR; q += B) rrec[q] = make_uint2(0u, 0xFFFFFFFFu);  // phases B/C reuse the area
         if (tid == 0) {
             sm->gmin[0] = sm->gmin[1] = 0xFFFFFFFFu;
@@ -237,8 +301,8 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
         // ---- A: delta-stepping, asynchronous inside a bucket ------------------------
         // Bucket round: (1) T from the min pending distance; (2) gather the pending vertices
         // with dist < T into the work queue; (3) compute waves pull 64-entry slices from the
-        // queue and push every vertex they improve below T straight back (deduplicated by
-        // the inq bits), so a bucket's light-arc chains need no barriers; far improvements
+        // queue and push every vertex they improve below T straight back, so a bucket's
+        // light-arc chains need no barriers; far improvements
         // and queue overflow go to the pending bitmask.  The last wave is the writer: it
         // drains the slices' parent records into wpr (HBM) so compute waves never wait on a
         // store.  A round ends when no wave holds a slice and the queue is empty.
@@ -309,7 +373,6 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                         pos++;
                     }
                     pend[k] = bits & ~take;
-                    inq[k] = take;
                     wmin[k] = rest;
                 }
             }
@@ -346,11 +409,15 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                             fin = bz == 0 && hh == t;
                         }
                         if (__builtin_amdgcn_readfirstlane(fin)) break;
+                        KD_COUNT(21, 1);
                         if (++spins > (1 << 22)) { if (lane == 0) raise_err(err, SHD_ROUTE_EDEVICE); break; }
                         __builtin_amdgcn_s_sleep(1);
                         continue;
                     }
                     spins = 0;
+#ifdef SHD_STAMPS
+                    unsigned long long ks0 = __builtin_amdgcn_s_memtime();
+#endif
                     // the slice: queue entries [h, h+nn), written right after reservation
                     const bool act = lane < nn;
                     int u = 0;
@@ -360,7 +427,6 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                         for (int w8 = 0; x == 0xFFFFu && w8 < (1 << 22); w8++) { __builtin_amdgcn_s_sleep(1); x = *slot; }
                         if (x == 0xFFFFu) raise_err(err, SHD_ROUTE_EDEVICE);
                         u = x == 0xFFFFu ? s : (int)x;
-                        atomicAnd(&inq[u >> 6], ~(1ull << (u & 63)));
                     }
                     const unsigned du = act ? ld16(dist, u) : 0u;
                     int beg = 0, deg = 0;
@@ -378,144 +444,78 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                     const int excl = incl - deg;
                     const int boff = beg - excl;
                     if (g.fused) wkey[lane] = ~0ull;
+#ifdef SHD_STAMPS
+                    if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[22] += t_ - ks0; ks0 = t_; }
+#endif
                     for (int base0 = 0; base0 < total; base0 += 64 * KD_P) {
+                        // The loop is issue-bound (15 waves share 4 SIMDs), so it is written for
+                        // few instructions per arc: straight-line, exec-masked atomics, one queue
+                        // reservation per window, and a rare slow path for CAS conflicts.
                         // owners: each lane whose row starts inside the window marks its start
                         const int pos = excl - base0;
                         const bool mark = deg > 0 && pos >= 0 && pos < 64 * KD_P;
                         if (mark) wmark[pos] = (unsigned char)(lane + 1);
                         __builtin_amdgcn_wave_barrier();
-                        int fl[KD_P];
-#pragma unroll
-                        for (int p = 0; p < KD_P; p++) fl[p] = wmark[64 * p + lane];
-                        uint2 rec[KD_P];
-                        unsigned od[KD_P];
-                        int oo[KD_P], aa[KD_P], ps[KD_P];
-                        // staged so the cross-lane reads of all steps issue back to back
-                        int pp[KD_P], cl[KD_P];
-                        bool bel[KD_P];
+                        uint32_t rx[KD_P], od[KD_P];
+                        int aa[KD_P], oo[KD_P];
 #pragma unroll
                         for (int p = 0; p < KD_P; p++) {
                             const int base = base0 + 64 * p;
-                            const unsigned long long M = __ballot(fl[p] != 0);
-                            const unsigned long long carry_m = __ballot(deg > 0 && excl < base && incl > base);
-                            const unsigned long long below = M & upto;
-                            bel[p] = below != 0ull;
-                            pp[p] = bel[p] ? 63 - __clzll((long long)below) : 0;
-                            cl[p] = carry_m ? __ffsll((long long)carry_m) - 1 : 0;
-                        }
-                        int via[KD_P];
-#pragma unroll
-                        for (int p = 0; p < KD_P; p++) via[p] = __builtin_amdgcn_ds_bpermute(pp[p] << 2, fl[p]) - 1;
-#pragma unroll
-                        for (int p = 0; p < KD_P; p++) oo[p] = bel[p] ? via[p] : cl[p];
-                        int ob[KD_P], ox[KD_P];
-#pragma unroll
-                        for (int p = 0; p < KD_P; p++) {
-                            ob[p] = __builtin_amdgcn_ds_bpermute(oo[p] << 2, boff);
-                            od[p] = (unsigned)__builtin_amdgcn_ds_bpermute(oo[p] << 2, (int)du);
-                            ox[p] = __builtin_amdgcn_ds_bpermute(oo[p] << 2, excl);
+                            const int fl = wmark[64 * p + lane];
+                            const unsigned long long below = __ballot(fl != 0) & upto;
+                            // no start at or before this position inside the chunk: the owner is
+                            // the lane whose row covers the chunk's first position
+                            const unsigned long long cov = __ballot(deg > 0 && excl <= base);
+                            const int carry = cov ? 63 - __clzll((long long)cov) : 0;
+                            const int pp = below ? 63 - __clzll((long long)below) : 0;
+                            const int via = __builtin_amdgcn_ds_bpermute(pp << 2, fl) - 1;
+                            oo[p] = below ? via : carry;
                         }
 #pragma unroll
                         for (int p = 0; p < KD_P; p++) {
+                            const int ob = __builtin_amdgcn_ds_bpermute(oo[p] << 2, boff);
+                            od[p] = (uint32_t)__builtin_amdgcn_ds_bpermute(oo[p] << 2, (int)du);
                             const int e = base0 + 64 * p + lane;
-                            ps[p] = e - ox[p];  // position in the owner's row
-                            aa[p] = e < total ? ob[p] + e : -1;
-                            rec[p] = g.orec[e < total ? ob[p] + e : 0];
+                            aa[p] = e < total ? ob + e : -1;
+                            rx[p] = g.orec[e < total ? ob + e : 0];
                         }
                         __builtin_amdgcn_wave_barrier();
                         if (mark) wmark[pos] = 0;
-                        // relax: all dist words read, all CAS attempts issued, then results checked
-                        uint32_t* dist32 = reinterpret_cast<uint32_t*>(dist);
-                        uint32_t wd[KD_P];
-#pragma unroll
-                        for (int p = 0; p < KD_P; p++) wd[p] = dist32[(rec[p].x & 0xFFFFu) >> 1];
-                        unsigned dv[KD_P], nd[KD_P];
-                        bool want[KD_P];
+                        // common path per step: read dist[v], compare, and append the improving
+                        // lanes (~5% of arcs) to the wave's list; the tight check for fused parents
+                        // is one exec-masked ds_min_u64
+                        int nimp = 0;
 #pragma unroll
                         for (int p = 0; p < KD_P; p++) {
-                            const unsigned v = rec[p].x & 0xFFFFu;
-                            dv[p] = (wd[p] >> ((v & 1u) * 16)) & 0xFFFFu;
-                            nd[p] = od[p] + (rec[p].x >> 16);
-                            want[p] = aa[p] >= 0 && nd[p] < dv[p] && nd[p] <= bound;
-                        }
-                        uint32_t prev[KD_P];
-#pragma unroll
-                        for (int p = 0; p < KD_P; p++) {
-                            const unsigned v = rec[p].x & 0xFFFFu, sh = (v & 1u) * 16;
-                            prev[p] = want[p] ? atomicCAS(&dist32[v >> 1], wd[p], (wd[p] & ~(0xFFFFu << sh)) | (nd[p] << sh))
-                                              : wd[p];
-                        }
-                        bool push[KD_P];
-#pragma unroll
-                        for (int p = 0; p < KD_P; p++) {
-                            push[p] = false;
-                            if (!want[p]) continue;
-                            const unsigned v = rec[p].x & 0xFFFFu, sh = (v & 1u) * 16;
-                            bool won = prev[p] == wd[p];
-                            uint32_t old = prev[p];
-                            while (!won) {  // lost a race on the word: retry while still an improvement
-                                if (nd[p] >= ((old >> sh) & 0xFFFFu)) break;
-                                const uint32_t got = atomicCAS(&dist32[v >> 1], old, (old & ~(0xFFFFu << sh)) | (nd[p] << sh));
-                                won = got == old;
-                                old = got;
+                            const unsigned v = rx[p] & 0xFFFFu, w = rx[p] >> 16;
+                            const unsigned dv = ld16(dist, (int)v), nd = od[p] + w;
+                            const bool imp = aa[p] >= 0 && nd < dv;  // nd < dv <= 0xFFFF: fits u16
+                            const unsigned long long im = __ballot(imp);
+                            if (imp) wimp[nimp + __popcll(im & (upto >> 1))] = v | (nd << 16);
+                            nimp += __popcll(im);
+                            // tie rule: largest w, then smallest (parent, eid) = arc index
+                            if (g.fused && aa[p] >= 0 && dv + w == od[p])
+                                atomicMin(&wkey[oo[p]], ((unsigned long long)(0xFFFFu - w) << 32) | (unsigned)aa[p]);
+                            if (nimp > KD_IMP - 64 || p == KD_P - 1) {
+                                kd_relax_list(wimp, nimp, lane, upto, reinterpret_cast<uint32_t*>(dist), pend, wmin, ring,
+                                              &sm->tail, rc, T);
+                                nimp = 0;
                             }
-                            if (!won) continue;
-                            const unsigned long long bit = 1ull << (v & 63);
-                            if (nd[p] < T) {
-                                push[p] = !(atomicOr(&inq[v >> 6], bit) & bit);
-                                if (push[p]) atomicAnd(&pend[v >> 6], ~bit);  // one copy: the queue's
-                            }
-                            else { atomicOr(&pend[v >> 6], bit); atomicMin(&wmin[v >> 6], nd[p]); }
-                        }
-                        // one queue reservation for all the group's pushes
-                        int cpre[KD_P], ctot = 0;
-#pragma unroll
-                        for (int p = 0; p < KD_P; p++) { cpre[p] = ctot; ctot += __popcll(__ballot(push[p])); }
-                        if (ctot) {
-                            int qb = 0, qk = 0;
-                            if (lane == 0) {
-                                for (;;) {
-                                    const int t = __hip_atomic_load(&sm->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                                    qk = min(ctot, rc - t);
-                                    if (qk <= 0) { qk = 0; break; }
-                                    if (atomicCAS(&sm->tail, t, t + qk) == t) { qb = t; break; }
-                                }
-                            }
-                            qb = __builtin_amdgcn_readfirstlane(qb);
-                            qk = __builtin_amdgcn_readfirstlane(qk);
-#pragma unroll
-                            for (int p = 0; p < KD_P; p++) {
-                                const unsigned long long bm = __ballot(push[p]);
-                                if (!push[p]) continue;
-                                const int rk = cpre[p] + __popcll(bm & (upto >> 1));
-                                const unsigned v = rec[p].x & 0xFFFFu;
-                                if (rk < qk) ring[qb + rk] = (uint16_t)v;
-                                else {  // queue full: back to the pending bitmask
-                                    atomicAnd(&inq[v >> 6], ~(1ull << (v & 63)));
-                                    atomicOr(&pend[v >> 6], 1ull << (v & 63));
-                                    atomicMin(&wmin[v >> 6], nd[p]);
-                                }
-                            }
-                        }
-#pragma unroll
-                        for (int p = 0; p < KD_P; p++) {
-                            // tie rule: largest w, then smallest (parent, eid) = row position
-                            const unsigned w = rec[p].x >> 16;
-                            if (g.fused && aa[p] >= 0 && dv[p] + w == od[p])
-                                atomicMin(&wkey[oo[p]], ((unsigned long long)(0xFFFFu - w) << 48) |
-                                                            ((unsigned long long)ps[p] << 32) |
-                                                            ((rec[p].x & 0xFFFFu) << 16) | (rec[p].y & 0xFFFFu));
                         }
                     }
+#ifdef SHD_STAMPS
+                    if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[23] += t_ - ks0; ks0 = t_; sm->acc[25] += (total + 64 * KD_P - 1) / (64 * KD_P); }
+#endif
                     KD_COUNT(7, total);
                     KD_COUNT(6, nn);
+                    KD_COUNT(20, 1);
                     __builtin_amdgcn_wave_barrier();
                     // parent records {winner, u | du << 16} to the writer's ring
                     const bool hasrec = act && u != s;
                     uint32_t prec = KD_NONE;
                     if (g.fused && hasrec) {
                         const unsigned long long kk = wkey[lane];
-                        if (kk != ~0ull && (0xFFFFu - (unsigned)(kk >> 48)) >= delta) prec = (uint32_t)kk;
+                        if (kk != ~0ull && (0xFFFFu - (unsigned)(kk >> 32)) >= delta) prec = (uint32_t)kk;  // arc index
                     }
                     const unsigned long long rm = __ballot(hasrec);
                     const int nr = __popcll(rm);
@@ -535,6 +535,9 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                         }
                     }
                     if (lane == 0) atomicSub(&sm->busy, 1);
+#ifdef SHD_STAMPS
+                    if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[24] += t_ - ks0; sm->acc[26] += 1; }
+#endif
                 }
                 if (lane == 0) atomicAdd(&sm->nexit, 1);
             } else {
@@ -655,11 +658,7 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
 #pragma unroll
                     for (int e = KD_TAIL - 1; e >= 0; e--)
                         if (a4[q] + e < r4[q] && dt[q][e] + (rc[q][e].x >> 16) == d4[q]) f = e;
-                    uint32_t fr = rc[q][0].x << 16 | (rc[q][0].y & 0xFFFFu);
-#pragma unroll
-                    for (int e = 1; e < KD_TAIL; e++)
-                        if (f == e) fr = rc[q][e].x << 16 | (rc[q][e].y & 0xFFFFu);
-                    out_a[q] = f >= 0 ? fr : KD_NONE;
+                    out_a[q] = f >= 0 ? KD_LIGHT | (uint32_t)(a4[q] + f) : KD_NONE;
                     if (v4[q] >= 0 && f < 0) {
                         if (r4[q] - a4[q] > KD_TAIL) {  // long tail: one wave per vertex below
                             const int at = atomicAdd(&sm->qcur[rnd], 1);
@@ -684,8 +683,7 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                     const uint2 rc = g.lrec[min(a, last_arc)];
                     const bool tight = a < r1 && ld16(dist, (int)(rc.x & 0xFFFFu)) + (rc.x >> 16) == dv;
                     const unsigned long long tm = __ballot(tight);
-                    const uint32_t mine = rc.x << 16 | (rc.y & 0xFFFFu);
-                    if (tm) fr = (uint32_t)__shfl((int)mine, __ffsll((long long)tm) - 1, 64);
+                    if (tm) fr = KD_LIGHT | (uint32_t)(a0 + __ffsll((long long)tm) - 1);
                 }
                 if (lane == 0) {
                     if (fr == KD_NONE) raise_err(err, SHD_ROUTE_EUNREACH);
@@ -716,19 +714,29 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
         KD_ACC(18);
         // dist is dead: its LDS becomes the parent array; wpr decodes into (parent, -r)
         uint16_t* parv = dist;
+        // parent records: out-arc index (fused), KD_LIGHT | light in-arc index (fix-up)
         for (int v0 = tid; v0 < n; v0 += B * 8) {
             uint32_t pr[8];
-            double rr[8];
 #pragma unroll
             for (int q = 0; q < 8; q++) pr[q] = wpr[min(v0 + q * B, n - 1)];
+            uint32_t px[8], pi[8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) rr[q] = g.rtab[pr[q] >= KD_SRC_MARK ? 0 : min((int)(pr[q] & 0xFFFFu), g.nrtab - 1)];
+            for (int q = 0; q < 8; q++) {
+                const bool bad = pr[q] >= KD_SRC_MARK;
+                const bool lt = !bad && (pr[q] & KD_LIGHT);
+                const uint32_t ix = bad ? 0u : (pr[q] & ~KD_LIGHT);
+                if (lt) { const uint2 r2 = g.lrec[min((int)ix, g.nlight - 1)]; px[q] = r2.x; pi[q] = r2.y; }
+                else { px[q] = g.orec[ix]; pi[q] = g.oridx[ix]; }
+            }
+            double rr[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) rr[q] = g.rtab[min((int)(pi[q] & 0xFFFFu), g.nrtab - 1)];
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const int v = v0 + q * B;
                 if (v >= n) continue;
                 const bool src_v = pr[q] == KD_SRC_MARK;
-                parv[v] = src_v ? (uint16_t)v : (uint16_t)(pr[q] >> 16);
+                parv[v] = src_v ? (uint16_t)v : (uint16_t)(px[q] & 0xFFFFu);
                 relv[v] = src_v ? cs : -rr[q];
             }
         }

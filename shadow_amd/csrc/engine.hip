@@ -56,7 +56,7 @@ struct shd_route {
     uint16_t* d_kd_oridx = nullptr; // rtab index per out-arc
     uint32_t* d_kd_lrec = nullptr;  // light in-arc records (2 x u32 per arc)
     double* d_kd_rtab = nullptr;    // distinct reliabilities
-    int kd_nlight = 0, kd_nrtab = 1;
+    int kd_nlight = 0, kd_nrtab = 1, kd_walk = 0;
     char* d_kd_ws = nullptr;
     int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD
     uint64_t device_bytes = 0;
@@ -373,6 +373,8 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 c->kd_nrtab = std::max<int>(1, (int)rtab.size());
                 const int per_cu = std::max(1, std::min((int)(kLdsBudget / lds), 2048 / blk));
                 c->kd_slots = 256 * per_cu;
+                // tests cap the grid so that every workgroup runs many sources in turn
+                if (const char* e = getenv("SHD_ROUTE_KDGRID")) c->kd_slots = std::max(1, std::min(c->kd_slots, atoi(e)));
                 c->kd_stride = kd_ws_stride(n);
                 if (hipMalloc((void**)&c->d_kd_ws, c->kd_stride * (size_t)c->kd_slots) != hipSuccess)
                     return SHD_ROUTE_ENOMEM;
@@ -382,6 +384,10 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
                 if (rc) return rc;
                 c->kd = 1; c->kd_block = blk; c->kd_lds = lds; c->kd_delta = delta; c->kd_qcap = qcap;
+                c->kd_walk = (blk == 1024 ? kd_walk_fits<1024>(n, qcap, c->kd_nrtab)
+                              : blk == 512 ? kd_walk_fits<512>(n, qcap, c->kd_nrtab)
+                                           : kd_walk_fits<256>(n, qcap, c->kd_nrtab)) ? 1 : 0;
+                if (const char* e = getenv("SHD_ROUTE_KDWALK")) c->kd_walk = c->kd_walk && atoi(e) != 0;
             }
         }
     }
@@ -651,7 +657,7 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         k.fused = c->directed ? 0 : 1; k.rc = c->kd_qcap;
         k.row = c->d_row; k.orec = c->d_kd_orec; k.oridx = c->d_kd_oridx;
         k.lrow = c->d_kd_lstart; k.lrec = reinterpret_cast<const uint2*>(c->d_kd_lrec); k.nlight = c->kd_nlight;
-        k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab;
+        k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab; k.walk = c->kd_walk;
         k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;
         const int grid = std::min(ns, c->kd_slots);
         if (c->kd_block == 1024)

@@ -80,6 +80,7 @@ struct DevDelta {
                                         // (directed graphs: every in-arc)
     const double* __restrict__ rtab;    // distinct 1 - loss values, indexed by ridx
     int nrtab;
+    int walk;                           // phase C by path walks in LDS (nrtab <= 256, fits)
     const double* __restrict__ vf;
     const double* __restrict__ self_w;
     const double* __restrict__ self_r;
@@ -113,6 +114,7 @@ struct KDSmall {
     int qtail[2];       // phase B/C list lengths (by parity)
     int qcur[2];        // phase B long-tail list lengths
     unsigned long long rmin;
+    int deep;           // phase C path walk: some target deeper than KD_MAXD
 #ifdef SHD_STAMPS
     unsigned long long acc[32];
 #endif
@@ -123,16 +125,19 @@ struct KDSmall {
 // phase A, and the phase B/C vertex lists (u16 x qcap + i32 x qcap) afterwards.
 template <int B>
 struct KDLayout {
-    size_t wmark, wkey, wimp, dist, pend, fix, wmin, work, ring, rrec, qv, qbeg, total;
+    size_t wmark, wkey, wimp, dist, pend, fix, wmin, work, ring, rrec, qv, qbeg, rix, rtabl, total;
     int qcap;
     __host__ __device__ static KDLayout make(int n, int rc, int rr) {
         KDLayout L;
         const size_t nw = (size_t)(n + 63) / 64;
         size_t o = a16(sizeof(KDSmall));
+        L.dist = o;  o += a16(sizeof(uint16_t) * (size_t)(n + 1));
+        // everything after dist is re-initialised per source (wmark included): the path walk
+        // of phase C reuses it for the parent-arc reliability indices (u8 x n) and rtab
+        L.rix = o;
         L.wmark = o; o += (size_t)(B / 64) * 64 * KD_P;
         L.wkey = o;  o += (size_t)(B / 64) * 64 * 8;
         L.wimp = o;  o += (size_t)(B / 64) * KD_IMP * 4;
-        L.dist = o;  o += a16(sizeof(uint16_t) * (size_t)(n + 1));
         L.pend = o;  o += a16(8 * nw);
         L.fix = o;   o += a16(8 * nw);
         L.wmin = o;  o += a16(4 * nw);
@@ -145,9 +150,11 @@ struct KDLayout {
         L.qbeg = o + a16(2 * (size_t)L.qcap);
         o += wbytes;
         L.total = o;
+        L.rtabl = a16(L.rix + (size_t)n);
         return L;
     }
 };
+constexpr int KD_MAXD = 32;           // phase C path walk: arcs held in registers
 constexpr int KD_RR = 1024;  // parent-record ring slots
 
 // per-workgroup HBM slice: relv f64[n] | wpr u32[n], the parent record of every vertex:
@@ -266,7 +273,6 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
     const bool writer = wid == NW - 1;  // drains parent records; never waits on a global load
     double* relv = reinterpret_cast<double*>(ws + (size_t)blockIdx.x * ws_stride);
     uint32_t* wpr = reinterpret_cast<uint32_t*>(ws + (size_t)blockIdx.x * ws_stride + a16(sizeof(double) * n));
-    for (int q = lane; q < 64 * KD_P; q += 64) wmark[q] = 0;
 #ifdef SHD_STAMPS
     if (tid < 32) sm->acc[tid] = 0;
     __syncthreads();
@@ -285,6 +291,7 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
         for (int v = tid; v < (n + 2) / 2; v += B) reinterpret_cast<uint32_t*>(dist)[v] = 0xFFFFFFFFu;
         for (int k = tid; k < nw; k += B) { pend[k] = 0ull; wmin[k] = 0xFFFFFFFFu; fix[k] = 0ull; }
         for (int q = tid; q < KD_RR; q += B) rrec[q] = make_uint2(0u, 0xFFFFFFFFu);  // phases B/C reuse the area
+        for (int q = lane; q < 64 * KD_P; q += 64) wmark[q] = 0;  // phase C reuses it
         if (tid == 0) {
             sm->gmin[0] = sm->gmin[1] = 0xFFFFFFFFu;
             sm->rtail = sm->rdone = 0;
@@ -710,10 +717,109 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
             if (lrow) __builtin_nontemporal_store(Lv, lrow + j);
         }
         wait_stores();  // wpr of phase B visible to the whole workgroup
+        if (tid == 0) { sm->deep = 0; sm->rmin = kInfBits; }
         __syncthreads();
         KD_ACC(18);
-        // dist is dead: its LDS becomes the parent array; wpr decodes into (parent, -r)
+        // dist is dead: its LDS becomes the parent array
         uint16_t* parv = dist;
+        if (g.walk && rrow) {
+            // ---- C': reliability by walking each target's tree path in LDS -------------
+            // parv u16 + rix u8 (index of the parent arc's reliability) + rtab in LDS; each
+            // target walks <= KD_MAXD arcs to the source, then folds the product source-first
+            // (the order the level sweep multiplies in, so the bits agree)
+            uint8_t* rixl = reinterpret_cast<uint8_t*>(smem + L.rix);
+            double* rtl = reinterpret_cast<double*>(smem + L.rtabl);
+            for (int k = tid; k < g.nrtab; k += B) rtl[k] = g.rtab[k];
+            for (int v0 = tid; v0 < n; v0 += B * 8) {
+                uint32_t pr[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) pr[q] = wpr[min(v0 + q * B, n - 1)];
+                uint32_t px[8], pi[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    const bool bad = pr[q] >= KD_SRC_MARK;
+                    const bool lt = !bad && (pr[q] & KD_LIGHT);
+                    const uint32_t ix = bad ? 0u : (pr[q] & ~KD_LIGHT);
+                    if (lt) { const uint2 r2 = g.lrec[min((int)ix, g.nlight - 1)]; px[q] = r2.x; pi[q] = r2.y; }
+                    else { px[q] = g.orec[ix]; pi[q] = g.oridx[ix]; }
+                }
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    const int v = v0 + q * B;
+                    if (v >= n) continue;
+                    parv[v] = pr[q] == KD_SRC_MARK ? (uint16_t)v
+                            : pr[q] == KD_NONE ? (uint16_t)0xFFFFu : (uint16_t)(px[q] & 0xFFFFu);
+                    rixl[v] = (uint8_t)min(pi[q] & 0xFFFFu, (uint32_t)(g.nrtab - 1));
+                }
+            }
+            __syncthreads();
+            KD_ACC(19);
+            for (int j0 = tid; j0 < nt; j0 += 2 * B) {
+                int t2[2], cur[2], d2[2];
+                bool act[2];
+                uint32_t pk[2][KD_MAXD / 4];
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const int j = j0 + q * B;
+                    t2[q] = j < nt ? tgt[j] : -1;
+                    act[q] = t2[q] >= 0 && t2[q] < n && t2[q] != s;
+                    cur[q] = act[q] ? t2[q] : s;
+                    d2[q] = 0;
+#pragma unroll
+                    for (int k = 0; k < KD_MAXD / 4; k++) pk[q][k] = 0u;
+                }
+                bool bad[2] = {false, false};
+#pragma unroll
+                for (int k = 0; k < KD_MAXD; k++) {
+                    if (!__any(act[0] || act[1])) break;
+                    uint32_t p[2], rx[2];
+#pragma unroll
+                    for (int q = 0; q < 2; q++) { p[q] = parv[cur[q]]; rx[q] = rixl[cur[q]]; }
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        if (!act[q]) continue;
+                        pk[q][k >> 2] |= rx[q] << ((k & 3) * 8);
+                        d2[q] = k + 1;
+                        if (p[q] == 0xFFFFu) { bad[q] = true; act[q] = false; }
+                        else if ((int)p[q] == s) act[q] = false;
+                        else cur[q] = (int)p[q];
+                    }
+                }
+                if (act[0] || act[1]) sm->deep = 1;  // the level sweep below redoes the row
+                double rr[2] = {cs, cs};
+#pragma unroll
+                for (int k = KD_MAXD - 1; k >= 0; k--) {
+                    if (!__any(k < d2[0] || k < d2[1])) continue;
+                    double x[2];
+#pragma unroll
+                    for (int q = 0; q < 2; q++) x[q] = rtl[(pk[q][k >> 2] >> ((k & 3) * 8)) & 0xFFu];
+#pragma unroll
+                    for (int q = 0; q < 2; q++)
+                        if (k < d2[q]) rr[q] *= x[q];
+                }
+                double f2[2];
+#pragma unroll
+                for (int q = 0; q < 2; q++) f2[q] = g.vf[(t2[q] >= 0 && t2[q] < n) ? t2[q] : s];
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const int j = j0 + q * B;
+                    if (j >= nt) continue;
+                    const int t = t2[q];
+                    double Rv = NAN;
+                    if (t >= 0 && t < n && !bad[q]) {
+                        if (t == s) Rv = isnan(g.self_w[s]) ? NAN : cs * g.self_r[s];
+                        else Rv = isnan(f2[q]) ? rr[q] : rr[q] * f2[q];
+                    }
+                    __builtin_nontemporal_store(Rv, rrow + j);
+                }
+            }
+            __syncthreads();
+            KD_ACC(13);
+            KD_STAMP(3);
+        }
+        const bool sweep = !(g.walk && rrow) || sm->deep;
+        if (sweep) {
+        // parent records: out-arc index (fused), KD_LIGHT | light in-arc index (fix-up)
         // parent records: out-arc index (fused), KD_LIGHT | light in-arc index (fix-up)
         for (int v0 = tid; v0 < n; v0 += B * 8) {
             uint32_t pr[8];
@@ -830,8 +936,6 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
         KD_STAMP(3);
 
         // ---- D: rel row out + row min ----------------------------------------------
-        if (tid == 0) sm->rmin = kInfBits;
-        __syncthreads();
         if (rrow) {
             for (int j0 = tid; j0 < nt; j0 += B * 4) {
                 int t4[4];
@@ -861,6 +965,7 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                 }
             }
         }
+        }  // sweep
         if (row_min) {
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) lmin = fmin(lmin, __shfl_xor(lmin, d, 64));
@@ -876,5 +981,12 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
 
 template <int B>
 inline size_t kd_lds_bytes(int n, int rc) { return KDLayout<B>::make(n, rc, KD_RR).total; }
+
+// phase C by path walks: u8 reliability index per vertex + the table itself in LDS
+template <int B>
+inline bool kd_walk_fits(int n, int rc, int nrtab) {
+    const KDLayout<B> L = KDLayout<B>::make(n, rc, KD_RR);
+    return nrtab <= 256 && L.rtabl + 8 * (size_t)nrtab <= L.total;
+}
 
 }  // namespace shd

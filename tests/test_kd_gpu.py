@@ -9,13 +9,35 @@ the LDS queue capacity (overflowing vertices must stay pending), and directednes
 import numpy as np
 import pytest
 
-from shadow_amd.graph import config, internet_like
+from shadow_amd.graph import Graph, config, internet_like
 
 pytestmark = pytest.mark.gpu
 
 
+def _chain(n, seed):
+    """A long path plus a few chords: tree depths far beyond the phase-C path walk's
+    register window (KD_MAXD arcs), so the level sweep must take over."""
+    rng = np.random.default_rng(seed)
+    e = [(i, i + 1) for i in range(n - 1)]
+    have = set(e) | {(b, a) for a, b in e}
+    while len(e) < n - 1 + n // 20:  # simple graph: no parallel edges
+        a, b = (int(x) for x in rng.integers(0, n, 2))
+        if a != b and (a, b) not in have:
+            have |= {(a, b), (b, a)}
+            e.append((a, b))
+    e = np.array(e, np.int32)
+    k = len(e)
+    loops = np.arange(n, dtype=np.int32)
+    lat = np.concatenate([rng.integers(1, 20, size=k), rng.integers(1, 5, size=n)]).astype(np.float64)
+    loss = np.concatenate([np.where(rng.random(k) < 0.3, 0.0, rng.integers(1, 50, size=k) * 1e-4), np.zeros(n)])
+    return Graph(n=n, src=np.concatenate([e[:, 0], loops]), dst=np.concatenate([e[:, 1], loops]),
+                 latency=lat, packetloss=loss, vertex_packetloss=np.zeros(n), name="chain")
+
+
 def _graph(name):
     from tests.golden import make_golden as mg
+    if name == "chain":
+        return _chain(600, 37)
     if name == "ba400":
         return internet_like(400, 4, seed=31, name="ba400")
     if name == "ties":
@@ -29,14 +51,23 @@ def _graph(name):
 
 @pytest.fixture
 def kd(monkeypatch):
+    """Forced KD with a small grid: each workgroup runs many sources back to back, so any
+    LDS state a phase fails to restore for the next source shows up as a mismatch."""
     monkeypatch.setenv("SHD_ROUTE_KERNEL", "kd")
+    monkeypatch.setenv("SHD_ROUTE_KDGRID", "7")
     return monkeypatch
 
 
-@pytest.mark.parametrize("name", ["ba400", "ties", "dir", "c2"])
+@pytest.mark.parametrize("walk", [None, "0"])
+@pytest.mark.parametrize("name", ["ba400", "ties", "dir", "c2", "chain"])
 @pytest.mark.parametrize("delta,qcap", [(None, None), (1, None), (7, 64), (100000, None), (None, 64)])
-def test_kd_rows_bitexact(oracle_mod, kd, name, delta, qcap):
+def test_kd_rows_bitexact(oracle_mod, kd, name, delta, qcap, walk):
+    """walk None: phase C by LDS path walks (level sweep only for deep rows); "0": sweep only."""
     from shadow_amd import route
+    if walk is None:
+        kd.delenv("SHD_ROUTE_KDWALK", raising=False)
+    else:
+        kd.setenv("SHD_ROUTE_KDWALK", walk)
     if delta is None:
         kd.delenv("SHD_ROUTE_DELTA", raising=False)
     else:
@@ -58,10 +89,12 @@ def test_kd_rows_bitexact(oracle_mod, kd, name, delta, qcap):
     assert np.array_equal(mn, olat.min(axis=1))
 
 
-def test_kd_c3_sources_subset(oracle_mod, kd):
-    """C3: attached subset (|A| < n) as targets, sources in arbitrary order."""
+@pytest.mark.parametrize("cfg", ["c3", "c4"])
+def test_kd_sources_subset(oracle_mod, kd, cfg):
+    """C3/C4 (512- and 1024-thread workgroups): attached subset (|A| < n) as targets,
+    sources in arbitrary order."""
     from shadow_amd import route
-    g = config("c3")
+    g = config(cfg)
     eng = route.RouteEngine(g)
     assert eng.info["kernel"] == 4
     og = oracle_mod.OracleGraph(g)

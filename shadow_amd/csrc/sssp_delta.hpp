@@ -58,6 +58,7 @@
 namespace shd {
 
 constexpr int KD_P = 8;  // arc steps (64 arcs each) with loads in flight per wave
+static_assert(KD_P == 8, "owner markers are read as one u64 per lane");
 constexpr int KD_TAIL = 4;  // light-tail arcs per fix-up vertex loaded speculatively
 constexpr int KD_W = 8;      // bitmask words per wave step in the gather / readiness scans
 constexpr int KD_IMP = 192;  // per-wave list of improving arcs (v | nd << 16), flushed past 128
@@ -68,6 +69,7 @@ constexpr uint32_t KD_LIGHT = 0x80000000u;     // parent record = light in-arc i
 struct DevDelta {
     int n, nw;
     int nlight;                         // light in-arcs
+    int nnz;                            // out-arcs
     int bound;
     int delta;                          // bucket width; arcs with w >= delta are heavy
     int fused;                          // undirected: parents found during expansion
@@ -132,8 +134,9 @@ struct KDLayout {
         const size_t nw = (size_t)(n + 63) / 64;
         size_t o = a16(sizeof(KDSmall));
         L.dist = o;  o += a16(sizeof(uint16_t) * (size_t)(n + 1));
-        // everything after dist is re-initialised per source (wmark included): the path walk
-        // of phase C reuses it for the parent-arc reliability indices (u8 x n) and rtab
+        // everything after dist is re-initialised per source or written before it is read:
+        // the path walk of phase C reuses it for the parent-arc reliability indices (u8 x n)
+        // and the reliability table
         L.rix = o;
         L.wmark = o; o += (size_t)(B / 64) * 64 * KD_P;
         L.wkey = o;  o += (size_t)(B / 64) * 64 * 8;
@@ -182,6 +185,61 @@ __device__ inline unsigned kd_wave_min_dpp(unsigned x) {
     v = (int)min((unsigned)v, (unsigned)__builtin_amdgcn_update_dpp(inf, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
     v = (int)min((unsigned)v, (unsigned)__builtin_amdgcn_update_dpp(inf, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
     return (unsigned)__builtin_amdgcn_readlane(v, 63);
+}
+
+// wave-wide inclusive prefix sum with DPP row shifts/broadcasts: VALU only (a __shfl_up
+// scan is six dependent ds_bpermute round trips through the LDS crossbar)
+__device__ inline int kd_wave_incl_sum(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return x;
+}
+
+// wave-wide inclusive prefix max of non-negative ints, as kd_wave_incl_sum
+__device__ inline int kd_wave_incl_max(int x) {
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false));
+    return x;
+}
+
+// ob[p] = x of lane own[p], od[p] = y of lane own[p] for the KD_P steps: all 16 crossbar
+// reads issued back to back with one wait (left to the compiler, register pressure makes
+// it wait after every pair, i.e. eight LDS round trips in a row)
+__device__ inline void kd_bpermute16(const int own[8], int x, int y, int ob[8], uint32_t od[8]) {
+    int a[8];
+#pragma unroll
+    for (int p = 0; p < 8; p++) a[p] = own[p] << 2;
+    asm volatile(
+        "ds_bpermute_b32 %0, %16, %24\n\t"
+        "ds_bpermute_b32 %1, %16, %25\n\t"
+        "ds_bpermute_b32 %2, %17, %24\n\t"
+        "ds_bpermute_b32 %3, %17, %25\n\t"
+        "ds_bpermute_b32 %4, %18, %24\n\t"
+        "ds_bpermute_b32 %5, %18, %25\n\t"
+        "ds_bpermute_b32 %6, %19, %24\n\t"
+        "ds_bpermute_b32 %7, %19, %25\n\t"
+        "ds_bpermute_b32 %8, %20, %24\n\t"
+        "ds_bpermute_b32 %9, %20, %25\n\t"
+        "ds_bpermute_b32 %10, %21, %24\n\t"
+        "ds_bpermute_b32 %11, %21, %25\n\t"
+        "ds_bpermute_b32 %12, %22, %24\n\t"
+        "ds_bpermute_b32 %13, %22, %25\n\t"
+        "ds_bpermute_b32 %14, %23, %24\n\t"
+        "ds_bpermute_b32 %15, %23, %25\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(ob[0]), "=&v"(od[0]), "=&v"(ob[1]), "=&v"(od[1]), "=&v"(ob[2]), "=&v"(od[2]),
+          "=&v"(ob[3]), "=&v"(od[3]), "=&v"(ob[4]), "=&v"(od[4]), "=&v"(ob[5]), "=&v"(od[5]),
+          "=&v"(ob[6]), "=&v"(od[6]), "=&v"(ob[7]), "=&v"(od[7])
+        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]),
+          "v"(x), "v"(y));
 }
 
 __device__ inline unsigned ld16(const uint16_t* d, int v) { return d[v]; }
@@ -254,10 +312,10 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
     const KDLayout<B> L = KDLayout<B>::make(n, g.rc, KD_RR);
     KDSmall* sm = reinterpret_cast<KDSmall*>(smem);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    unsigned char* wmark = reinterpret_cast<unsigned char*>(smem + L.wmark) + wid * 64 * KD_P;
     unsigned long long* wkey = reinterpret_cast<unsigned long long*>(smem + L.wkey) + wid * 64;
     uint32_t* wimp = reinterpret_cast<uint32_t*>(smem + L.wimp) + wid * KD_IMP;
     uint16_t* dist = reinterpret_cast<uint16_t*>(smem + L.dist);
+    unsigned char* wmark = reinterpret_cast<unsigned char*>(smem + L.wmark) + wid * 64 * KD_P;
     unsigned long long* pend = reinterpret_cast<unsigned long long*>(smem + L.pend);
     unsigned* wmin = reinterpret_cast<unsigned*>(smem + L.wmin);
     unsigned long long* fix = reinterpret_cast<unsigned long long*>(smem + L.fix);
@@ -268,6 +326,8 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
     const unsigned bound = (unsigned)g.bound;
     const unsigned delta = (unsigned)g.delta;
     const int qcap = L.qcap;
+    const __amdgpu_buffer_rsrc_t orsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(g.orec), (short)0, g.nnz * 4, 0x00020000);
     const int rc = g.rc;
     constexpr int NW = B / 64;
     const bool writer = wid == NW - 1;  // drains parent records; never waits on a global load
@@ -325,7 +385,7 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
             {
                 unsigned m0 = 0xFFFFFFFFu;
                 for (int k = tid; k < nw; k += B) m0 = min(m0, wmin[k]);
-                const unsigned wm = kd_wave_min(m0);
+                const unsigned wm = kd_wave_min_dpp(m0);
                 if (lane == 0 && wm != 0xFFFFFFFFu) atomicMin(&sm->gmin[par], wm);
             }
             for (int q = tid; q < rc; q += B) ring[q] = 0xFFFFu;
@@ -359,15 +419,10 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                     }
                 }
                 const int cnt = __popcll(take);
-                int incl = cnt;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const int y = __shfl_up(incl, d, 64);
-                    if (lane >= d) incl += y;
-                }
+                int incl = kd_wave_incl_sum(cnt);
                 int base = 0;
                 if (lane == 63 && incl) base = atomicAdd(&sm->tail, incl);
-                base = __shfl(base, 63, 64);
+                base = __builtin_amdgcn_readlane(base, 63);
                 int pos = base + incl - cnt;
                 if (act) {
                     unsigned long long b = take;
@@ -441,74 +496,115 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                         const int r0 = g.row[u], r1 = g.row[u + 1];
                         if (act) { beg = r0; deg = r1 - r0; }
                     }
-                    int incl = deg;
-#pragma unroll
-                    for (int d = 1; d < 64; d <<= 1) {
-                        const int y = __shfl_up(incl, d, 64);
-                        if (lane >= d) incl += y;
-                    }
-                    const int total = __shfl(incl, 63, 64);
+                    int incl = kd_wave_incl_sum(deg);
+                    const int total = __builtin_amdgcn_readlane(incl, 63);
                     const int excl = incl - deg;
                     const int boff = beg - excl;
                     if (g.fused) wkey[lane] = ~0ull;
+                    // rows of the slice's active lanes all non-empty (always, undirected): the
+                    // owner of arc position q is then (#rows starting at or before q) - 1, a
+                    // running row count plus one mbcnt per step
+                    const bool dense = __ballot(act && deg == 0) == 0ull;
+                    int rows_before = 0;  // rows starting before the current step (dense slices)
 #ifdef SHD_STAMPS
                     if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[22] += t_ - ks0; ks0 = t_; }
 #endif
+                    int nimp = 0;  // improving arcs listed, relaxed when the list fills or the slice ends
                     for (int base0 = 0; base0 < total; base0 += 64 * KD_P) {
                         // The loop is issue-bound (15 waves share 4 SIMDs), so it is written for
                         // few instructions per arc: straight-line, exec-masked atomics, one queue
-                        // reservation per window, and a rare slow path for CAS conflicts.
+                        // reservation per list flush, and a rare slow path for CAS conflicts.
                         // owners: each lane whose row starts inside the window marks its start
+                        // (lane + 1; marker of position q at byte (q % 64) * 8 + q / 64, so one
+                        // ds_read_b64 per lane fetches its position in all KD_P steps); per step a
+                        // DPP prefix max over the lanes turns the marks into owners, seeded at
+                        // position 0 with the row covering the step's first arc
                         const int pos = excl - base0;
                         const bool mark = deg > 0 && pos >= 0 && pos < 64 * KD_P;
-                        if (mark) wmark[pos] = (unsigned char)(lane + 1);
+                        const int mslot = ((pos & 63) << 3) | (pos >> 6);
+                        if (mark) wmark[mslot] = (unsigned char)(lane + 1);
                         __builtin_amdgcn_wave_barrier();
+                        const unsigned long long fl8 = *reinterpret_cast<const unsigned long long*>(wmark + lane * 8);
                         uint32_t rx[KD_P], od[KD_P];
                         int aa[KD_P], oo[KD_P];
+                        if (dense) {
 #pragma unroll
-                        for (int p = 0; p < KD_P; p++) {
-                            const int base = base0 + 64 * p;
-                            const int fl = wmark[64 * p + lane];
-                            const unsigned long long below = __ballot(fl != 0) & upto;
-                            // no start at or before this position inside the chunk: the owner is
-                            // the lane whose row covers the chunk's first position
-                            const unsigned long long cov = __ballot(deg > 0 && excl <= base);
-                            const int carry = cov ? 63 - __clzll((long long)cov) : 0;
-                            const int pp = below ? 63 - __clzll((long long)below) : 0;
-                            const int via = __builtin_amdgcn_ds_bpermute(pp << 2, fl) - 1;
-                            oo[p] = below ? via : carry;
+                            for (int p = 0; p < KD_P; p++) {
+                                const unsigned long long st = __ballot(((fl8 >> (8 * p)) & 0xFFu) != 0);
+                                const unsigned long long sh = st >> 1;
+                                oo[p] = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(sh >> 32),
+                                            __builtin_amdgcn_mbcnt_lo((unsigned)sh, (unsigned)(rows_before + (int)(st & 1ull) - 1)));
+                                rows_before += __popcll(st);
+                            }
+                        } else {
+#pragma unroll
+                            for (int p = 0; p < KD_P; p++) {
+                                const int base = base0 + 64 * p;
+                                const unsigned long long cov = __ballot(deg > 0 && excl <= base);
+                                const int carry = cov ? 63 - __clzll((long long)cov) : 0;
+                                int f = (int)((fl8 >> (8 * p)) & 0xFFu);
+                                if (lane == 0 && f == 0) f = carry + 1;
+                                oo[p] = kd_wave_incl_max(f) - 1;
+                            }
                         }
+                        int obv[KD_P];
+                        kd_bpermute16(oo, boff, (int)du, obv, od);
+                        // out-arc records through a buffer descriptor: 32-bit offsets, and the
+                        // positions past the slice's arcs need no clamp (range-checked, read 0)
 #pragma unroll
                         for (int p = 0; p < KD_P; p++) {
-                            const int ob = __builtin_amdgcn_ds_bpermute(oo[p] << 2, boff);
-                            od[p] = (uint32_t)__builtin_amdgcn_ds_bpermute(oo[p] << 2, (int)du);
                             const int e = base0 + 64 * p + lane;
-                            aa[p] = e < total ? ob + e : -1;
-                            rx[p] = g.orec[e < total ? ob + e : 0];
+                            aa[p] = obv[p] + e;
+                            rx[p] = __builtin_amdgcn_raw_buffer_load_b32(orsrc, (uint32_t)aa[p] << 2, 0, 0);
                         }
                         __builtin_amdgcn_wave_barrier();
-                        if (mark) wmark[pos] = 0;
+#ifdef SHD_STAMPS
+                        if (wid == 0) {
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                            if (lane == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[27] += t_ - ks0; ks0 = t_; }
+                        }
+#endif
                         // common path per step: read dist[v], compare, and append the improving
                         // lanes (~5% of arcs) to the wave's list; the tight check for fused parents
                         // is one exec-masked ds_min_u64
-                        int nimp = 0;
+                        if (mark) wmark[mslot] = 0;
+                        const bool lastw = base0 + 64 * KD_P >= total;
+                        // all KD_P dist reads in flight before the first LDS store of the steps
+                        // (the compiler cannot move a read above a store that may alias it)
+                        unsigned dvs[KD_P];
+#pragma unroll
+                        for (int p = 0; p < KD_P; p++) dvs[p] = ld16(dist, (int)(rx[p] & 0xFFFFu));
 #pragma unroll
                         for (int p = 0; p < KD_P; p++) {
                             const unsigned v = rx[p] & 0xFFFFu, w = rx[p] >> 16;
-                            const unsigned dv = ld16(dist, (int)v), nd = od[p] + w;
-                            const bool imp = aa[p] >= 0 && nd < dv;  // nd < dv <= 0xFFFF: fits u16
+                            const bool valid = base0 + 64 * p + lane < total;
+                            const unsigned dv = dvs[p], nd = od[p] + w;
+                            const bool imp = valid && nd < dv;  // nd < dv <= 0xFFFF: fits u16
                             const unsigned long long im = __ballot(imp);
                             if (imp) wimp[nimp + __popcll(im & (upto >> 1))] = v | (nd << 16);
                             nimp += __popcll(im);
                             // tie rule: largest w, then smallest (parent, eid) = arc index
-                            if (g.fused && aa[p] >= 0 && dv + w == od[p])
+                            if (g.fused && valid && dv + w == od[p])
                                 atomicMin(&wkey[oo[p]], ((unsigned long long)(0xFFFFu - w) << 32) | (unsigned)aa[p]);
-                            if (nimp > KD_IMP - 64 || p == KD_P - 1) {
+                            if (nimp > KD_IMP - 64 || (lastw && p == KD_P - 1)) {
+#ifdef SHD_STAMPS
+                                unsigned long long kr0 = 0;
+                                if (wid == 0) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); kr0 = __builtin_amdgcn_s_memtime(); }
+#endif
                                 kd_relax_list(wimp, nimp, lane, upto, reinterpret_cast<uint32_t*>(dist), pend, wmin, ring,
                                               &sm->tail, rc, T);
+#ifdef SHD_STAMPS
+                                if (wid == 0) {
+                                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                                    if (lane == 0) sm->acc[29] += __builtin_amdgcn_s_memtime() - kr0;
+                                }
+#endif
                                 nimp = 0;
                             }
                         }
+#ifdef SHD_STAMPS
+                        if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[28] += t_ - ks0; ks0 = t_; }
+#endif
                     }
 #ifdef SHD_STAMPS
                     if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[23] += t_ - ks0; ks0 = t_; sm->acc[25] += (total + 64 * KD_P - 1) / (64 * KD_P); }
@@ -611,15 +707,10 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                 const int k = k0 + tid;
                 unsigned long long bits = k < nw ? fix[k] : 0ull;
                 const int cnt = __popcll(bits);
-                int incl = cnt;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const int y = __shfl_up(incl, d, 64);
-                    if (lane >= d) incl += y;
-                }
+                int incl = kd_wave_incl_sum(cnt);
                 int base = 0;
                 if (lane == 63 && incl) base = atomicAdd(&sm->qtail[rnd], incl);
-                base = __shfl(base, 63, 64);
+                base = __builtin_amdgcn_readlane(base, 63);
                 int pos = base + incl - cnt;
                 unsigned long long b = bits, listed = 0ull;
                 while (b && pos < qcap) {
@@ -881,15 +972,10 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                         if (v4[q] >= 0 && !((pw[q] >> (p4[q] & 63)) & 1ull)) ready |= 1ull << (v4[q] & 63);
                 }
                 const int cnt = __popcll(ready);
-                int incl = cnt;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const int y = __shfl_up(incl, d, 64);
-                    if (lane >= d) incl += y;
-                }
+                int incl = kd_wave_incl_sum(cnt);
                 int base = 0;
                 if (lane == 63 && incl) base = atomicAdd(&sm->qtail[c], incl);
-                base = __shfl(base, 63, 64);
+                base = __builtin_amdgcn_readlane(base, 63);
                 int pos = base + incl - cnt;
                 unsigned long long listed = 0ull;
                 b = ready;

@@ -21,6 +21,7 @@
 #include <limits>
 #include <new>
 #include <numeric>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/shd_route.h"

@@ -68,6 +68,17 @@ struct shd_route {
 
 namespace {
 
+// KD workgroup sizes: f(std::integral_constant<int, B>) for the runtime block size
+template <typename F>
+auto kd_dispatch(int blk, F f) {
+    switch (blk) {
+        case 1024: return f(std::integral_constant<int, 1024>{});
+        case 768: return f(std::integral_constant<int, 768>{});
+        case 512: return f(std::integral_constant<int, 512>{});
+        default: return f(std::integral_constant<int, 256>{});
+    }
+}
+
 int hip_check(hipError_t e) { return e == hipSuccess ? SHD_ROUTE_OK : SHD_ROUTE_EDEVICE; }
 
 template <typename T>
@@ -307,21 +318,23 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
             std::nth_element(ws.begin(), ws.begin() + k, ws.end());
             delta = std::max(1, ws[k]);
         }
-        const int blk = n > 16384 ? 1024 : n > 4096 ? 512 : 256;
-        const size_t base = blk == 1024 ? kd_lds_bytes<1024>(n, 0) : blk == 512 ? kd_lds_bytes<512>(n, 0)
-                                                                               : kd_lds_bytes<256>(n, 0);
+        int blk = n > 16384 ? 1024 : n > 4096 ? 512 : 256;
+        if (const char* e = getenv("SHD_ROUTE_KDBLOCK")) {
+            const int b = atoi(e);
+            if (b == 256 || b == 512 || b == 768 || b == 1024) blk = b;
+        }
+        const size_t base = kd_dispatch(blk, [&](auto B) { return kd_lds_bytes<decltype(B)::value>(n, 0); });
         if (base + 2 * 512 <= kLdsBudget) {
             // queue: the rest of the CU's LDS at one workgroup per CU (large n), else enough
             // for a few workgroups per CU
             // work queue: the rest of the CU's LDS at one workgroup per CU (large n), else
             // enough for a few workgroups per CU
             int qcap;
-            if (blk == 1024) qcap = (int)std::min<size_t>((size_t)n, (kLdsBudget - base - 64) / 2);
+            if (blk >= 768) qcap = (int)std::min<size_t>((size_t)n, (kLdsBudget - base - 64) / 2);
             else qcap = std::min(n, std::max(1024, n / 2));
             if (const char* e = getenv("SHD_ROUTE_QCAP")) qcap = std::min(qcap, std::max(64, atoi(e)));
             qcap &= ~7;
-            const size_t lds = blk == 1024 ? kd_lds_bytes<1024>(n, qcap) : blk == 512 ? kd_lds_bytes<512>(n, qcap)
-                                                                           : kd_lds_bytes<256>(n, qcap);
+            const size_t lds = kd_dispatch(blk, [&](auto B) { return kd_lds_bytes<decltype(B)::value>(n, qcap); });
             int maxdeg = 0;
             for (int v = 0; v < n; v++) maxdeg = std::max(maxdeg, row[v + 1] - row[v]);
             // reliability table: every distinct 1-loss value (exact bits), indexed by u16
@@ -379,14 +392,11 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 if (hipMalloc((void**)&c->d_kd_ws, c->kd_stride * (size_t)c->kd_slots) != hipSuccess)
                     return SHD_ROUTE_ENOMEM;
                 c->allocs.push_back(c->d_kd_ws);
-                const void* fn = blk == 1024 ? (const void*)sssp_delta_kernel<1024>
-                               : blk == 512 ? (const void*)sssp_delta_kernel<512> : (const void*)sssp_delta_kernel<256>;
+                const void* fn = kd_dispatch(blk, [&](auto B) { return (const void*)sssp_delta_kernel<decltype(B)::value>; });
                 rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
                 if (rc) return rc;
                 c->kd = 1; c->kd_block = blk; c->kd_lds = lds; c->kd_delta = delta; c->kd_qcap = qcap;
-                c->kd_walk = (blk == 1024 ? kd_walk_fits<1024>(n, qcap, c->kd_nrtab)
-                              : blk == 512 ? kd_walk_fits<512>(n, qcap, c->kd_nrtab)
-                                           : kd_walk_fits<256>(n, qcap, c->kd_nrtab)) ? 1 : 0;
+                c->kd_walk = kd_dispatch(blk, [&](auto B) { return kd_walk_fits<decltype(B)::value>(n, qcap, c->kd_nrtab); }) ? 1 : 0;
                 if (const char* e = getenv("SHD_ROUTE_KDWALK")) c->kd_walk = c->kd_walk && atoi(e) != 0;
             }
         }
@@ -660,15 +670,12 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab; k.walk = c->kd_walk;
         k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;
         const int grid = std::min(ns, c->kd_slots);
-        if (c->kd_block == 1024)
-            hipLaunchKernelGGL(sssp_delta_kernel<1024>, dim3(grid), dim3(1024), c->kd_lds, st, k, d_src, ns, d_tgt,
+        kd_dispatch(c->kd_block, [&](auto B) {
+            constexpr int b = decltype(B)::value;
+            hipLaunchKernelGGL(sssp_delta_kernel<b>, dim3(grid), dim3(b), c->kd_lds, st, k, d_src, ns, d_tgt,
                                nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kd_ws, c->kd_stride);
-        else if (c->kd_block == 512)
-            hipLaunchKernelGGL(sssp_delta_kernel<512>, dim3(grid), dim3(512), c->kd_lds, st, k, d_src, ns, d_tgt,
-                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kd_ws, c->kd_stride);
-        else
-            hipLaunchKernelGGL(sssp_delta_kernel<256>, dim3(grid), dim3(256), c->kd_lds, st, k, d_src, ns, d_tgt,
-                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kd_ws, c->kd_stride);
+            return 0;
+        });
         return hip_check(hipGetLastError());
     }
     if (c->sel == 3 && !(dispatch && c->prefer_direct)) {

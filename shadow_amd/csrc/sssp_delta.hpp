@@ -158,6 +158,7 @@ struct KDLayout {
     }
 };
 constexpr int KD_MAXD = 32;           // phase C path walk: arcs held in registers
+constexpr int KD_WQ = 3;              // phase C path walk: targets per thread
 constexpr int KD_RR = 1024;  // parent-record ring slots
 
 // per-workgroup HBM slice: relv f64[n] | wpr u32[n], the parent record of every vertex:
@@ -281,17 +282,11 @@ __device__ inline void kd_relax_list(const uint32_t* wimp, int cnt, int lane, un
         const unsigned long long pm = __ballot(push);
         if (pm) {
             const int ctot = __popcll(pm);
-            int qb = 0, qk = 0;
-            if (lane == 0) {
-                for (;;) {
-                    const int t = __hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    qk = min(ctot, rc - t);
-                    if (qk <= 0) { qk = 0; break; }
-                    if (atomicCAS(tail, t, t + qk) == t) { qb = t; break; }
-                }
-            }
+            // reservation: tail may run past rc; readers clamp it, entries past rc stay pending
+            int qb = 0;
+            if (lane == 0) qb = atomicAdd(tail, ctot);
             qb = __builtin_amdgcn_readfirstlane(qb);
-            qk = __builtin_amdgcn_readfirstlane(qk);
+            const int qk = max(0, min(ctot, rc - qb));
             const int rk = __popcll(pm & (upto >> 1));
             // one copy of the vertex: the queue's (else the pending bitmask)
             if (push && rk < qk) { ring[qb + rk] = (uint16_t)v; atomicAnd(&pend[v >> 6], ~(1ull << (v & 63))); }
@@ -450,11 +445,11 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                     if (lane == 0) {
                         // idle waves only read: busy is raised just around a real grab, so an
                         // idle wave never hides the all-idle state from the others
-                        if (__hip_atomic_load(&sm->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >
+                        if (min(__hip_atomic_load(&sm->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), rc) >
                             __hip_atomic_load(&sm->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
                             atomicAdd(&sm->busy, 1);
                             h = __hip_atomic_load(&sm->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            const int t = __hip_atomic_load(&sm->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            const int t = min(__hip_atomic_load(&sm->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), rc);
                             nn = min(64, t - h);
                             if (nn > 0 && atomicCAS(&sm->head, h, h + nn) != h) nn = 0;
                             if (nn <= 0) { nn = 0; atomicSub(&sm->busy, 1); }
@@ -466,7 +461,7 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                         int fin = 0;
                         if (lane == 0) {
                             const int bz = __hip_atomic_load(&sm->busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            const int t = __hip_atomic_load(&sm->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            const int t = min(__hip_atomic_load(&sm->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), rc);
                             const int hh = __hip_atomic_load(&sm->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             fin = bz == 0 && hh == t;
                         }
@@ -526,7 +521,7 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                         __builtin_amdgcn_wave_barrier();
                         const unsigned long long fl8 = *reinterpret_cast<const unsigned long long*>(wmark + lane * 8);
                         uint32_t rx[KD_P], od[KD_P];
-                        int aa[KD_P], oo[KD_P];
+                        int oo[KD_P];
                         if (dense) {
 #pragma unroll
                             for (int p = 0; p < KD_P; p++) {
@@ -551,12 +546,10 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                         kd_bpermute16(oo, boff, (int)du, obv, od);
                         // out-arc records through a buffer descriptor: 32-bit offsets, and the
                         // positions past the slice's arcs need no clamp (range-checked, read 0)
+                        const int lb = base0 + lane;  // arc of step p: obv[p] + lb + 64 p
 #pragma unroll
-                        for (int p = 0; p < KD_P; p++) {
-                            const int e = base0 + 64 * p + lane;
-                            aa[p] = obv[p] + e;
-                            rx[p] = __builtin_amdgcn_raw_buffer_load_b32(orsrc, (uint32_t)aa[p] << 2, 0, 0);
-                        }
+                        for (int p = 0; p < KD_P; p++)
+                            rx[p] = __builtin_amdgcn_raw_buffer_load_b32(orsrc, ((uint32_t)(obv[p] + lb) << 2) + 256u * p, 0, 0);
                         __builtin_amdgcn_wave_barrier();
 #ifdef SHD_STAMPS
                         if (wid == 0) {
@@ -574,19 +567,25 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                         unsigned dvs[KD_P];
 #pragma unroll
                         for (int p = 0; p < KD_P; p++) dvs[p] = ld16(dist, (int)(rx[p] & 0xFFFFu));
+                        const int nstep = min(KD_P, (total - base0 + 63) >> 6);  // steps holding arcs
 #pragma unroll
                         for (int p = 0; p < KD_P; p++) {
+                            if (p >= nstep) break;
                             const unsigned v = rx[p] & 0xFFFFu, w = rx[p] >> 16;
-                            const bool valid = base0 + 64 * p + lane < total;
+                            const bool valid = lb + 64 * p < total;
                             const unsigned dv = dvs[p], nd = od[p] + w;
                             const bool imp = valid && nd < dv;  // nd < dv <= 0xFFFF: fits u16
                             const unsigned long long im = __ballot(imp);
-                            if (imp) wimp[nimp + __popcll(im & (upto >> 1))] = v | (nd << 16);
+                            if (imp) {
+                                const unsigned r = __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((unsigned)im, (unsigned)nimp));
+                                wimp[r] = v | (nd << 16);
+                            }
                             nimp += __popcll(im);
                             // tie rule: largest w, then smallest (parent, eid) = arc index
                             if (g.fused && valid && dv + w == od[p])
-                                atomicMin(&wkey[oo[p]], ((unsigned long long)(0xFFFFu - w) << 32) | (unsigned)aa[p]);
-                            if (nimp > KD_IMP - 64 || (lastw && p == KD_P - 1)) {
+                                atomicMin(&wkey[oo[p]], ((unsigned long long)(0xFFFFu - w) << 32) | (unsigned)(obv[p] + lb + 64 * p));
+                            if (nimp > KD_IMP - 64 || (lastw && p == nstep - 1)) {
 #ifdef SHD_STAMPS
                                 unsigned long long kr0 = 0;
                                 if (wid == 0) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); kr0 = __builtin_amdgcn_s_memtime(); }
@@ -845,54 +844,68 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
             }
             __syncthreads();
             KD_ACC(19);
-            for (int j0 = tid; j0 < nt; j0 += 2 * B) {
-                int t2[2], cur[2], d2[2];
-                bool act[2];
-                uint32_t pk[2][KD_MAXD / 4];
+            for (int j0 = tid; j0 < nt; j0 += KD_WQ * B) {
+                // KD_WQ targets per thread: independent parent chains in flight
+                int t2[KD_WQ], cur[KD_WQ], d2[KD_WQ];
+                bool act[KD_WQ], bad[KD_WQ];
+                uint32_t pk[KD_WQ][KD_MAXD / 4];
 #pragma unroll
-                for (int q = 0; q < 2; q++) {
+                for (int q = 0; q < KD_WQ; q++) {
                     const int j = j0 + q * B;
                     t2[q] = j < nt ? tgt[j] : -1;
                     act[q] = t2[q] >= 0 && t2[q] < n && t2[q] != s;
                     cur[q] = act[q] ? t2[q] : s;
                     d2[q] = 0;
+                    bad[q] = false;
 #pragma unroll
                     for (int k = 0; k < KD_MAXD / 4; k++) pk[q][k] = 0u;
                 }
-                bool bad[2] = {false, false};
 #pragma unroll
                 for (int k = 0; k < KD_MAXD; k++) {
-                    if (!__any(act[0] || act[1])) break;
-                    uint32_t p[2], rx[2];
+                    bool any = false;
 #pragma unroll
-                    for (int q = 0; q < 2; q++) { p[q] = parv[cur[q]]; rx[q] = rixl[cur[q]]; }
+                    for (int q = 0; q < KD_WQ; q++) any = any || act[q];
+                    if (!__any(any)) break;
+                    uint32_t p[KD_WQ], rx[KD_WQ];
 #pragma unroll
-                    for (int q = 0; q < 2; q++) {
-                        if (!act[q]) continue;
-                        pk[q][k >> 2] |= rx[q] << ((k & 3) * 8);
-                        d2[q] = k + 1;
-                        if (p[q] == 0xFFFFu) { bad[q] = true; act[q] = false; }
-                        else if ((int)p[q] == s) act[q] = false;
-                        else cur[q] = (int)p[q];
+                    for (int q = 0; q < KD_WQ; q++) { p[q] = parv[cur[q]]; rx[q] = rixl[cur[q]]; }
+#pragma unroll
+                    for (int q = 0; q < KD_WQ; q++) {
+                        pk[q][k >> 2] |= act[q] ? rx[q] << ((k & 3) * 8) : 0u;
+                        d2[q] = act[q] ? k + 1 : d2[q];
+                        bad[q] = bad[q] || (act[q] && p[q] == 0xFFFFu);
+                        const bool stop = p[q] == 0xFFFFu || (int)p[q] == s;
+                        cur[q] = act[q] && !stop ? (int)p[q] : cur[q];
+                        act[q] = act[q] && !stop;
                     }
                 }
-                if (act[0] || act[1]) sm->deep = 1;  // the level sweep below redoes the row
-                double rr[2] = {cs, cs};
+                {
+                    bool any = false;
+#pragma unroll
+                    for (int q = 0; q < KD_WQ; q++) any = any || act[q];
+                    if (any) sm->deep = 1;  // the level sweep below redoes the row
+                }
+                double rr[KD_WQ];
+#pragma unroll
+                for (int q = 0; q < KD_WQ; q++) rr[q] = cs;
 #pragma unroll
                 for (int k = KD_MAXD - 1; k >= 0; k--) {
-                    if (!__any(k < d2[0] || k < d2[1])) continue;
-                    double x[2];
+                    bool any = false;
 #pragma unroll
-                    for (int q = 0; q < 2; q++) x[q] = rtl[(pk[q][k >> 2] >> ((k & 3) * 8)) & 0xFFu];
+                    for (int q = 0; q < KD_WQ; q++) any = any || k < d2[q];
+                    if (!__any(any)) continue;
+                    double x[KD_WQ];
 #pragma unroll
-                    for (int q = 0; q < 2; q++)
+                    for (int q = 0; q < KD_WQ; q++) x[q] = rtl[(pk[q][k >> 2] >> ((k & 3) * 8)) & 0xFFu];
+#pragma unroll
+                    for (int q = 0; q < KD_WQ; q++)
                         if (k < d2[q]) rr[q] *= x[q];
                 }
-                double f2[2];
+                double f2[KD_WQ];
 #pragma unroll
-                for (int q = 0; q < 2; q++) f2[q] = g.vf[(t2[q] >= 0 && t2[q] < n) ? t2[q] : s];
+                for (int q = 0; q < KD_WQ; q++) f2[q] = g.vf[(t2[q] >= 0 && t2[q] < n) ? t2[q] : s];
 #pragma unroll
-                for (int q = 0; q < 2; q++) {
+                for (int q = 0; q < KD_WQ; q++) {
                     const int j = j0 + q * B;
                     if (j >= nt) continue;
                     const int t = t2[q];

@@ -561,19 +561,17 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                         // lanes (~5% of arcs) to the wave's list; the tight check for fused parents
                         // is one exec-masked ds_min_u64
                         if (mark) wmark[mslot] = 0;
-                        const bool lastw = base0 + 64 * KD_P >= total;
                         // all KD_P dist reads in flight before the first LDS store of the steps
                         // (the compiler cannot move a read above a store that may alias it)
                         unsigned dvs[KD_P];
 #pragma unroll
                         for (int p = 0; p < KD_P; p++) dvs[p] = ld16(dist, (int)(rx[p] & 0xFFFFu));
-                        const int nstep = min(KD_P, (total - base0 + 63) >> 6);  // steps holding arcs
-#pragma unroll
-                        for (int p = 0; p < KD_P; p++) {
-                            if (p >= nstep) break;
+                        // one step; FULL: every lane holds an arc (all but the slice's last window)
+                        auto step = [&](const int p, auto full) __attribute__((always_inline)) {
                             const unsigned v = rx[p] & 0xFFFFu, w = rx[p] >> 16;
-                            const bool valid = lb + 64 * p < total;
                             const unsigned dv = dvs[p], nd = od[p] + w;
+                            bool valid = true;
+                            if constexpr (!decltype(full)::value) valid = lb + 64 * p < total;
                             const bool imp = valid && nd < dv;  // nd < dv <= 0xFFFF: fits u16
                             const unsigned long long im = __ballot(imp);
                             if (imp) {
@@ -585,26 +583,36 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                             // tie rule: largest w, then smallest (parent, eid) = arc index
                             if (g.fused && valid && dv + w == od[p])
                                 atomicMin(&wkey[oo[p]], ((unsigned long long)(0xFFFFu - w) << 32) | (unsigned)(obv[p] + lb + 64 * p));
-                            if (nimp > KD_IMP - 64 || (lastw && p == nstep - 1)) {
-#ifdef SHD_STAMPS
-                                unsigned long long kr0 = 0;
-                                if (wid == 0) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); kr0 = __builtin_amdgcn_s_memtime(); }
-#endif
-                                kd_relax_list(wimp, nimp, lane, upto, reinterpret_cast<uint32_t*>(dist), pend, wmin, ring,
-                                              &sm->tail, rc, T);
-#ifdef SHD_STAMPS
-                                if (wid == 0) {
-                                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                                    if (lane == 0) sm->acc[29] += __builtin_amdgcn_s_memtime() - kr0;
-                                }
-#endif
-                                nimp = 0;
+                        };
+                        // the list holds KD_IMP >= 3 x 64 entries: a flush check every second step
+                        static_assert(KD_IMP >= 192, "two steps between flush checks");
+                        auto flush = [&]() __attribute__((always_inline)) {
+                            kd_relax_list(wimp, nimp, lane, upto, reinterpret_cast<uint32_t*>(dist), pend, wmin, ring,
+                                          &sm->tail, rc, T);
+                            nimp = 0;
+                        };
+                        if (base0 + 64 * KD_P <= total) {
+#pragma unroll
+                            for (int p = 0; p < KD_P; p += 2) {
+                                step(p, std::true_type{});
+                                step(p + 1, std::true_type{});
+                                if (nimp > KD_IMP - 128) flush();
+                            }
+                        } else {
+                            const int nstep = (total - base0 + 63) >> 6;  // steps holding arcs (< KD_P)
+#pragma unroll
+                            for (int p = 0; p < KD_P; p += 2) {
+                                if (p >= nstep) break;
+                                step(p, std::false_type{});
+                                if (p + 1 < nstep) step(p + 1, std::false_type{});
+                                if (nimp > KD_IMP - 128) flush();
                             }
                         }
 #ifdef SHD_STAMPS
                         if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[28] += t_ - ks0; ks0 = t_; }
 #endif
                     }
+                    if (nimp) kd_relax_list(wimp, nimp, lane, upto, reinterpret_cast<uint32_t*>(dist), pend, wmin, ring, &sm->tail, rc, T);
 #ifdef SHD_STAMPS
                     if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[23] += t_ - ks0; ks0 = t_; sm->acc[25] += (total + 64 * KD_P - 1) / (64 * KD_P); }
 #endif

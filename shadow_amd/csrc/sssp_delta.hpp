@@ -505,71 +505,80 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                     if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[22] += t_ - ks0; ks0 = t_; }
 #endif
                     int nimp = 0;  // improving arcs listed, relaxed when the list fills or the slice ends
-                    for (int base0 = 0; base0 < total; base0 += 64 * KD_P) {
-                        // The loop is issue-bound (15 waves share 4 SIMDs), so it is written for
-                        // few instructions per arc: straight-line, exec-masked atomics, one queue
-                        // reservation per list flush, and a rare slow path for CAS conflicts.
-                        // owners: each lane whose row starts inside the window marks its start
-                        // (lane + 1; marker of position q at byte (q % 64) * 8 + q / 64, so one
-                        // ds_read_b64 per lane fetches its position in all KD_P steps); per step a
-                        // DPP prefix max over the lanes turns the marks into owners, seeded at
-                        // position 0 with the row covering the step's first arc
-                        const int pos = excl - base0;
-                        const bool mark = deg > 0 && pos >= 0 && pos < 64 * KD_P;
-                        const int mslot = ((pos & 63) << 3) | (pos >> 6);
-                        if (mark) wmark[mslot] = (unsigned char)(lane + 1);
-                        __builtin_amdgcn_wave_barrier();
-                        const unsigned long long fl8 = *reinterpret_cast<const unsigned long long*>(wmark + lane * 8);
-                        uint32_t rx[KD_P], od[KD_P];
-                        int oo[KD_P];
-                        if (dense) {
+                    // Windows of KD_P steps x 64 arcs, software-pipelined: the owners and out-arc
+                    // loads of window k+1 are issued before window k is processed, so the L2/HBM
+                    // latency of the records overlaps the dist reads and relaxations.
+                    struct Win {
+                        uint32_t rx[KD_P];   // out-arc records v | w << 16
+                        uint32_t odo[KD_P];  // owner's du | owner lane << 16
+                        int obv[KD_P];       // owner's arc offset: arc of step p = obv + b0 + lane + 64 p
+                    };
+                    Win wa, wb;
+                    const int dul = (int)(du | ((unsigned)lane << 16));
+                    // owners: each lane whose row starts inside the window marks its start (lane + 1;
+                    // marker of position q at byte (q % 64) * 8 + q / 64, so one ds_read_b64 per lane
+                    // fetches its position in all KD_P steps).  Dense slices: owner = running row
+                    // count + mbcnt of the step's start mask; else a DPP prefix max over the marks,
+                    // seeded at position 0 with the row covering the step's first arc.  The loads
+                    // are issued even for a window past the slice's arcs (range-checked no-ops), so
+                    // the load counter the next window waits on is static.
+                    auto issue = [&](Win& W, const int b0) __attribute__((always_inline)) {
+                        const bool live = b0 < total;
+                        if (live) {
+                            const int pos = excl - b0;
+                            const bool mark = deg > 0 && pos >= 0 && pos < 64 * KD_P;
+                            const int mslot = ((pos & 63) << 3) | (pos >> 6);
+                            if (mark) wmark[mslot] = (unsigned char)(lane + 1);
+                            __builtin_amdgcn_wave_barrier();
+                            const unsigned long long fl8 = *reinterpret_cast<const unsigned long long*>(wmark + lane * 8);
+                            int oo[KD_P];
+                            if (dense) {
 #pragma unroll
-                            for (int p = 0; p < KD_P; p++) {
-                                const unsigned long long st = __ballot(((fl8 >> (8 * p)) & 0xFFu) != 0);
-                                const unsigned long long sh = st >> 1;
-                                oo[p] = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(sh >> 32),
-                                            __builtin_amdgcn_mbcnt_lo((unsigned)sh, (unsigned)(rows_before + (int)(st & 1ull) - 1)));
-                                rows_before += __popcll(st);
+                                for (int p = 0; p < KD_P; p++) {
+                                    const unsigned long long st = __ballot(((fl8 >> (8 * p)) & 0xFFu) != 0);
+                                    const unsigned long long sh = st >> 1;
+                                    oo[p] = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(sh >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((unsigned)sh, (unsigned)(rows_before + (int)(st & 1ull) - 1)));
+                                    rows_before += __popcll(st);
+                                }
+                            } else {
+#pragma unroll
+                                for (int p = 0; p < KD_P; p++) {
+                                    const int base = b0 + 64 * p;
+                                    const unsigned long long cov = __ballot(deg > 0 && excl <= base);
+                                    const int carry = cov ? 63 - __clzll((long long)cov) : 0;
+                                    int f = (int)((fl8 >> (8 * p)) & 0xFFu);
+                                    if (lane == 0 && f == 0) f = carry + 1;
+                                    oo[p] = kd_wave_incl_max(f) - 1;
+                                }
                             }
+                            kd_bpermute16(oo, boff, dul, W.obv, W.odo);
+                            if (mark) wmark[mslot] = 0;
                         } else {
 #pragma unroll
-                            for (int p = 0; p < KD_P; p++) {
-                                const int base = base0 + 64 * p;
-                                const unsigned long long cov = __ballot(deg > 0 && excl <= base);
-                                const int carry = cov ? 63 - __clzll((long long)cov) : 0;
-                                int f = (int)((fl8 >> (8 * p)) & 0xFFu);
-                                if (lane == 0 && f == 0) f = carry + 1;
-                                oo[p] = kd_wave_incl_max(f) - 1;
-                            }
+                            for (int p = 0; p < KD_P; p++) { W.obv[p] = 0; W.odo[p] = 0u; }
                         }
-                        int obv[KD_P];
-                        kd_bpermute16(oo, boff, (int)du, obv, od);
-                        // out-arc records through a buffer descriptor: 32-bit offsets, and the
-                        // positions past the slice's arcs need no clamp (range-checked, read 0)
-                        const int lb = base0 + lane;  // arc of step p: obv[p] + lb + 64 p
+                        const int lbw = b0 + lane;
+                        const int soff = live ? 0 : 0x40000000;  // past every record: no-op loads
 #pragma unroll
                         for (int p = 0; p < KD_P; p++)
-                            rx[p] = __builtin_amdgcn_raw_buffer_load_b32(orsrc, ((uint32_t)(obv[p] + lb) << 2) + 256u * p, 0, 0);
-                        __builtin_amdgcn_wave_barrier();
-#ifdef SHD_STAMPS
-                        if (wid == 0) {
-                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                            if (lane == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[27] += t_ - ks0; ks0 = t_; }
-                        }
-#endif
-                        // common path per step: read dist[v], compare, and append the improving
-                        // lanes (~5% of arcs) to the wave's list; the tight check for fused parents
-                        // is one exec-masked ds_min_u64
-                        if (mark) wmark[mslot] = 0;
+                            W.rx[p] = __builtin_amdgcn_raw_buffer_load_b32(orsrc, ((uint32_t)(W.obv[p] + lbw) << 2) + 256u * p, soff, 0);
+                    };
+                    // one window: read dist[v], compare, and append the improving lanes (~5% of
+                    // arcs) to the wave's list; the tight check for fused parents is one exec-masked
+                    // ds_min_u64 per step
+                    auto process = [&](const Win& W, const int b0) __attribute__((always_inline)) {
+                        const int lb = b0 + lane;
                         // all KD_P dist reads in flight before the first LDS store of the steps
                         // (the compiler cannot move a read above a store that may alias it)
                         unsigned dvs[KD_P];
 #pragma unroll
-                        for (int p = 0; p < KD_P; p++) dvs[p] = ld16(dist, (int)(rx[p] & 0xFFFFu));
+                        for (int p = 0; p < KD_P; p++) dvs[p] = ld16(dist, (int)(W.rx[p] & 0xFFFFu));
                         // one step; FULL: every lane holds an arc (all but the slice's last window)
                         auto step = [&](const int p, auto full) __attribute__((always_inline)) {
-                            const unsigned v = rx[p] & 0xFFFFu, w = rx[p] >> 16;
-                            const unsigned dv = dvs[p], nd = od[p] + w;
+                            const unsigned v = W.rx[p] & 0xFFFFu, w = W.rx[p] >> 16;
+                            const unsigned odu = W.odo[p] & 0xFFFFu;
+                            const unsigned dv = dvs[p], nd = odu + w;
                             bool valid = true;
                             if constexpr (!decltype(full)::value) valid = lb + 64 * p < total;
                             const bool imp = valid && nd < dv;  // nd < dv <= 0xFFFF: fits u16
@@ -581,8 +590,8 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                             }
                             nimp += __popcll(im);
                             // tie rule: largest w, then smallest (parent, eid) = arc index
-                            if (g.fused && valid && dv + w == od[p])
-                                atomicMin(&wkey[oo[p]], ((unsigned long long)(0xFFFFu - w) << 32) | (unsigned)(obv[p] + lb + 64 * p));
+                            if (g.fused && valid && dv + w == odu)
+                                atomicMin(&wkey[W.odo[p] >> 16], ((unsigned long long)(0xFFFFu - w) << 32) | (unsigned)(W.obv[p] + lb + 64 * p));
                         };
                         // the list holds KD_IMP >= 3 x 64 entries: a flush check every second step
                         static_assert(KD_IMP >= 192, "two steps between flush checks");
@@ -591,7 +600,7 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                                           &sm->tail, rc, T);
                             nimp = 0;
                         };
-                        if (base0 + 64 * KD_P <= total) {
+                        if (b0 + 64 * KD_P <= total) {
 #pragma unroll
                             for (int p = 0; p < KD_P; p += 2) {
                                 step(p, std::true_type{});
@@ -599,7 +608,7 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                                 if (nimp > KD_IMP - 128) flush();
                             }
                         } else {
-                            const int nstep = (total - base0 + 63) >> 6;  // steps holding arcs (< KD_P)
+                            const int nstep = (total - b0 + 63) >> 6;  // steps holding arcs (< KD_P)
 #pragma unroll
                             for (int p = 0; p < KD_P; p += 2) {
                                 if (p >= nstep) break;
@@ -608,9 +617,16 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                                 if (nimp > KD_IMP - 128) flush();
                             }
                         }
-#ifdef SHD_STAMPS
-                        if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[28] += t_ - ks0; ks0 = t_; }
-#endif
+                    };
+                    issue(wa, 0);
+                    for (int b0 = 0; b0 < total;) {
+                        issue(wb, b0 + 64 * KD_P);
+                        process(wa, b0);
+                        b0 += 64 * KD_P;
+                        if (b0 >= total) break;
+                        issue(wa, b0 + 64 * KD_P);
+                        process(wb, b0);
+                        b0 += 64 * KD_P;
                     }
                     if (nimp) kd_relax_list(wimp, nimp, lane, upto, reinterpret_cast<uint32_t*>(dist), pend, wmin, ring, &sm->tail, rc, T);
 #ifdef SHD_STAMPS

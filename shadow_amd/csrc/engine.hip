@@ -318,20 +318,24 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
             std::nth_element(ws.begin(), ws.begin() + k, ws.end());
             delta = std::max(1, ws[k]);
         }
-        int blk = n > 16384 ? 1024 : n > 4096 ? 512 : 256;
+        // one 1024-thread workgroup per CU when dist fills the LDS; smaller graphs run several
+        // 256-thread workgroups (sources) per CU
+        int blk = n > 16384 ? 1024 : 256;
         if (const char* e = getenv("SHD_ROUTE_KDBLOCK")) {
             const int b = atoi(e);
             if (b == 256 || b == 512 || b == 768 || b == 1024) blk = b;
         }
         const size_t base = kd_dispatch(blk, [&](auto B) { return kd_lds_bytes<decltype(B)::value>(n, 0); });
         if (base + 2 * 512 <= kLdsBudget) {
-            // queue: the rest of the CU's LDS at one workgroup per CU (large n), else enough
-            // for a few workgroups per CU
             // work queue: the rest of the CU's LDS at one workgroup per CU (large n), else
             // enough for a few workgroups per CU
             int qcap;
-            if (blk >= 768) qcap = (int)std::min<size_t>((size_t)n, (kLdsBudget - base - 64) / 2);
-            else qcap = std::min(n, std::max(1024, n / 2));
+            if (blk < 768) {
+                // four 256-thread workgroups per CU: the queue takes what is left of a quarter
+                const size_t quarter = kLdsBudget / 4;
+                qcap = base + 64 + 2 * 512 <= quarter ? (int)std::min<size_t>((size_t)n, (quarter - base - 64) / 2)
+                                                      : std::min(n, std::max(1024, n / 2));
+            } else qcap = (int)std::min<size_t>((size_t)n, (kLdsBudget - base - 64) / 2);
             if (const char* e = getenv("SHD_ROUTE_QCAP")) qcap = std::min(qcap, std::max(64, atoi(e)));
             qcap &= ~7;
             const size_t lds = kd_dispatch(blk, [&](auto B) { return kd_lds_bytes<decltype(B)::value>(n, qcap); });
@@ -384,7 +388,8 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 if (rc) return rc;
                 c->kd_nlight = lrow[n];
                 c->kd_nrtab = std::max<int>(1, (int)rtab.size());
-                const int per_cu = std::max(1, std::min((int)(kLdsBudget / lds), 2048 / blk));
+                // 16 waves per CU: 4 per SIMD at <= 128 VGPRs (amdgpu_waves_per_eu(4))
+                const int per_cu = std::max(1, std::min((int)(kLdsBudget / lds), 1024 / blk));
                 c->kd_slots = 256 * per_cu;
                 // tests cap the grid so that every workgroup runs many sources in turn
                 if (const char* e = getenv("SHD_ROUTE_KDGRID")) c->kd_slots = std::max(1, std::min(c->kd_slots, atoi(e)));
@@ -429,7 +434,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
             c->kb_npart = npart;
         }
     }
-    c->sel = c->kb ? 2 : c->k32 ? 1 : c->kd ? 4 : c->k16 ? 3 : 0;  // K32 still beats KD on C3-class graphs
+    c->sel = c->kb ? 2 : c->kd ? 4 : c->k32 ? 1 : c->k16 ? 3 : 0;  // K32 still beats KD on C3-class graphs
     return SHD_ROUTE_OK;
 }
 

@@ -159,7 +159,9 @@ struct KDLayout {
 };
 constexpr int KD_MAXD = 32;           // phase C path walk: arcs held in registers
 constexpr int KD_WQ = 3;              // phase C path walk: targets per thread
-constexpr int KD_RR = 1024;  // parent-record ring slots
+constexpr int KD_RR = 1024;  // parent-record ring slots (1024-thread workgroups; smaller ones use 256)
+template <int B>
+constexpr int kd_rr() { return B >= 1024 ? KD_RR : 256; }
 
 // per-workgroup HBM slice: relv f64[n] | wpr u32[n], the parent record of every vertex:
 // parent << 16 | ridx of the parent arc (KD_SRC_MARK for the source)
@@ -297,14 +299,15 @@ __device__ inline void kd_relax_list(const uint32_t* wimp, int cnt, int lane, un
 }
 
 template <int B>
-__global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __restrict__ src, int ns,
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sssp_delta_kernel(DevDelta g, const int* __restrict__ src, int ns,
                                                        const int* __restrict__ tgt, int nt, long long ld,
                                                        double* __restrict__ lat_out, double* __restrict__ rel_out,
                                                        double* __restrict__ row_min, int* __restrict__ err,
                                                        char* __restrict__ ws, size_t ws_stride) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int n = g.n, nw = g.nw;
-    const KDLayout<B> L = KDLayout<B>::make(n, g.rc, KD_RR);
+    constexpr int RR = kd_rr<B>();
+    const KDLayout<B> L = KDLayout<B>::make(n, g.rc, RR);
     KDSmall* sm = reinterpret_cast<KDSmall*>(smem);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     unsigned long long* wkey = reinterpret_cast<unsigned long long*>(smem + L.wkey) + wid * 64;
@@ -345,7 +348,7 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
         const double cs = isnan(fs) ? 1.0 : 1.0 * fs;
         for (int v = tid; v < (n + 2) / 2; v += B) reinterpret_cast<uint32_t*>(dist)[v] = 0xFFFFFFFFu;
         for (int k = tid; k < nw; k += B) { pend[k] = 0ull; wmin[k] = 0xFFFFFFFFu; fix[k] = 0ull; }
-        for (int q = tid; q < KD_RR; q += B) rrec[q] = make_uint2(0u, 0xFFFFFFFFu);  // phases B/C reuse the area
+        for (int q = tid; q < RR; q += B) rrec[q] = make_uint2(0u, 0xFFFFFFFFu);  // phases B/C reuse the area
         for (int q = lane; q < 64 * KD_P; q += 64) wmark[q] = 0;  // phase C reuses it
         if (tid == 0) {
             sm->gmin[0] = sm->gmin[1] = 0xFFFFFFFFu;
@@ -649,13 +652,13 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                         int rb = 0;
                         if (lane == 0) {
                             rb = atomicAdd(&sm->rtail, nr);
-                            for (int w8 = 0; rb + nr - __hip_atomic_load(&sm->rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > KD_RR
+                            for (int w8 = 0; rb + nr - __hip_atomic_load(&sm->rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > RR
                                              && w8 < (1 << 22); w8++)
                                 __builtin_amdgcn_s_sleep(1);
                         }
                         rb = __builtin_amdgcn_readfirstlane(rb);
                         if (hasrec) {  // one 64-bit LDS write: the writer never sees half a record
-                            const int slot = (rb + __popcll(rm & (upto >> 1))) & (KD_RR - 1);
+                            const int slot = (rb + __popcll(rm & (upto >> 1))) & (RR - 1);
                             *reinterpret_cast<volatile unsigned long long*>(&rrec[slot]) =
                                 (unsigned long long)prec | ((unsigned long long)((uint32_t)u | (du << 16)) << 32);
                         }
@@ -675,7 +678,7 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
                     if (rt > rd) {
                         const int k = min(64, rt - rd);
                         if (lane < k) {
-                            const int slot = (rd + lane) & (KD_RR - 1);
+                            const int slot = (rd + lane) & (RR - 1);
                             volatile unsigned long long* sp = reinterpret_cast<volatile unsigned long long*>(&rrec[slot]);
                             unsigned long long rv = *sp;
                             for (int w8 = 0; (rv >> 32) == 0xFFFFFFFFull && w8 < (1 << 22); w8++) {
@@ -1103,12 +1106,12 @@ __global__ __launch_bounds__(B) void sssp_delta_kernel(DevDelta g, const int* __
 }
 
 template <int B>
-inline size_t kd_lds_bytes(int n, int rc) { return KDLayout<B>::make(n, rc, KD_RR).total; }
+inline size_t kd_lds_bytes(int n, int rc) { return KDLayout<B>::make(n, rc, kd_rr<B>()).total; }
 
 // phase C by path walks: u8 reliability index per vertex + the table itself in LDS
 template <int B>
 inline bool kd_walk_fits(int n, int rc, int nrtab) {
-    const KDLayout<B> L = KDLayout<B>::make(n, rc, KD_RR);
+    const KDLayout<B> L = KDLayout<B>::make(n, rc, kd_rr<B>());
     return nrtab <= 256 && L.rtabl + 8 * (size_t)nrtab <= L.total;
 }
 

@@ -9,7 +9,7 @@ import json
 import os
 import sys
 
-HOT = ("sssp_batch_kernel", "path_attr_kernel", "sssp_k32_kernel", "sssp_rows_kernel", "sssp_k16")
+HOT = ("sssp_batch_kernel", "path_attr_kernel", "sssp_k32_kernel", "sssp_rows_kernel", "sssp_k16", "sssp_delta_kernel")
 
 
 def load(path):

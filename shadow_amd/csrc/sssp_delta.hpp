@@ -158,7 +158,9 @@ struct KDLayout {
     }
 };
 constexpr int KD_MAXD = 32;           // phase C path walk: arcs held in registers
-constexpr int KD_WQ = 3;              // phase C path walk: targets per thread
+constexpr int KD_WQ = 4;              // phase C path walk: targets per thread
+constexpr int KD_ONE = 254;           // phase C: rtab slot holding 1.0 (the source's own step)
+constexpr int KD_NAN = 255;           // phase C: rtab slot holding NaN (unreachable vertices)
 constexpr int KD_RR = 1024;  // parent-record ring slots (1024-thread workgroups; smaller ones use 256)
 template <int B>
 constexpr int kd_rr() { return B >= 1024 ? KD_RR : 256; }
@@ -844,72 +846,76 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             // parv u16 + rix u8 (index of the parent arc's reliability) + rtab in LDS; each
             // target walks <= KD_MAXD arcs to the source, then folds the product source-first
             // (the order the level sweep multiplies in, so the bits agree)
+            // rtl[KD_ONE] = 1.0 is the source's own "arc" (a walk parked at the source keeps
+            // multiplying by an exact 1.0) and rtl[KD_NAN] marks unreachable vertices
             uint8_t* rixl = reinterpret_cast<uint8_t*>(smem + L.rix);
             double* rtl = reinterpret_cast<double*>(smem + L.rtabl);
-            for (int k = tid; k < g.nrtab; k += B) rtl[k] = g.rtab[k];
+            for (int k = tid; k < 256; k += B)
+                rtl[k] = k < g.nrtab ? g.rtab[k] : k == KD_ONE ? 1.0 : NAN;
             for (int v0 = tid; v0 < n; v0 += B * 8) {
-                uint32_t pr[8];
+                uint32_t pr[8], dv8[8];
 #pragma unroll
-                for (int q = 0; q < 8; q++) pr[q] = wpr[min(v0 + q * B, n - 1)];
+                for (int q = 0; q < 8; q++) {
+                    pr[q] = wpr[min(v0 + q * B, n - 1)];
+                    dv8[q] = dist[min(v0 + q * B, n - 1)];
+                }
                 uint32_t px[8], pi[8];
 #pragma unroll
                 for (int q = 0; q < 8; q++) {
-                    const bool bad = pr[q] >= KD_SRC_MARK;
+                    const bool bad = pr[q] >= KD_SRC_MARK || dv8[q] == 0xFFFFu;
                     const bool lt = !bad && (pr[q] & KD_LIGHT);
                     const uint32_t ix = bad ? 0u : (pr[q] & ~KD_LIGHT);
                     if (lt) { const uint2 r2 = g.lrec[min((int)ix, g.nlight - 1)]; px[q] = r2.x; pi[q] = r2.y; }
                     else { px[q] = g.orec[ix]; pi[q] = g.oridx[ix]; }
                 }
+                // (each thread overwrites only the dist entries it read itself)
 #pragma unroll
                 for (int q = 0; q < 8; q++) {
                     const int v = v0 + q * B;
                     if (v >= n) continue;
-                    parv[v] = pr[q] == KD_SRC_MARK ? (uint16_t)v
-                            : pr[q] == KD_NONE ? (uint16_t)0xFFFFu : (uint16_t)(px[q] & 0xFFFFu);
-                    rixl[v] = (uint8_t)min(pi[q] & 0xFFFFu, (uint32_t)(g.nrtab - 1));
+                    const bool src_v = v == s, unr = !src_v && dv8[q] == 0xFFFFu;
+                    parv[v] = src_v || unr ? (uint16_t)s : (uint16_t)(px[q] & 0xFFFFu);
+                    rixl[v] = src_v ? (uint8_t)KD_ONE : unr ? (uint8_t)KD_NAN
+                                                     : (uint8_t)min(pi[q] & 0xFFFFu, (uint32_t)(g.nrtab - 1));
                 }
             }
             __syncthreads();
             KD_ACC(19);
             for (int j0 = tid; j0 < nt; j0 += KD_WQ * B) {
-                // KD_WQ targets per thread: independent parent chains in flight
-                int t2[KD_WQ], cur[KD_WQ], d2[KD_WQ];
-                bool act[KD_WQ], bad[KD_WQ];
+                // KD_WQ targets per thread: independent parent chains in flight.  A chain that
+                // reaches the source stays there (parv[s] = s, factor 1.0), so a step is two LDS
+                // reads and a byte insert, and the wave stops when every chain is parked.
+                int t2[KD_WQ], cur[KD_WQ];
                 uint32_t pk[KD_WQ][KD_MAXD / 4];
 #pragma unroll
                 for (int q = 0; q < KD_WQ; q++) {
                     const int j = j0 + q * B;
                     t2[q] = j < nt ? tgt[j] : -1;
-                    act[q] = t2[q] >= 0 && t2[q] < n && t2[q] != s;
-                    cur[q] = act[q] ? t2[q] : s;
-                    d2[q] = 0;
-                    bad[q] = false;
+                    cur[q] = t2[q] >= 0 && t2[q] < n ? t2[q] : s;
 #pragma unroll
                     for (int k = 0; k < KD_MAXD / 4; k++) pk[q][k] = 0u;
                 }
+                int kmax = 0;  // wave-uniform: steps taken
 #pragma unroll
                 for (int k = 0; k < KD_MAXD; k++) {
                     bool any = false;
 #pragma unroll
-                    for (int q = 0; q < KD_WQ; q++) any = any || act[q];
+                    for (int q = 0; q < KD_WQ; q++) any = any || cur[q] != s;
                     if (!__any(any)) break;
+                    kmax = k + 1;
                     uint32_t p[KD_WQ], rx[KD_WQ];
 #pragma unroll
                     for (int q = 0; q < KD_WQ; q++) { p[q] = parv[cur[q]]; rx[q] = rixl[cur[q]]; }
 #pragma unroll
                     for (int q = 0; q < KD_WQ; q++) {
-                        pk[q][k >> 2] |= act[q] ? rx[q] << ((k & 3) * 8) : 0u;
-                        d2[q] = act[q] ? k + 1 : d2[q];
-                        bad[q] = bad[q] || (act[q] && p[q] == 0xFFFFu);
-                        const bool stop = p[q] == 0xFFFFu || (int)p[q] == s;
-                        cur[q] = act[q] && !stop ? (int)p[q] : cur[q];
-                        act[q] = act[q] && !stop;
+                        pk[q][k >> 2] |= rx[q] << ((k & 3) * 8);
+                        cur[q] = (int)p[q];
                     }
                 }
                 {
                     bool any = false;
 #pragma unroll
-                    for (int q = 0; q < KD_WQ; q++) any = any || act[q];
+                    for (int q = 0; q < KD_WQ; q++) any = any || cur[q] != s;
                     if (any) sm->deep = 1;  // the level sweep below redoes the row
                 }
                 double rr[KD_WQ];
@@ -917,16 +923,12 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                 for (int q = 0; q < KD_WQ; q++) rr[q] = cs;
 #pragma unroll
                 for (int k = KD_MAXD - 1; k >= 0; k--) {
-                    bool any = false;
-#pragma unroll
-                    for (int q = 0; q < KD_WQ; q++) any = any || k < d2[q];
-                    if (!__any(any)) continue;
+                    if (k >= kmax) continue;
                     double x[KD_WQ];
 #pragma unroll
                     for (int q = 0; q < KD_WQ; q++) x[q] = rtl[(pk[q][k >> 2] >> ((k & 3) * 8)) & 0xFFu];
 #pragma unroll
-                    for (int q = 0; q < KD_WQ; q++)
-                        if (k < d2[q]) rr[q] *= x[q];
+                    for (int q = 0; q < KD_WQ; q++) rr[q] *= x[q];
                 }
                 double f2[KD_WQ];
 #pragma unroll
@@ -937,7 +939,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     if (j >= nt) continue;
                     const int t = t2[q];
                     double Rv = NAN;
-                    if (t >= 0 && t < n && !bad[q]) {
+                    if (t >= 0 && t < n) {
                         if (t == s) Rv = isnan(g.self_w[s]) ? NAN : cs * g.self_r[s];
                         else Rv = isnan(f2[q]) ? rr[q] : rr[q] * f2[q];
                     }
@@ -1112,7 +1114,7 @@ inline size_t kd_lds_bytes(int n, int rc) { return KDLayout<B>::make(n, rc, kd_r
 template <int B>
 inline bool kd_walk_fits(int n, int rc, int nrtab) {
     const KDLayout<B> L = KDLayout<B>::make(n, rc, kd_rr<B>());
-    return nrtab <= 256 && L.rtabl + 8 * (size_t)nrtab <= L.total;
+    return nrtab <= KD_ONE && L.rtabl + 8 * 256 <= L.total;
 }
 
 }  // namespace shd

@@ -56,7 +56,7 @@ struct shd_route {
     uint16_t* d_kd_oridx = nullptr; // rtab index per out-arc
     uint32_t* d_kd_lrec = nullptr;  // light in-arc records (2 x u32 per arc)
     double* d_kd_rtab = nullptr;    // distinct reliabilities
-    int kd_nlight = 0, kd_nrtab = 1, kd_walk = 0;
+    int kd_nlight = 0, kd_nrtab = 1, kd_walk = 0, kd_packed = 0;
     char* d_kd_ws = nullptr;
     int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD
     uint64_t device_bytes = 0;
@@ -367,7 +367,15 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 // out-arc records {v | w << 16, ridx}; light in-CSR records {u | w << 16, ridx}
                 // (light = w < delta; directed graphs: every in-arc, fused parents are off)
                 std::vector<uint32_t> orec(c->nnz);
-                for (int a = 0; a < c->nnz; a++) orec[a] = (uint32_t)col[a] | ((uint32_t)w[a] << 16);
+                // packed records (w < 256, <= 256 reliabilities): v | w << 16 | ridx << 24, so the
+                // fused parent's reliability index comes with the arc the expansion loaded
+                int maxw = 0;
+                for (int a = 0; a < c->nnz; a++) maxw = std::max(maxw, (int)w[a]);
+                bool packed = maxw < 256 && rtab.size() <= 256;
+                if (const char* e = getenv("SHD_ROUTE_KDPACK")) packed = packed && atoi(e) != 0;
+                for (int a = 0; a < c->nnz; a++)
+                    orec[a] = (uint32_t)col[a] | ((uint32_t)w[a] << 16) | (packed ? (uint32_t)ridx_out[a] << 24 : 0u);
+                c->kd_packed = packed ? 1 : 0;
                 std::vector<int> lrow(n + 1, 0);
                 std::vector<uint32_t> lrec;
                 for (int v = 0; v < n; v++) {
@@ -672,7 +680,7 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         k.fused = c->directed ? 0 : 1; k.rc = c->kd_qcap;
         k.row = c->d_row; k.orec = c->d_kd_orec; k.oridx = c->d_kd_oridx;
         k.nnz = c->nnz; k.lrow = c->d_kd_lstart; k.lrec = reinterpret_cast<const uint2*>(c->d_kd_lrec); k.nlight = c->kd_nlight;
-        k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab; k.walk = c->kd_walk;
+        k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab; k.walk = c->kd_walk; k.packed = c->kd_packed;
         k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;
         const int grid = std::min(ns, c->kd_slots);
         kd_dispatch(c->kd_block, [&](auto B) {

@@ -64,7 +64,6 @@ constexpr int KD_W = 8;      // bitmask words per wave step in the gather / read
 constexpr int KD_IMP = 192;  // per-wave list of improving arcs (v | nd << 16), flushed past 128
 constexpr uint32_t KD_NONE = 0xFFFFFFFFu;      // no parent recorded
 constexpr uint32_t KD_SRC_MARK = 0xFFFFFFFEu;  // parent record of the source itself
-constexpr uint32_t KD_LIGHT = 0x80000000u;     // parent record = light in-arc index | KD_LIGHT
 
 struct DevDelta {
     int n, nw;
@@ -83,6 +82,7 @@ struct DevDelta {
     const double* __restrict__ rtab;    // distinct 1 - loss values, indexed by ridx
     int nrtab;
     int walk;                           // phase C by path walks in LDS (nrtab <= 256, fits)
+    int packed;                         // orec = v | w << 16 | ridx << 24 (w < 256, nrtab <= 256)
     const double* __restrict__ vf;
     const double* __restrict__ self_w;
     const double* __restrict__ self_r;
@@ -166,7 +166,7 @@ template <int B>
 constexpr int kd_rr() { return B >= 1024 ? KD_RR : 256; }
 
 // per-workgroup HBM slice: relv f64[n] | wpr u32[n], the parent record of every vertex:
-// parent << 16 | ridx of the parent arc (KD_SRC_MARK for the source)
+// parent | ridx << 16 of the parent arc (KD_SRC_MARK for the source)
 __host__ __device__ inline size_t kd_ws_stride(int n) { return a16(sizeof(double) * n) + a16(sizeof(uint32_t) * n) + 256; }
 
 // LDS-only workgroup barrier: outstanding global stores (output rows) stay in flight.
@@ -326,6 +326,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
     const unsigned bound = (unsigned)g.bound;
     const unsigned delta = (unsigned)g.delta;
     const int qcap = L.qcap;
+    const unsigned wmask = g.packed ? 0xFFu : 0xFFFFu;
     const __amdgpu_buffer_rsrc_t orsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(g.orec), (short)0, g.nnz * 4, 0x00020000);
     const int rc = g.rc;
@@ -581,7 +582,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         for (int p = 0; p < KD_P; p++) dvs[p] = ld16(dist, (int)(W.rx[p] & 0xFFFFu));
                         // one step; FULL: every lane holds an arc (all but the slice's last window)
                         auto step = [&](const int p, auto full) __attribute__((always_inline)) {
-                            const unsigned v = W.rx[p] & 0xFFFFu, w = W.rx[p] >> 16;
+                            const unsigned v = W.rx[p] & 0xFFFFu, w = (W.rx[p] >> 16) & wmask;
                             const unsigned odu = W.odo[p] & 0xFFFFu;
                             const unsigned dv = dvs[p], nd = odu + w;
                             bool valid = true;
@@ -594,9 +595,13 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                                 wimp[r] = v | (nd << 16);
                             }
                             nimp += __popcll(im);
-                            // tie rule: largest w, then smallest (parent, eid) = arc index
-                            if (g.fused && valid && dv + w == odu)
-                                atomicMin(&wkey[W.odo[p] >> 16], ((unsigned long long)(0xFFFFu - w) << 32) | (unsigned)(W.obv[p] + lb + 64 * p));
+                            // tie rule: largest w, then smallest (parent, eid) = smallest v (simple
+                            // graph, rows sorted by (v, eid)); the low word is the record the
+                            // writer stores: parent | ridx << 16 (packed) or the arc index
+                            if (g.fused && valid && dv + w == odu) {
+                                const uint32_t lo = g.packed ? ((W.rx[p] & 0xFFFFu) | ((W.rx[p] >> 8) & 0xFF0000u)) : (uint32_t)(W.obv[p] + lb + 64 * p);
+                                atomicMin(&wkey[W.odo[p] >> 16], ((unsigned long long)(((0xFFFFu - w) << 16) | v) << 32) | lo);
+                            }
                         };
                         // the list holds KD_IMP >= 3 x 64 entries: a flush check every second step
                         static_assert(KD_IMP >= 192, "two steps between flush checks");
@@ -646,7 +651,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     uint32_t prec = KD_NONE;
                     if (g.fused && hasrec) {
                         const unsigned long long kk = wkey[lane];
-                        if (kk != ~0ull && (0xFFFFu - (unsigned)(kk >> 32)) >= delta) prec = (uint32_t)kk;  // arc index
+                        if (kk != ~0ull && (0xFFFFu - (unsigned)(kk >> 48)) >= delta) prec = (uint32_t)kk;  // heavy winner
                     }
                     const unsigned long long rm = __ballot(hasrec);
                     const int nr = __popcll(rm);
@@ -678,23 +683,49 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                 for (;;) {
                     const int rt = __hip_atomic_load(&sm->rtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if (rt > rd) {
-                        const int k = min(64, rt - rd);
-                        if (lane < k) {
-                            const int slot = (rd + lane) & (RR - 1);
-                            volatile unsigned long long* sp = reinterpret_cast<volatile unsigned long long*>(&rrec[slot]);
-                            unsigned long long rv = *sp;
-                            for (int w8 = 0; (rv >> 32) == 0xFFFFFFFFull && w8 < (1 << 22); w8++) {
-                                __builtin_amdgcn_s_sleep(1);
-                                rv = *sp;
+                        // up to 4 x 64 records per pass: the winners' parent and reliability
+                        // index are gathered here (the writer has the latency to spare), so
+                        // wpr holds parent | ridx << 16 and phase C decodes without gathers
+                        const int k = min(4 * 64, rt - rd);
+                        int uu[4];
+                        uint32_t xx[4];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            uu[q] = -1;
+                            xx[q] = KD_NONE;
+                            if (q * 64 + lane < k) {
+                                const int slot = (rd + q * 64 + lane) & (RR - 1);
+                                volatile unsigned long long* sp = reinterpret_cast<volatile unsigned long long*>(&rrec[slot]);
+                                unsigned long long rv = *sp;
+                                for (int w8 = 0; (rv >> 32) == 0xFFFFFFFFull && w8 < (1 << 22); w8++) {
+                                    __builtin_amdgcn_s_sleep(1);
+                                    rv = *sp;
+                                }
+                                const uint32_t x = (uint32_t)rv, y = (uint32_t)(rv >> 32);
+                                *sp = 0xFFFFFFFF00000000ull;
+                                const int u = (int)(y & 0xFFFFu);
+                                if (y != 0xFFFFFFFFu && ld16(dist, u) == (y >> 16)) {  // from u's latest expansion
+                                    const unsigned long long bit = 1ull << (u & 63);
+                                    if (x != KD_NONE) { uu[q] = u; xx[q] = x; atomicAnd(&fix[u >> 6], ~bit); }
+                                    else atomicOr(&fix[u >> 6], bit);
+                                }
                             }
-                            const uint32_t x = (uint32_t)rv, y = (uint32_t)(rv >> 32);
-                            *sp = 0xFFFFFFFF00000000ull;
-                            const int u = (int)(y & 0xFFFFu);
-                            if (y != 0xFFFFFFFFu && ld16(dist, u) == (y >> 16)) {  // from u's latest expansion
-                                const unsigned long long bit = 1ull << (u & 63);
-                                if (x != KD_NONE) { wpr[u] = x; atomicAnd(&fix[u >> 6], ~bit); }
-                                else atomicOr(&fix[u >> 6], bit);
+                        }
+                        if (g.packed) {  // the record already is parent | ridx << 16
+#pragma unroll
+                            for (int q = 0; q < 4; q++)
+                                if (uu[q] >= 0) wpr[uu[q]] = xx[q];
+                        } else {  // arc index: gather the parent and its reliability index
+                            uint32_t pv[4], pi[4];
+#pragma unroll
+                            for (int q = 0; q < 4; q++) {
+                                const uint32_t a = uu[q] >= 0 ? xx[q] : 0u;
+                                pv[q] = g.orec[a];
+                                pi[q] = g.oridx[a];
                             }
+#pragma unroll
+                            for (int q = 0; q < 4; q++)
+                                if (uu[q] >= 0) wpr[uu[q]] = (pv[q] & 0xFFFFu) | (pi[q] << 16);
                         }
                         rd += k;
                         __builtin_amdgcn_wave_barrier();
@@ -781,10 +812,14 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     int f = -1;
+                    uint32_t rec = KD_NONE;  // parent | ridx << 16 of the first tight arc
 #pragma unroll
                     for (int e = KD_TAIL - 1; e >= 0; e--)
-                        if (a4[q] + e < r4[q] && dt[q][e] + (rc[q][e].x >> 16) == d4[q]) f = e;
-                    out_a[q] = f >= 0 ? KD_LIGHT | (uint32_t)(a4[q] + f) : KD_NONE;
+                        if (a4[q] + e < r4[q] && dt[q][e] + (rc[q][e].x >> 16) == d4[q]) {
+                            f = e;
+                            rec = (rc[q][e].x & 0xFFFFu) | (rc[q][e].y << 16);
+                        }
+                    out_a[q] = rec;
                     if (v4[q] >= 0 && f < 0) {
                         if (r4[q] - a4[q] > KD_TAIL) {  // long tail: one wave per vertex below
                             const int at = atomicAdd(&sm->qcur[rnd], 1);
@@ -809,7 +844,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     const uint2 rc = g.lrec[min(a, last_arc)];
                     const bool tight = a < r1 && ld16(dist, (int)(rc.x & 0xFFFFu)) + (rc.x >> 16) == dv;
                     const unsigned long long tm = __ballot(tight);
-                    if (tm) fr = KD_LIGHT | (uint32_t)(a0 + __ffsll((long long)tm) - 1);
+                    if (tm) fr = (uint32_t)__builtin_amdgcn_readlane((int)((rc.x & 0xFFFFu) | (rc.y << 16)), __ffsll((long long)tm) - 1);
                 }
                 if (lane == 0) {
                     if (fr == KD_NONE) raise_err(err, SHD_ROUTE_EUNREACH);
@@ -859,24 +894,15 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     pr[q] = wpr[min(v0 + q * B, n - 1)];
                     dv8[q] = dist[min(v0 + q * B, n - 1)];
                 }
-                uint32_t px[8], pi[8];
-#pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const bool bad = pr[q] >= KD_SRC_MARK || dv8[q] == 0xFFFFu;
-                    const bool lt = !bad && (pr[q] & KD_LIGHT);
-                    const uint32_t ix = bad ? 0u : (pr[q] & ~KD_LIGHT);
-                    if (lt) { const uint2 r2 = g.lrec[min((int)ix, g.nlight - 1)]; px[q] = r2.x; pi[q] = r2.y; }
-                    else { px[q] = g.orec[ix]; pi[q] = g.oridx[ix]; }
-                }
                 // (each thread overwrites only the dist entries it read itself)
 #pragma unroll
                 for (int q = 0; q < 8; q++) {
                     const int v = v0 + q * B;
                     if (v >= n) continue;
                     const bool src_v = v == s, unr = !src_v && dv8[q] == 0xFFFFu;
-                    parv[v] = src_v || unr ? (uint16_t)s : (uint16_t)(px[q] & 0xFFFFu);
+                    parv[v] = src_v || unr ? (uint16_t)s : (uint16_t)(pr[q] & 0xFFFFu);
                     rixl[v] = src_v ? (uint8_t)KD_ONE : unr ? (uint8_t)KD_NAN
-                                                     : (uint8_t)min(pi[q] & 0xFFFFu, (uint32_t)(g.nrtab - 1));
+                                                     : (uint8_t)min(pr[q] >> 16, (uint32_t)(g.nrtab - 1));
                 }
             }
             __syncthreads();
@@ -952,30 +978,20 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         }
         const bool sweep = !(g.walk && rrow) || sm->deep;
         if (sweep) {
-        // parent records: out-arc index (fused), KD_LIGHT | light in-arc index (fix-up)
-        // parent records: out-arc index (fused), KD_LIGHT | light in-arc index (fix-up)
+        // parent records: parent | ridx << 16 (writer wave and phase B), KD_SRC_MARK at s
         for (int v0 = tid; v0 < n; v0 += B * 8) {
             uint32_t pr[8];
 #pragma unroll
             for (int q = 0; q < 8; q++) pr[q] = wpr[min(v0 + q * B, n - 1)];
-            uint32_t px[8], pi[8];
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const bool bad = pr[q] >= KD_SRC_MARK;
-                const bool lt = !bad && (pr[q] & KD_LIGHT);
-                const uint32_t ix = bad ? 0u : (pr[q] & ~KD_LIGHT);
-                if (lt) { const uint2 r2 = g.lrec[min((int)ix, g.nlight - 1)]; px[q] = r2.x; pi[q] = r2.y; }
-                else { px[q] = g.orec[ix]; pi[q] = g.oridx[ix]; }
-            }
             double rr[8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) rr[q] = g.rtab[min((int)(pi[q] & 0xFFFFu), g.nrtab - 1)];
+            for (int q = 0; q < 8; q++) rr[q] = g.rtab[min((int)(pr[q] >> 16), g.nrtab - 1)];
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const int v = v0 + q * B;
                 if (v >= n) continue;
                 const bool src_v = pr[q] == KD_SRC_MARK;
-                parv[v] = src_v ? (uint16_t)v : (uint16_t)(px[q] & 0xFFFFu);
+                parv[v] = src_v ? (uint16_t)v : (uint16_t)(pr[q] & 0xFFFFu);
                 relv[v] = src_v ? cs : -rr[q];
             }
         }

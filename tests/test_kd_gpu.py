@@ -62,12 +62,16 @@ def kd(monkeypatch):
 @pytest.mark.parametrize("name", ["ba400", "ties", "dir", "c2", "chain"])
 @pytest.mark.parametrize("delta,qcap", [(None, None), (1, None), (7, 64), (100000, None), (None, 64)])
 def test_kd_rows_bitexact(oracle_mod, kd, name, delta, qcap, walk):
-    """walk None: phase C by LDS path walks (level sweep only for deep rows); "0": sweep only."""
+    """walk None: phase C by LDS path walks (level sweep only for deep rows) over packed
+    out-arc records (v | w << 16 | ridx << 24); "0": level sweeps only, unpacked records
+    (the writer wave gathers each winner's parent and reliability index)."""
     from shadow_amd import route
     if walk is None:
         kd.delenv("SHD_ROUTE_KDWALK", raising=False)
+        kd.delenv("SHD_ROUTE_KDPACK", raising=False)
     else:
         kd.setenv("SHD_ROUTE_KDWALK", walk)
+        kd.setenv("SHD_ROUTE_KDPACK", "0")
     if delta is None:
         kd.delenv("SHD_ROUTE_DELTA", raising=False)
     else:

@@ -56,7 +56,7 @@ struct shd_route {
     uint16_t* d_kd_oridx = nullptr; // rtab index per out-arc
     uint32_t* d_kd_lrec = nullptr;  // light in-arc records (2 x u32 per arc)
     double* d_kd_rtab = nullptr;    // distinct reliabilities
-    int kd_nlight = 0, kd_nrtab = 1, kd_walk = 0, kd_packed = 0;
+    int kd_nlight = 0, kd_nrtab = 1, kd_walk = 0, kd_packed = 0, kd_fused = 0;
     char* d_kd_ws = nullptr;
     int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD
     uint64_t device_bytes = 0;
@@ -364,11 +364,12 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 }
             }
             if (lds <= kLdsBudget && maxdeg <= 65535 && rtab_ok) {
-                // out-arc records {v | w << 16, ridx}; light in-CSR records {u | w << 16, ridx}
-                // (light = w < delta; directed graphs: every in-arc, fused parents are off)
+                // out-arc records v | w << 16 (| ridx << 24 when packed); light in-CSR records
+                // {u | w << 16, ridx}, light = w < delta.  Fused parents (found during the
+                // expansion, 32-bit tie keys) need an undirected graph and packed records
+                // (w < 256, <= 256 reliabilities); otherwise the in-CSR holds every in-arc and
+                // phase B finds every parent.
                 std::vector<uint32_t> orec(c->nnz);
-                // packed records (w < 256, <= 256 reliabilities): v | w << 16 | ridx << 24, so the
-                // fused parent's reliability index comes with the arc the expansion loaded
                 int maxw = 0;
                 for (int a = 0; a < c->nnz; a++) maxw = std::max(maxw, (int)w[a]);
                 bool packed = maxw < 256 && rtab.size() <= 256;
@@ -376,12 +377,14 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 for (int a = 0; a < c->nnz; a++)
                     orec[a] = (uint32_t)col[a] | ((uint32_t)w[a] << 16) | (packed ? (uint32_t)ridx_out[a] << 24 : 0u);
                 c->kd_packed = packed ? 1 : 0;
+                const bool fused = !c->directed && packed;
+                c->kd_fused = fused ? 1 : 0;
                 std::vector<int> lrow(n + 1, 0);
                 std::vector<uint32_t> lrec;
                 for (int v = 0; v < n; v++) {
                     for (int q = irow[v]; q < irow[v + 1]; q++) {
                         const int a = order[q];
-                        if (!c->directed && (int)w[a] >= delta) continue;
+                        if (fused && (int)w[a] >= delta) continue;
                         lrec.push_back((uint32_t)cin[q] | ((uint32_t)w[a] << 16));
                         lrec.push_back(ridx_out[a]);
                     }
@@ -677,7 +680,7 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
     if (c->sel == 4 && !(dispatch && c->prefer_direct)) {
         DevDelta k;
         k.n = c->n; k.nw = (c->n + 63) / 64; k.bound = c->k32_bound; k.delta = c->kd_delta;
-        k.fused = c->directed ? 0 : 1; k.rc = c->kd_qcap;
+        k.fused = c->kd_fused; k.rc = c->kd_qcap;
         k.row = c->d_row; k.orec = c->d_kd_orec; k.oridx = c->d_kd_oridx;
         k.nnz = c->nnz; k.lrow = c->d_kd_lstart; k.lrec = reinterpret_cast<const uint2*>(c->d_kd_lrec); k.nlight = c->kd_nlight;
         k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab; k.walk = c->kd_walk; k.packed = c->kd_packed;

@@ -71,7 +71,7 @@ struct DevDelta {
     int nnz;                            // out-arcs
     int bound;
     int delta;                          // bucket width; arcs with w >= delta are heavy
-    int fused;                          // undirected: parents found during expansion
+    int fused;                          // undirected + packed records: parents found during expansion
     int rc;                             // LDS work-queue capacity per bucket round (vertices)
     const int* __restrict__ row;        // out-CSR offsets (n+1)
     const uint32_t* __restrict__ orec;  // out-arcs v | w << 16, rows sorted by (v, eid)
@@ -139,7 +139,7 @@ struct KDLayout {
         // and the reliability table
         L.rix = o;
         L.wmark = o; o += (size_t)(B / 64) * 64 * KD_P;
-        L.wkey = o;  o += (size_t)(B / 64) * 64 * 8;
+        L.wkey = o;  o += (size_t)(B / 64) * 64 * 4;
         L.wimp = o;  o += (size_t)(B / 64) * KD_IMP * 4;
         L.pend = o;  o += a16(8 * nw);
         L.fix = o;   o += a16(8 * nw);
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
     const KDLayout<B> L = KDLayout<B>::make(n, g.rc, RR);
     KDSmall* sm = reinterpret_cast<KDSmall*>(smem);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    unsigned long long* wkey = reinterpret_cast<unsigned long long*>(smem + L.wkey) + wid * 64;
+    uint32_t* wkey = reinterpret_cast<uint32_t*>(smem + L.wkey) + wid * 64;
     uint32_t* wimp = reinterpret_cast<uint32_t*>(smem + L.wimp) + wid * KD_IMP;
     uint16_t* dist = reinterpret_cast<uint16_t*>(smem + L.dist);
     unsigned char* wmark = reinterpret_cast<unsigned char*>(smem + L.wmark) + wid * 64 * KD_P;
@@ -501,7 +501,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     const int total = __builtin_amdgcn_readlane(incl, 63);
                     const int excl = incl - deg;
                     const int boff = beg - excl;
-                    if (g.fused) wkey[lane] = ~0ull;
+                    if (g.fused) wkey[lane] = ~0u;
                     // rows of the slice's active lanes all non-empty (always, undirected): the
                     // owner of arc position q is then (#rows starting at or before q) - 1, a
                     // running row count plus one mbcnt per step
@@ -596,12 +596,10 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                             }
                             nimp += __popcll(im);
                             // tie rule: largest w, then smallest (parent, eid) = smallest v (simple
-                            // graph, rows sorted by (v, eid)); the low word is the record the
-                            // writer stores: parent | ridx << 16 (packed) or the arc index
-                            if (g.fused && valid && dv + w == odu) {
-                                const uint32_t lo = g.packed ? ((W.rx[p] & 0xFFFFu) | ((W.rx[p] >> 8) & 0xFF0000u)) : (uint32_t)(W.obv[p] + lb + 64 * p);
-                                atomicMin(&wkey[W.odo[p] >> 16], ((unsigned long long)(((0xFFFFu - w) << 16) | v) << 32) | lo);
-                            }
+                            // graph, rows sorted by (v, eid)).  Packed records: the key
+                            // (255 - w) << 24 | v << 8 | ridx is one byte permutation of ~rec / rec
+                            if (g.fused && valid && dv + w == odu)
+                                atomicMin(&wkey[W.odo[p] >> 16], __builtin_amdgcn_perm(~W.rx[p], W.rx[p], 0x06010003u));
                         };
                         // the list holds KD_IMP >= 3 x 64 entries: a flush check every second step
                         static_assert(KD_IMP >= 192, "two steps between flush checks");
@@ -650,8 +648,9 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     const bool hasrec = act && u != s;
                     uint32_t prec = KD_NONE;
                     if (g.fused && hasrec) {
-                        const unsigned long long kk = wkey[lane];
-                        if (kk != ~0ull && (0xFFFFu - (unsigned)(kk >> 48)) >= delta) prec = (uint32_t)kk;  // heavy winner
+                        const uint32_t kk = wkey[lane];
+                        if (kk != ~0u && (0xFFu - (kk >> 24)) >= delta)  // heavy winner: parent | ridx << 16
+                            prec = ((kk >> 8) & 0xFFFFu) | ((kk & 0xFFu) << 16);
                     }
                     const unsigned long long rm = __ballot(hasrec);
                     const int nr = __popcll(rm);
@@ -683,9 +682,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                 for (;;) {
                     const int rt = __hip_atomic_load(&sm->rtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if (rt > rd) {
-                        // up to 4 x 64 records per pass: the winners' parent and reliability
-                        // index are gathered here (the writer has the latency to spare), so
-                        // wpr holds parent | ridx << 16 and phase C decodes without gathers
+                        // up to 4 x 64 records per pass
                         const int k = min(4 * 64, rt - rd);
                         int uu[4];
                         uint32_t xx[4];
@@ -711,22 +708,9 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                                 }
                             }
                         }
-                        if (g.packed) {  // the record already is parent | ridx << 16
 #pragma unroll
-                            for (int q = 0; q < 4; q++)
-                                if (uu[q] >= 0) wpr[uu[q]] = xx[q];
-                        } else {  // arc index: gather the parent and its reliability index
-                            uint32_t pv[4], pi[4];
-#pragma unroll
-                            for (int q = 0; q < 4; q++) {
-                                const uint32_t a = uu[q] >= 0 ? xx[q] : 0u;
-                                pv[q] = g.orec[a];
-                                pi[q] = g.oridx[a];
-                            }
-#pragma unroll
-                            for (int q = 0; q < 4; q++)
-                                if (uu[q] >= 0) wpr[uu[q]] = (pv[q] & 0xFFFFu) | (pi[q] << 16);
-                        }
+                        for (int q = 0; q < 4; q++)  // records are parent | ridx << 16
+                            if (uu[q] >= 0) wpr[uu[q]] = xx[q];
                         rd += k;
                         __builtin_amdgcn_wave_barrier();
                         if (lane == 0) __hip_atomic_store(&sm->rdone, rd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

@@ -94,12 +94,14 @@ struct DevDelta {
 // parts, 12-15 phase C (sweeps, compute, store drain, barriers), 16-19 phase B parts
 // accumulated in LDS (sm->acc) and written out once per source: a global read-modify-
 // write inside the timed regions would drain the wave's vmcnt and distort them
+#define KD_ACCP (sm->acc)
 #define KD_STAMP(slot) do { if (tid == 0) sm->acc[slot] = __builtin_amdgcn_s_memtime(); } while (0)
 #define KD_COUNT(slot, x) do { if (lane == 0 && (x)) atomicAdd(&sm->acc[slot], (unsigned long long)(x)); } while (0)
 #define KD_MARK() do { if (tid == 0) kd_t = __builtin_amdgcn_s_memtime(); } while (0)
 #define KD_ACC(slot) do { if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[slot] += t_ - kd_t; kd_t = t_; } } while (0)
 #define KD_FLUSH() do { lds_barrier(); if (g.dbg) for (int q_ = tid; q_ < 32; q_ += B) g.dbg[(size_t)i * 32 + q_] = sm->acc[q_]; lds_barrier(); if (tid < 32) sm->acc[tid] = 0; lds_barrier(); } while (0)
 #else
+#define KD_ACCP nullptr
 #define KD_STAMP(slot) do { } while (0)
 #define KD_COUNT(slot, x) do { } while (0)
 #define KD_MARK() do { } while (0)
@@ -138,7 +140,7 @@ struct KDLayout {
         // the path walk of phase C reuses it for the parent-arc reliability indices (u8 x n)
         // and the reliability table
         L.rix = o;
-        L.wmark = o; o += (size_t)(B / 64) * 64 * KD_P;
+        L.wmark = o; o += (size_t)(B / 64) * 8 * KD_P;
         L.wkey = o;  o += (size_t)(B / 64) * 64 * 4;
         L.wimp = o;  o += (size_t)(B / 64) * KD_IMP * 4;
         L.pend = o;  o += a16(8 * nw);
@@ -161,7 +163,7 @@ constexpr int KD_MAXD = 32;           // phase C path walk: arcs held in registe
 constexpr int KD_WQ = 4;              // phase C path walk: targets per thread
 constexpr int KD_ONE = 254;           // phase C: rtab slot holding 1.0 (the source's own step)
 constexpr int KD_NAN = 255;           // phase C: rtab slot holding NaN (unreachable vertices)
-constexpr int KD_RR = 1024;  // parent-record ring slots (1024-thread workgroups; smaller ones use 256)
+constexpr int KD_RR = 512;  // parent-record ring slots (1024-thread workgroups; smaller ones use 256)
 template <int B>
 constexpr int kd_rr() { return B >= 1024 ? KD_RR : 256; }
 
@@ -265,7 +267,7 @@ __device__ inline void pop4(unsigned long long* b, int k, int v[4]) {
 // them out.  Called by a whole wave (ballots); `cnt` is wave-uniform.
 __device__ inline void kd_relax_list(const uint32_t* wimp, int cnt, int lane, unsigned long long upto,
                                      uint32_t* dist32, unsigned long long* pend, unsigned* wmin, uint16_t* ring,
-                                     int* tail, int rc, unsigned T) {
+                                     int* tail, int rc, unsigned T, unsigned long long* sm_acc) {
     __builtin_amdgcn_wave_barrier();
     for (int b0 = 0; b0 < cnt; b0 += 64) {
         const bool act = b0 + lane < cnt;
@@ -295,6 +297,9 @@ __device__ inline void kd_relax_list(const uint32_t* wimp, int cnt, int lane, un
             // one copy of the vertex: the queue's (else the pending bitmask)
             if (push && rk < qk) { ring[qb + rk] = (uint16_t)v; atomicAnd(&pend[v >> 6], ~(1ull << (v & 63))); }
             if (push && rk >= qk) { atomicOr(&pend[v >> 6], 1ull << (v & 63)); atomicMin(&wmin[v >> 6], nd); }
+#ifdef SHD_STAMPS
+            if (lane == 0 && ctot > qk) atomicAdd(&sm_acc[14], (unsigned long long)(ctot - qk));
+#endif
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
     uint32_t* wkey = reinterpret_cast<uint32_t*>(smem + L.wkey) + wid * 64;
     uint32_t* wimp = reinterpret_cast<uint32_t*>(smem + L.wimp) + wid * KD_IMP;
     uint16_t* dist = reinterpret_cast<uint16_t*>(smem + L.dist);
-    unsigned char* wmark = reinterpret_cast<unsigned char*>(smem + L.wmark) + wid * 64 * KD_P;
+    uint32_t* wmark = reinterpret_cast<uint32_t*>(smem + L.wmark) + wid * 2 * KD_P;  // 64 x KD_P start bits
     unsigned long long* pend = reinterpret_cast<unsigned long long*>(smem + L.pend);
     unsigned* wmin = reinterpret_cast<unsigned*>(smem + L.wmin);
     unsigned long long* fix = reinterpret_cast<unsigned long long*>(smem + L.fix);
@@ -352,7 +357,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         for (int v = tid; v < (n + 2) / 2; v += B) reinterpret_cast<uint32_t*>(dist)[v] = 0xFFFFFFFFu;
         for (int k = tid; k < nw; k += B) { pend[k] = 0ull; wmin[k] = 0xFFFFFFFFu; fix[k] = 0ull; }
         for (int q = tid; q < RR; q += B) rrec[q] = make_uint2(0u, 0xFFFFFFFFu);  // phases B/C reuse the area
-        for (int q = lane; q < 64 * KD_P; q += 64) wmark[q] = 0;  // phase C reuses it
+        if (lane < 2 * KD_P) wmark[lane] = 0u;  // phase C reuses it
         if (tid == 0) {
             sm->gmin[0] = sm->gmin[1] = 0xFFFFFFFFu;
             sm->rtail = sm->rdone = 0;
@@ -432,7 +437,13 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         b &= b - 1;
                         const int u = (k << 6) + bi;
                         if (pos < rc) ring[pos] = (uint16_t)u;
-                        else { take &= ~(1ull << bi); rest = min(rest, (unsigned)dist[u]); }
+                        else {
+                            take &= ~(1ull << bi);
+                            rest = min(rest, (unsigned)dist[u]);
+#ifdef SHD_STAMPS
+                            atomicAdd(&sm->acc[15], 1ull);
+#endif
+                        }
                         pos++;
                     }
                     pend[k] = bits & ~take;
@@ -491,22 +502,37 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         if (x == 0xFFFFu) raise_err(err, SHD_ROUTE_EDEVICE);
                         u = x == 0xFFFFu ? s : (int)x;
                     }
-                    const unsigned du = act ? ld16(dist, u) : 0u;
+                    const unsigned du0 = act ? ld16(dist, u) : 0u;
                     int beg = 0, deg = 0;
                     {
                         const int r0 = g.row[u], r1 = g.row[u + 1];
                         if (act) { beg = r0; deg = r1 - r0; }
+                    }
+                    // the expansion needs the non-empty rows on lanes 0..R-1 (owner = running
+                    // row count + mbcnt); a slice with an empty row among them (directed graphs)
+                    // is compacted through the wave's list area, which is free at this point
+                    const unsigned long long nonempty = __ballot(deg > 0);
+                    const int crank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(nonempty >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((unsigned)nonempty, 0u));
+                    unsigned du = du0;
+                    const int deg0 = deg;
+                    if ((nonempty & (nonempty + 1ull)) != 0ull) {  // not a prefix of the lanes
+                        if (deg > 0) { wimp[crank] = (uint32_t)beg; wimp[64 + crank] = (uint32_t)deg; wimp[128 + crank] = du0; }
+                        __builtin_amdgcn_wave_barrier();
+                        const int R = __popcll(nonempty);
+                        beg = lane < R ? (int)wimp[lane] : 0;
+                        deg = lane < R ? (int)wimp[64 + lane] : 0;
+                        du = lane < R ? wimp[128 + lane] : 0u;
+                        __builtin_amdgcn_wave_barrier();
                     }
                     int incl = kd_wave_incl_sum(deg);
                     const int total = __builtin_amdgcn_readlane(incl, 63);
                     const int excl = incl - deg;
                     const int boff = beg - excl;
                     if (g.fused) wkey[lane] = ~0u;
-                    // rows of the slice's active lanes all non-empty (always, undirected): the
-                    // owner of arc position q is then (#rows starting at or before q) - 1, a
-                    // running row count plus one mbcnt per step
-                    const bool dense = __ballot(act && deg == 0) == 0ull;
-                    int rows_before = 0;  // rows starting before the current step (dense slices)
+                    // owner of arc position q = (#rows starting at or before q) - 1: a running
+                    // row count plus one mbcnt per step
+                    int rows_before = 0;  // rows starting before the current step
 #ifdef SHD_STAMPS
                     if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[22] += t_ - ks0; ks0 = t_; }
 #endif
@@ -531,35 +557,26 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     auto issue = [&](Win& W, const int b0) __attribute__((always_inline)) {
                         const bool live = b0 < total;
                         if (live) {
+                            // start bits of the window's rows (u64 per step), one atomic OR per
+                            // row start; lane p < KD_P reads step p's word, readlane hands it out
                             const int pos = excl - b0;
                             const bool mark = deg > 0 && pos >= 0 && pos < 64 * KD_P;
-                            const int mslot = ((pos & 63) << 3) | (pos >> 6);
-                            if (mark) wmark[mslot] = (unsigned char)(lane + 1);
+                            if (mark) atomicOr(&wmark[pos >> 5], 1u << (pos & 31));
                             __builtin_amdgcn_wave_barrier();
-                            const unsigned long long fl8 = *reinterpret_cast<const unsigned long long*>(wmark + lane * 8);
+                            const unsigned long long mw = reinterpret_cast<const unsigned long long*>(wmark)[lane & (KD_P - 1)];
                             int oo[KD_P];
-                            if (dense) {
 #pragma unroll
-                                for (int p = 0; p < KD_P; p++) {
-                                    const unsigned long long st = __ballot(((fl8 >> (8 * p)) & 0xFFu) != 0);
-                                    const unsigned long long sh = st >> 1;
-                                    oo[p] = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(sh >> 32),
-                                                __builtin_amdgcn_mbcnt_lo((unsigned)sh, (unsigned)(rows_before + (int)(st & 1ull) - 1)));
-                                    rows_before += __popcll(st);
-                                }
-                            } else {
-#pragma unroll
-                                for (int p = 0; p < KD_P; p++) {
-                                    const int base = b0 + 64 * p;
-                                    const unsigned long long cov = __ballot(deg > 0 && excl <= base);
-                                    const int carry = cov ? 63 - __clzll((long long)cov) : 0;
-                                    int f = (int)((fl8 >> (8 * p)) & 0xFFu);
-                                    if (lane == 0 && f == 0) f = carry + 1;
-                                    oo[p] = kd_wave_incl_max(f) - 1;
-                                }
+                            for (int p = 0; p < KD_P; p++) {
+                                const unsigned long long st =
+                                    ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(mw >> 32), p) << 32) |
+                                    (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mw, p);
+                                const unsigned long long sh = st >> 1;
+                                oo[p] = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(sh >> 32),
+                                            __builtin_amdgcn_mbcnt_lo((unsigned)sh, (unsigned)(rows_before + (int)(st & 1ull) - 1)));
+                                rows_before += __popcll(st);
                             }
                             kd_bpermute16(oo, boff, dul, W.obv, W.odo);
-                            if (mark) wmark[mslot] = 0;
+                            if (lane < KD_P) reinterpret_cast<unsigned long long*>(wmark)[lane] = 0ull;
                         } else {
 #pragma unroll
                             for (int p = 0; p < KD_P; p++) { W.obv[p] = 0; W.odo[p] = 0u; }
@@ -605,7 +622,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         static_assert(KD_IMP >= 192, "two steps between flush checks");
                         auto flush = [&]() __attribute__((always_inline)) {
                             kd_relax_list(wimp, nimp, lane, upto, reinterpret_cast<uint32_t*>(dist), pend, wmin, ring,
-                                          &sm->tail, rc, T);
+                                          &sm->tail, rc, T, KD_ACCP);
                             nimp = 0;
                         };
                         if (b0 + 64 * KD_P <= total) {
@@ -636,7 +653,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         process(wb, b0);
                         b0 += 64 * KD_P;
                     }
-                    if (nimp) kd_relax_list(wimp, nimp, lane, upto, reinterpret_cast<uint32_t*>(dist), pend, wmin, ring, &sm->tail, rc, T);
+                    if (nimp) kd_relax_list(wimp, nimp, lane, upto, reinterpret_cast<uint32_t*>(dist), pend, wmin, ring, &sm->tail, rc, T, KD_ACCP);
 #ifdef SHD_STAMPS
                     if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[23] += t_ - ks0; ks0 = t_; sm->acc[25] += (total + 64 * KD_P - 1) / (64 * KD_P); }
 #endif
@@ -648,7 +665,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     const bool hasrec = act && u != s;
                     uint32_t prec = KD_NONE;
                     if (g.fused && hasrec) {
-                        const uint32_t kk = wkey[lane];
+                        const uint32_t kk = deg0 > 0 ? wkey[crank] : ~0u;
                         if (kk != ~0u && (0xFFu - (kk >> 24)) >= delta)  // heavy winner: parent | ridx << 16
                             prec = ((kk >> 8) & 0xFFFFu) | ((kk & 0xFFu) << 16);
                     }
@@ -666,7 +683,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         if (hasrec) {  // one 64-bit LDS write: the writer never sees half a record
                             const int slot = (rb + __popcll(rm & (upto >> 1))) & (RR - 1);
                             *reinterpret_cast<volatile unsigned long long*>(&rrec[slot]) =
-                                (unsigned long long)prec | ((unsigned long long)((uint32_t)u | (du << 16)) << 32);
+                                (unsigned long long)prec | ((unsigned long long)((uint32_t)u | (du0 << 16)) << 32);
                         }
                     }
                     if (lane == 0) atomicSub(&sm->busy, 1);

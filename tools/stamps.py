@@ -68,7 +68,7 @@ if eng.info["kernel"] == 4:
     print(f"  wave0 slices {ns0:.0f}: setup {d[:, 22].mean() / ns0:.0f}  groups {d[:, 23].mean() / ns0:.0f} ({d[:, 25].mean() / ns0:.2f} groups/slice)  records {d[:, 24].mean() / ns0:.0f} cyc/slice")
     ng = max(d[:, 25].mean(), 1)
     print(f"  wave0 per group: owners {d[:, 30].mean() / ng:.0f}  owners+loads {d[:, 27].mean() / ng:.0f}  process {d[:, 28].mean() / ng:.0f} (relax {d[:, 29].mean() / ng:.0f}) cyc")
-    print(f"  gather: pending bits scanned/source {d[:, 14].mean():.0f}  taken {d[:, 15].mean():.0f}")
+    print(f"  queue overflow/source: pushes to pending {d[:, 14].mean():.0f}  gathered past capacity {d[:, 15].mean():.0f}")
     for k, nm in [(11, "minreduce"), (8, "gather"), (9, "prep"), (10, "expand"), (16, "B.short"), (17, "B.long"),
                   (18, "lat row+drain"), (19, "par copy"), (13, "C.compute")]:
         print(f"  A.{nm:10s} mean {d[:, k].mean():10.0f} cyc  ({d[:, k].mean() / max(d[:, 5].mean(), 1):.0f}/sweep)")

@@ -89,7 +89,7 @@ typedef struct shd_route_info {
     int32_t kernel;          /* SSSP kernel: 0 = generic f64, 1 = integer K32 (LDS keys) */
     int32_t dist_bound;      /* K32: proven bound on every shortest-path latency (ms) */
     int32_t block;           /* threads per workgroup of the SSSP kernel */
-    int32_t reserved;
+    int32_t reserved;        /* KD: bucket width delta; KB: 1 when path attributes are fused */
 } shd_route_info_t;
 
 int shd_route_create(shd_route_t** out, const shd_graph_t* graph, int device);

@@ -1,5 +1,7 @@
 // engine.hip -- host side of the routing engine (C-ABI in include/shd_route.h).
 #include "common.hpp"
+
+#include <map>
 #include "sssp_f64.hpp"
 #include "sssp_k32.hpp"
 #include "sssp_batch.hpp"
@@ -41,6 +43,10 @@ struct shd_route {
     uint32_t* d_kb_arc = nullptr;
     KBSeg* d_kb_seg = nullptr;
     KBHub* d_kb_hub = nullptr;
+    int kb_fused = 0, kbf_nrtab = 0, kb_grid_cap = 0;  // sssp_batch_kernel<true>: rows in one kernel
+    size_t kbf_lds = 0;
+    uint32_t* d_kbf_arc = nullptr;    // in-arcs u << 16 | ridx << 8 | w
+    double* d_kbf_rtab = nullptr;     // distinct reliabilities
     uint32_t* d_keys = nullptr;     // key rows scratch (ns x n u32), grown on demand
     size_t keys_cap = 0;
     // K16 large-graph kernel (sssp_k16.hpp)
@@ -438,11 +444,49 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
         if (kbl <= kLdsBudget) {
             rc = upload(c, &c->d_kb_seg, segs);
             if (!rc && !hubs.empty()) rc = upload(c, &c->d_kb_hub, hubs);
-            if (!rc) rc = hip_check(hipFuncSetAttribute((const void*)sssp_batch_kernel,
+            if (!rc) rc = hip_check(hipFuncSetAttribute((const void*)sssp_batch_kernel<false>,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kbl));
             if (rc) return rc;
             c->kb = 1; c->kb_lds = kbl; c->kb_nseg = (int)segs.size(); c->kb_nhub = (int)hubs.size();
             c->kb_npart = npart;
+            // fused rows (no key rows, no K2): records u << 16 | ridx << 8 | w need w < 256 and
+            // <= 254 distinct reliabilities; parent records of <= KB_RIT segments per thread
+            int maxw = 0;
+            for (int a = 0; a < c->nnz; a++) maxw = std::max(maxw, (int)w[a]);
+            std::map<uint64_t, int> rix;
+            for (int q = 0; q < c->nnz; q++) {
+                uint64_t bits;
+                std::memcpy(&bits, &rin[q], 8);
+                rix.emplace(bits, 0);
+            }
+            const KBLayout FL = KBLayout::make(n, c->nnz, npart, true);
+            const size_t fbl = kKBSmall + FL.total;
+            bool fuse = maxw < 256 && rix.size() <= (size_t)KB_ONE && (int)segs.size() <= KB_RIT * KB_BLOCK &&
+                        (int)hubs.size() <= KB_BLOCK && fbl <= kLdsBudget;
+            if (const char* e = getenv("SHD_ROUTE_KBFUSE")) fuse = fuse && atoi(e) != 0;
+            if (fuse) {
+                std::vector<double> rtab;
+                for (auto& kv : rix) {
+                    kv.second = (int)rtab.size();
+                    double x;
+                    std::memcpy(&x, &kv.first, 8);
+                    rtab.push_back(x);
+                }
+                std::vector<uint32_t> farc(((size_t)c->nnz + 3) / 4 * 4, 0u);
+                for (int q = 0; q < c->nnz; q++) {
+                    uint64_t bits;
+                    std::memcpy(&bits, &rin[q], 8);
+                    farc[q] = ((uint32_t)cin[q] << 16) | ((uint32_t)rix[bits] << 8) | (uint32_t)w[order[q]];
+                }
+                rc = upload(c, &c->d_kbf_arc, farc);
+                if (!rc) rc = upload(c, &c->d_kbf_rtab, rtab);
+                if (!rc) rc = hip_check(hipFuncSetAttribute((const void*)sssp_batch_kernel<true>,
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)fbl));
+                if (rc) return rc;
+                c->kb_fused = 1; c->kbf_lds = fbl; c->kbf_nrtab = (int)rtab.size();
+            }
+            // tests cap the grid so that every workgroup runs several batches in turn
+            if (const char* e = getenv("SHD_ROUTE_KBGRID")) c->kb_grid_cap = std::max(1, atoi(e));
         }
     }
     c->sel = c->kb ? 2 : c->kd ? 4 : c->k32 ? 1 : c->k16 ? 3 : 0;  // K32 still beats KD on C3-class graphs
@@ -626,7 +670,7 @@ int shd_route_get_info(const shd_route_t* c, shd_route_info_t* info) {
     info->dist_bound = c->k32_bound;
     info->block = c->sel == 2 ? KB_BLOCK : c->sel == 3 ? K16_BLOCK : c->sel == 4 ? c->kd_block
                 : c->sel == 1 ? c->k32_block : kBlock;
-    info->reserved = c->sel == 4 ? c->kd_delta : 0;
+    info->reserved = c->sel == 4 ? c->kd_delta : c->sel == 2 ? c->kb_fused : 0;
     info->device_bytes = c->device_bytes;
     info->min_edge_latency = c->min_w;
     return SHD_ROUTE_OK;
@@ -649,6 +693,22 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
     }
     const int dispatch = (flags & SHD_ROUTE_DISPATCH) ? 1 : 0;
     if (c->sel == 2 && !(dispatch && c->prefer_direct)) {
+        DevKB kb;
+        kb.n = c->n; kb.nnz = c->nnz; kb.nseg = c->kb_nseg; kb.nhub = c->kb_nhub; kb.npart = c->kb_npart;
+        kb.bound = c->k32_bound; kb.arc = c->d_kb_arc; kb.row_in = c->d_k32_row_in; kb.seg = c->d_kb_seg;
+        kb.hub = c->d_kb_hub;
+        kb.rtab = c->d_kbf_rtab; kb.nrtab = c->kbf_nrtab;
+        kb.vf = c->d_vf; kb.self_w = c->d_self_w; kb.self_r = c->d_self_r;
+        int gridb = std::min((ns + KB_SRC - 1) / KB_SRC, 1 << 20);
+        if (c->kb_grid_cap > 0) gridb = std::min(gridb, c->kb_grid_cap);
+        if (c->kb_fused) {
+            // KB with fused path attributes: the rows in one kernel
+            kb.arc = c->d_kbf_arc;
+            kb.dbg = c->d_dbg ? c->d_dbg + (size_t)ns * 8 : nullptr;
+            hipLaunchKernelGGL(sssp_batch_kernel<true>, dim3(gridb), dim3(KB_BLOCK), c->kbf_lds, st, kb, d_src, ns,
+                               nullptr, 0LL, c->d_err, d_tgt, nt, (long long)ld, d_lat, d_rel, d_row_min);
+            return hip_check(hipGetLastError());
+        }
         // KB distances+parents for KB_SRC sources per workgroup -> key rows -> K2
         const size_t need = (size_t)ns * c->n;
         if (need > c->keys_cap) {
@@ -658,14 +718,9 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
             if (hipMalloc((void**)&c->d_keys, need * sizeof(uint32_t)) != hipSuccess) return SHD_ROUTE_ENOMEM;
             c->keys_cap = need;
         }
-        DevKB kb;
-        kb.n = c->n; kb.nnz = c->nnz; kb.nseg = c->kb_nseg; kb.nhub = c->kb_nhub; kb.npart = c->kb_npart;
-        kb.bound = c->k32_bound; kb.arc = c->d_kb_arc; kb.row_in = c->d_k32_row_in; kb.seg = c->d_kb_seg;
-        kb.hub = c->d_kb_hub;
         kb.dbg = c->d_dbg ? c->d_dbg + (size_t)ns * 8 : nullptr;
-        const int gridb = std::min((ns + KB_SRC - 1) / KB_SRC, 1 << 20);
-        hipLaunchKernelGGL(sssp_batch_kernel, dim3(gridb), dim3(KB_BLOCK), c->kb_lds, st, kb, d_src, ns, c->d_keys,
-                           (long long)c->n, c->d_err);
+        hipLaunchKernelGGL(sssp_batch_kernel<false>, dim3(gridb), dim3(KB_BLOCK), c->kb_lds, st, kb, d_src, ns,
+                           c->d_keys, (long long)c->n, c->d_err, d_tgt, nt, (long long)ld, d_lat, d_rel, d_row_min);
         int rc = hip_check(hipGetLastError());
         if (rc) return rc;
         DevAttr at;

@@ -24,6 +24,11 @@ namespace shd {
 constexpr int KB_SRC = 8;     // sources per workgroup (u16 x 8 = 16 bytes per vertex)
 constexpr int KB_SEG = 16;    // max arcs per segment
 constexpr int KB_BLOCK = 1024;
+constexpr int KB_RIT = 3;     // fused: segments per thread whose parent records stay in registers
+constexpr int KB_WQ = 4;      // fused: targets per lane walked together
+constexpr int KB_MAXD = 32;   // fused: arcs a walk collects in registers (deeper: slow path)
+constexpr int KB_ONE = 254;   // fused: rtab slot holding 1.0 (the source's own step)
+constexpr int KB_NAN = 255;   // fused: rtab slot holding NaN (unreachable vertices)
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
@@ -44,6 +49,12 @@ struct DevKB {
     const KBSeg* __restrict__ seg;
     const KBHub* __restrict__ hub;
     unsigned long long* dbg;   // SHD_STAMPS builds: 8 words per workgroup
+    // fused path attributes (sssp_batch_kernel<true>): arc = u << 16 | ridx << 8 | w
+    const double* __restrict__ rtab;    // distinct 1 - loss values (<= 254), indexed by ridx
+    int nrtab;
+    const double* __restrict__ vf;
+    const double* __restrict__ self_w;
+    const double* __restrict__ self_r;
 };
 #ifdef SHD_STAMPS
 #define KB_STAMP(slot) do { if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + (slot)] += __builtin_amdgcn_s_memtime(); } while (0)
@@ -53,19 +64,27 @@ struct DevKB {
 #define KB_COUNT(slot) do { } while (0)
 #endif
 
+// fused: once the parents are known the arc region is dead and holds the walk arrays
+// par u16[KB_SRC][n] and rix u8[KB_SRC][n]; the reliability table follows P.
 struct KBLayout {
-    size_t arc, D, P, total;
-    __host__ __device__ static KBLayout make(int n, int nnz, int npart) {
+    size_t arc, par, rix, D, P, rt, total;
+    __host__ __device__ static KBLayout make(int n, int nnz, int npart, bool fused = false) {
         KBLayout L;
         size_t o = 0;
-        L.arc = o; o += a16(sizeof(uint32_t) * (size_t)nnz);
+        L.arc = o;
+        L.par = o;
+        L.rix = o + a16((size_t)2 * KB_SRC * n);
+        size_t arcb = a16(sizeof(uint32_t) * (size_t)nnz);
+        if (fused) arcb = arcb > L.rix + a16((size_t)KB_SRC * n) ? arcb : L.rix + a16((size_t)KB_SRC * n);
+        o += arcb;
         L.D = o;   o += a16((size_t)16 * n);
         L.P = o;   o += a16((size_t)16 * npart);
+        L.rt = o;  o += fused ? (size_t)8 * 256 : 0;
         L.total = o;
         return L;
     }
 };
-constexpr size_t kKBSmall = 16;
+constexpr size_t kKBSmall = 80;  // changed flag + fused row minima (u64 x 8)
 
 struct u16x8 { us2 h[4]; };
 
@@ -107,13 +126,17 @@ __device__ inline u16x8 addsat8(const u16x8& a, us2 w) {
     return r;
 }
 
+// arc weight as a u16 pair: low 16 bits (u << 16 | w), or the low byte of the fused
+// record (u << 16 | ridx << 8 | w)
+template <bool kFused>
 __device__ inline us2 wsplat(uint32_t rec) {
-    const unsigned short w = (unsigned short)(rec & 0xFFFFu);
+    const unsigned short w = (unsigned short)(rec & (kFused ? 0xFFu : 0xFFFFu));
     const us2 r = {w, w};
     return r;
 }
 
 // min over arcs [a0, a1) of D[u] + w, four independent arc/distance reads in flight.
+template <bool kFused>
 __device__ inline u16x8 relax_row(const uint32_t* arc, const char* D, int a0, int a1) {
     u16x8 acc = inf8();
     int a = a0;
@@ -123,22 +146,69 @@ __device__ inline u16x8 relax_row(const uint32_t* arc, const char* D, int a0, in
         const u16x8 d1 = ld8(D + (size_t)16 * (r1 >> 16));
         const u16x8 d2 = ld8(D + (size_t)16 * (r2 >> 16));
         const u16x8 d3 = ld8(D + (size_t)16 * (r3 >> 16));
-        acc = min8(min8(acc, addsat8(d0, wsplat(r0))), addsat8(d1, wsplat(r1)));
-        acc = min8(min8(acc, addsat8(d2, wsplat(r2))), addsat8(d3, wsplat(r3)));
+        acc = min8(min8(acc, addsat8(d0, wsplat<kFused>(r0))), addsat8(d1, wsplat<kFused>(r1)));
+        acc = min8(min8(acc, addsat8(d2, wsplat<kFused>(r2))), addsat8(d3, wsplat<kFused>(r3)));
     }
     for (; a < a1; a++) {
         const uint32_t r0 = arc[a];
-        acc = min8(acc, addsat8(ld8(D + (size_t)16 * (r0 >> 16)), wsplat(r0)));
+        acc = min8(acc, addsat8(ld8(D + (size_t)16 * (r0 >> 16)), wsplat<kFused>(r0)));
     }
     return acc;
 }
 
+// first tight arc of in-arcs [a0, a1) for each of the batch's sources: slot (a - r0) or
+// 0xFFFF when none (or when the vertex is unreached for that source)
+template <bool kFused>
+__device__ inline void first_tight(const uint32_t* arc, const char* D, int a0, int a1, int r0,
+                                   const u16x8& dv, unsigned short (&slot)[KB_SRC]) {
+#pragma unroll
+    for (int b = 0; b < KB_SRC; b++) slot[b] = 0xFFFFu;
+    for (int a = a0; a < a1; a += 4) {
+        u16x8 c[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t rec = arc[min(a + q, a1 - 1)];
+            c[q] = addsat8(ld8(D + (size_t)16 * (rec >> 16)), wsplat<kFused>(rec));
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (a + q >= a1) break;
+#pragma unroll
+            for (int b = 0; b < KB_SRC; b++) {
+                const unsigned short cb = c[q].h[b >> 1][b & 1], db = dv.h[b >> 1][b & 1];
+                if (slot[b] == 0xFFFFu && db != 0xFFFFu && cb == db) slot[b] = (unsigned short)(a + q - r0);
+            }
+        }
+    }
+}
+
+// fused walk record of (v, source b): parent | rix << 16
+__device__ inline uint32_t kb_record(const uint32_t* arc, int v, int s, unsigned short db, int r0,
+                                     unsigned short slot) {
+    if (v == s) return (uint32_t)v | ((uint32_t)KB_ONE << 16);
+    if (db == 0xFFFFu || slot == 0xFFFFu) return (uint32_t)(s < 0 ? v : s) | ((uint32_t)KB_NAN << 16);
+    const uint32_t rec = arc[r0 + slot];
+    return (rec >> 16) | (((rec >> 8) & 0xFFu) << 16);
+}
+
+// kFused = false: distances + parents -> key rows (dist16 << 16 | slot16) for K2.
+// kFused = true : the whole row in one kernel.  Parent records stay in registers until the
+// arcs are dead, then become par u16 / rix u8 arrays in the arc region; two waves per
+// source write the lat row from D and the rel row by walking each target's tree path in
+// LDS and folding the factors source-first -- the multiplication order of K2's level
+// sweep (relv[v] = relv[parent] * r), so the bits agree.  Row minima as K2.
+template <bool kFused>
 __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int* __restrict__ src, int ns,
                                                               uint32_t* __restrict__ keys, long long kld,
-                                                              int* __restrict__ err) {
+                                                              int* __restrict__ err,
+                                                              const int* __restrict__ tgt, int nt, long long ld,
+                                                              double* __restrict__ lat_out,
+                                                              double* __restrict__ rel_out,
+                                                              double* __restrict__ row_min) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int* changed = reinterpret_cast<int*>(smem);
-    const KBLayout L = KBLayout::make(g.n, g.nnz, g.npart);
+    unsigned long long* rmin = reinterpret_cast<unsigned long long*>(smem + 16);
+    const KBLayout L = KBLayout::make(g.n, g.nnz, g.npart, kFused);
     char* base = smem + kKBSmall;
     uint32_t* arc = reinterpret_cast<uint32_t*>(base + L.arc);
     char* D = base + L.D;
@@ -147,15 +217,21 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
     const int n = g.n;
 
     if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memtime();
-    // stage the in-CSR into LDS once per workgroup (16-byte loads)
-    {
+    double* rtl = reinterpret_cast<double*>(base + L.rt);
+    if constexpr (kFused) {
+        for (int k = tid; k < 256; k += KB_BLOCK)
+            rtl[k] = k < g.nrtab ? g.rtab[k] : k == KB_ONE ? 1.0 : NAN;
+    }
+    auto stage = [&]() {  // the in-CSR into LDS (16-byte loads)
         const int nq = (g.nnz + 3) / 4;
         const uint4* s4 = reinterpret_cast<const uint4*>(g.arc);
         uint4* d4 = reinterpret_cast<uint4*>(arc);
         for (int q = tid; q < nq; q += KB_BLOCK) d4[q] = s4[q];
-    }
+    };
+    if constexpr (!kFused) stage();
 
     for (int i0 = blockIdx.x * KB_SRC; i0 < ns; i0 += gridDim.x * KB_SRC) {
+        if constexpr (kFused) stage();  // the previous batch's walk arrays overwrote it
         int sb[KB_SRC];
 #pragma unroll
         for (int b = 0; b < KB_SRC; b++) {
@@ -175,6 +251,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
                 if (sb[b] == v) d.h[b >> 1][b & 1] = 0;
             st8(D + (size_t)16 * v, d);
         }
+        if (kFused && tid < KB_SRC) rmin[tid] = kInfBits;
         __syncthreads();
 
         if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memtime();
@@ -186,7 +263,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
             int ch = 0;
             for (int k = tid; k < g.nseg; k += KB_BLOCK) {
                 const KBSeg sg = g.seg[k];
-                const u16x8 acc = relax_row(arc, D, sg.a0, sg.a1);
+                const u16x8 acc = relax_row<kFused>(arc, D, sg.a0, sg.a1);
                 if (sg.p < 0) {
                     const u16x8 old = ld8(D + (size_t)16 * sg.v);
                     const u16x8 nw = min8(old, acc);
@@ -211,31 +288,14 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
         }
 
         if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memtime();
+        if constexpr (!kFused) {
         // ---- parents: first tight arc of each in-row, per source -----------------
         for (int k = tid; k < g.nseg; k += KB_BLOCK) {
             const KBSeg sg = g.seg[k];
             const u16x8 dv = ld8(D + (size_t)16 * sg.v);
-            unsigned short slot[KB_SRC];
-#pragma unroll
-            for (int b = 0; b < KB_SRC; b++) slot[b] = 0xFFFFu;
             const int r0 = g.row_in[sg.v];
-            for (int a = sg.a0; a < sg.a1; a += 4) {
-                u16x8 c[4];
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const uint32_t rec = arc[min(a + q, sg.a1 - 1)];
-                    c[q] = addsat8(ld8(D + (size_t)16 * (rec >> 16)), wsplat(rec));
-                }
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if (a + q >= sg.a1) break;
-#pragma unroll
-                    for (int b = 0; b < KB_SRC; b++) {
-                        const unsigned short cb = c[q].h[b >> 1][b & 1], db = dv.h[b >> 1][b & 1];
-                        if (slot[b] == 0xFFFFu && db != 0xFFFFu && cb == db) slot[b] = (unsigned short)(a + q - r0);
-                    }
-                }
-            }
+            unsigned short slot[KB_SRC];
+            first_tight<false>(arc, D, sg.a0, sg.a1, r0, dv, slot);
             if (sg.p < 0) {
 #pragma unroll
                 for (int b = 0; b < KB_SRC; b++) {
@@ -272,6 +332,182 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
             }
         }
         __syncthreads();
+        } else {
+        // ---- parents -> walk records, held in registers while the arcs are live ----
+        // (host guarantees nseg <= KB_RIT * KB_BLOCK and nhub <= KB_BLOCK)
+        uint32_t prec[KB_RIT][KB_SRC];
+        int pv[KB_RIT];
+#pragma unroll
+        for (int it = 0; it < KB_RIT; it++) {
+            const int k = tid + it * KB_BLOCK;
+            pv[it] = -1;
+            if (k >= g.nseg) continue;
+            const KBSeg sg = g.seg[k];
+            const u16x8 dv = ld8(D + (size_t)16 * sg.v);
+            const int r0 = g.row_in[sg.v];
+            unsigned short slot[KB_SRC];
+            first_tight<true>(arc, D, sg.a0, sg.a1, r0, dv, slot);
+            if (sg.p < 0) {
+                pv[it] = sg.v;
+#pragma unroll
+                for (int b = 0; b < KB_SRC; b++)
+                    prec[it][b] = kb_record(arc, sg.v, sb[b], dv.h[b >> 1][b & 1], r0, slot[b]);
+            } else {
+                u16x8 ps;
+#pragma unroll
+                for (int b = 0; b < KB_SRC; b++) ps.h[b >> 1][b & 1] = slot[b];
+                st8(P + (size_t)16 * sg.p, ps);  // earlier segments hold lower slots
+            }
+        }
+        __syncthreads();
+        uint32_t hrec[KB_SRC];
+        int hv = -1;
+        if (tid < g.nhub) {
+            const KBHub h = g.hub[tid];
+            hv = h.v;
+            const u16x8 dv = ld8(D + (size_t)16 * h.v);
+            const int r0 = g.row_in[h.v];
+            u16x8 acc = inf8();
+            for (int p = h.p0; p < h.p1; p++) acc = min8(acc, ld8(P + (size_t)16 * p));
+#pragma unroll
+            for (int b = 0; b < KB_SRC; b++)
+                hrec[b] = kb_record(arc, h.v, sb[b], dv.h[b >> 1][b & 1], r0, acc.h[b >> 1][b & 1]);
+        }
+        __syncthreads();  // every arc read done: the region becomes par / rix
+        uint16_t* par = reinterpret_cast<uint16_t*>(base + L.par);
+        uint8_t* rix = reinterpret_cast<uint8_t*>(base + L.rix);
+#pragma unroll
+        for (int it = 0; it < KB_RIT; it++) {
+            if (pv[it] < 0) continue;
+#pragma unroll
+            for (int b = 0; b < KB_SRC; b++) {
+                par[b * n + pv[it]] = (uint16_t)(prec[it][b] & 0xFFFFu);
+                rix[b * n + pv[it]] = (uint8_t)(prec[it][b] >> 16);
+            }
+        }
+        if (hv >= 0) {
+#pragma unroll
+            for (int b = 0; b < KB_SRC; b++) {
+                par[b * n + hv] = (uint16_t)(hrec[b] & 0xFFFFu);
+                rix[b * n + hv] = (uint8_t)(hrec[b] >> 16);
+            }
+        }
+        __syncthreads();
+        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memtime();
+
+        // ---- rows: KB_BLOCK / 64 / KB_SRC waves per source ----------------------
+        constexpr int WPS = KB_BLOCK / 64 / KB_SRC;
+        const int wv = tid >> 6, lane = tid & 63;
+        const int b = wv % KB_SRC;
+        const int i = i0 + b;
+        int s = -1;
+        if (i < ns) {
+            s = src[i];
+            if (s < 0 || s >= n) s = -1;
+        }
+        if (s >= 0) {
+            const double fs = g.vf[s];
+            const double cs = isnan(fs) ? 1.0 : 1.0 * fs;
+            const uint16_t* pb = par + b * n;
+            const uint8_t* xb = rix + b * n;
+            double* lrow = lat_out ? lat_out + (long long)i * ld : nullptr;
+            double* rrow = rel_out ? rel_out + (long long)i * ld : nullptr;
+            double lmin = INFINITY;
+            constexpr int STEP = WPS * 64;
+            for (int j0 = (wv / KB_SRC) * 64 + lane; j0 - lane < nt; j0 += STEP * KB_WQ) {
+                int tq[KB_WQ], cur[KB_WQ];
+                uint32_t pk[KB_WQ][KB_MAXD / 4];
+#pragma unroll
+                for (int q = 0; q < KB_WQ; q++) {
+                    const int j = j0 + q * STEP;
+                    tq[q] = j < nt ? tgt[j] : -1;
+                    cur[q] = tq[q] >= 0 && tq[q] < n ? tq[q] : s;
+#pragma unroll
+                    for (int k = 0; k < KB_MAXD / 4; k++) pk[q][k] = 0u;
+                }
+                // walk: a chain that reaches the source stays there (par[s] = s, factor 1.0)
+                int kmax = 0;  // wave-uniform
+#pragma unroll
+                for (int k = 0; k < KB_MAXD; k++) {
+                    bool any = false;
+#pragma unroll
+                    for (int q = 0; q < KB_WQ; q++) any = any || cur[q] != s;
+                    if (!__any(any)) break;
+                    kmax = k + 1;
+                    uint32_t p[KB_WQ], rx[KB_WQ];
+#pragma unroll
+                    for (int q = 0; q < KB_WQ; q++) { p[q] = pb[cur[q]]; rx[q] = xb[cur[q]]; }
+#pragma unroll
+                    for (int q = 0; q < KB_WQ; q++) {
+                        pk[q][k >> 2] |= rx[q] << ((k & 3) * 8);
+                        cur[q] = (int)p[q];
+                    }
+                }
+                double rr[KB_WQ];
+#pragma unroll
+                for (int q = 0; q < KB_WQ; q++) rr[q] = cs;
+#pragma unroll
+                for (int k = KB_MAXD - 1; k >= 0; k--) {
+                    if (k >= kmax) continue;
+                    double x[KB_WQ];
+#pragma unroll
+                    for (int q = 0; q < KB_WQ; q++) x[q] = rtl[(pk[q][k >> 2] >> ((k & 3) * 8)) & 0xFFu];
+#pragma unroll
+                    for (int q = 0; q < KB_WQ; q++) rr[q] *= x[q];
+                }
+#pragma unroll
+                for (int q = 0; q < KB_WQ; q++) {
+                    if (cur[q] == s) continue;
+                    // deeper than KB_MAXD arcs (rare): fold depth by depth, re-walking from t
+                    const int t = tq[q];
+                    int depth = 0;
+                    for (int c = t; c != s && depth <= n; c = pb[c]) depth++;
+                    double r = cs;
+                    for (int d = 1; d <= depth && d <= n; d++) {
+                        int c = t;
+                        for (int k = 0; k < depth - d; k++) c = pb[c];
+                        r *= rtl[xb[c]];
+                    }
+                    rr[q] = r;
+                }
+                double ft[KB_WQ];
+#pragma unroll
+                for (int q = 0; q < KB_WQ; q++) ft[q] = g.vf[tq[q] >= 0 && tq[q] < n ? tq[q] : s];
+#pragma unroll
+                for (int q = 0; q < KB_WQ; q++) {
+                    const int j = j0 + q * STEP;
+                    if (j >= nt) continue;
+                    const int t = tq[q];
+                    double Lv, Rv;
+                    if (t < 0 || t >= n) {
+                        raise_err(err, SHD_ROUTE_EINVAL);
+                        Lv = Rv = NAN;
+                    } else if (t == s) {  // batch path [s]: one self-loop hop (topology.c:1471-1499)
+                        const double w = g.self_w[s];
+                        if (isnan(w)) { raise_err(err, SHD_ROUTE_ENOEDGE); Lv = Rv = NAN; }
+                        else { Lv = 0.0 + w; Rv = cs * g.self_r[s]; }
+                    } else {
+                        const unsigned short dt = *reinterpret_cast<const unsigned short*>(D + (size_t)16 * t + 2 * b);
+                        if (dt == 0xFFFFu) {
+                            raise_err(err, SHD_ROUTE_EUNREACH);
+                            Lv = Rv = NAN;
+                        } else {
+                            Lv = (double)dt;
+                            Rv = isnan(ft[q]) ? rr[q] : rr[q] * ft[q];
+                        }
+                    }
+                    if (lrow) __builtin_nontemporal_store(Lv, lrow + j);
+                    if (rrow) __builtin_nontemporal_store(Rv, rrow + j);
+                    lmin = fmin(lmin, Lv);
+                }
+            }
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) lmin = fmin(lmin, __shfl_xor(lmin, d, 64));
+            if (lane == 0 && lmin < INFINITY) atomicMin(&rmin[b], as_u(lmin));
+        }
+        __syncthreads();
+        if (tid < KB_SRC && i0 + tid < ns && row_min) row_min[i0 + tid] = as_d(rmin[tid]);
+        }  // kFused
         if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memtime();
     }
 }

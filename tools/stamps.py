@@ -42,10 +42,18 @@ for rep in range(3):
 d_all = dbg.cpu().numpy().astype(np.int64).reshape(-1, 32 if eng.info["kernel"] == 4 else 8)
 d = d_all[: len(S)]
 if eng.info["kernel"] == 2:
-    kb = d_all[len(S):]
-    print(f"config {a.config} n={g.n} nnz={g.nnz} sources={len(S)} kernel=KB+K2")
-    print(f"  KB stage   mean {np.mean(kb[:,1]-kb[:,0]):10.0f} cyc")
+    flat = dbg.cpu().numpy().astype(np.int64)
+    kb = flat[len(S) * 8: len(S) * 8 + nwg * 8].reshape(nwg, 8)
+    fused = eng.info["reserved"] == 1
+    print(f"config {a.config} n={g.n} nnz={g.nnz} sources={len(S)} kernel=KB{' fused' if fused else '+K2'}")
+    print(f"  KB stage+init mean {np.mean(kb[:,1]-kb[:,0]):10.0f} cyc")
     print(f"  KB sweeps  mean {np.mean(kb[:,2]-kb[:,1]):10.0f} cyc  max {np.max(kb[:,2]-kb[:,1])}  rounds mean {kb[:,4].mean():.1f} max {kb[:,4].max():.0f}")
+    if fused:
+        print(f"  KB parents mean {np.mean(kb[:,5]-kb[:,2]):10.0f} cyc")
+        print(f"  KB rows    mean {np.mean(kb[:,3]-kb[:,5]):10.0f} cyc  max {np.max(kb[:,3]-kb[:,5])}")
+        t0 = kb[:, 0] - kb[:, 0].min()
+        print(f"  total      mean {np.mean(kb[:,3]-kb[:,0]):10.0f} cyc  start spread max {t0.max()}  end max {(kb[:,3]-kb[:,0].min()).max()}")
+        sys.exit(0)
     print(f"  KB parents mean {np.mean(kb[:,3]-kb[:,2]):10.0f} cyc")
     print(f"  K2 phaseB  mean {np.mean(d[:,1]-d[:,0]):10.0f} cyc")
     print(f"  K2 sweeps  mean {np.mean(d[:,2]-d[:,1]):10.0f} cyc  sweeps mean {d[:,5].mean():.1f}")

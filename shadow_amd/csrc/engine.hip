@@ -43,7 +43,7 @@ struct shd_route {
     uint32_t* d_kb_arc = nullptr;
     KBSeg* d_kb_seg = nullptr;
     KBHub* d_kb_hub = nullptr;
-    int kb_fused = 0, kbf_nrtab = 0, kb_grid_cap = 0;  // sssp_batch_kernel<true>: rows in one kernel
+    int kb_fused = 0, kbf_nrtab = 0, kb_grid_cap = 0, kbf_tcap = 0;  // sssp_batch_kernel<true>: rows in one kernel
     size_t kbf_lds = 0;
     uint32_t* d_kbf_arc = nullptr;    // in-arcs u << 16 | ridx << 8 | w
     double* d_kbf_rtab = nullptr;     // distinct reliabilities
@@ -444,7 +444,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
         if (kbl <= kLdsBudget) {
             rc = upload(c, &c->d_kb_seg, segs);
             if (!rc && !hubs.empty()) rc = upload(c, &c->d_kb_hub, hubs);
-            if (!rc) rc = hip_check(hipFuncSetAttribute((const void*)sssp_batch_kernel<false>,
+            if (!rc) rc = hip_check(hipFuncSetAttribute((const void*)sssp_batch_kernel,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kbl));
             if (rc) return rc;
             c->kb = 1; c->kb_lds = kbl; c->kb_nseg = (int)segs.size(); c->kb_nhub = (int)hubs.size();
@@ -459,10 +459,15 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 std::memcpy(&bits, &rin[q], 8);
                 rix.emplace(bits, 0);
             }
-            const KBLayout FL = KBLayout::make(n, c->nnz, npart, true);
-            const size_t fbl = kKBSmall + FL.total;
+            // staged targets: as many as the rest of the LDS holds (one chunk when nt <= n)
+            const size_t fb0 = kKBSmall + KBLayout::make(n, c->nnz, npart, true, 0).total;
+            int tcap = fb0 < kLdsBudget ? (int)std::min<size_t>((size_t)n, (kLdsBudget - fb0 - 64) / 4) : 0;
+            tcap = tcap >= 64 ? (tcap & ~63) : 0;
+            const size_t fbl = kKBSmall + KBLayout::make(n, c->nnz, npart, true, tcap).total;
             bool fuse = maxw < 256 && rix.size() <= (size_t)KB_ONE && (int)segs.size() <= KB_RIT * KB_BLOCK &&
-                        (int)hubs.size() <= KB_BLOCK && fbl <= kLdsBudget;
+                        (int)hubs.size() <= KB_BLOCK && c->nnz < 0xFFFF && KB_SRC * n <= KB_CV * KB_BLOCK && npart < 0xFFFF && tcap >= 64 &&
+                        fbl <= kLdsBudget;
+            if (const char* e = getenv("SHD_ROUTE_KBTCAP")) tcap = std::max(64, std::min(tcap, atoi(e)) & ~63);
             if (const char* e = getenv("SHD_ROUTE_KBFUSE")) fuse = fuse && atoi(e) != 0;
             if (fuse) {
                 std::vector<double> rtab;
@@ -480,10 +485,10 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 }
                 rc = upload(c, &c->d_kbf_arc, farc);
                 if (!rc) rc = upload(c, &c->d_kbf_rtab, rtab);
-                if (!rc) rc = hip_check(hipFuncSetAttribute((const void*)sssp_batch_kernel<true>,
+                if (!rc) rc = hip_check(hipFuncSetAttribute((const void*)sssp_batch_rows_kernel,
                                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)fbl));
                 if (rc) return rc;
-                c->kb_fused = 1; c->kbf_lds = fbl; c->kbf_nrtab = (int)rtab.size();
+                c->kb_fused = 1; c->kbf_lds = fbl; c->kbf_nrtab = (int)rtab.size(); c->kbf_tcap = tcap;
             }
             // tests cap the grid so that every workgroup runs several batches in turn
             if (const char* e = getenv("SHD_ROUTE_KBGRID")) c->kb_grid_cap = std::max(1, atoi(e));
@@ -705,8 +710,9 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
             // KB with fused path attributes: the rows in one kernel
             kb.arc = c->d_kbf_arc;
             kb.dbg = c->d_dbg ? c->d_dbg + (size_t)ns * 8 : nullptr;
-            hipLaunchKernelGGL(sssp_batch_kernel<true>, dim3(gridb), dim3(KB_BLOCK), c->kbf_lds, st, kb, d_src, ns,
-                               nullptr, 0LL, c->d_err, d_tgt, nt, (long long)ld, d_lat, d_rel, d_row_min);
+            kb.tcap = c->kbf_tcap;
+            hipLaunchKernelGGL(sssp_batch_rows_kernel, dim3(gridb), dim3(KB_BLOCK), c->kbf_lds, st, kb, d_src, ns,
+                               c->d_err, d_tgt, nt, (long long)ld, d_lat, d_rel, d_row_min);
             return hip_check(hipGetLastError());
         }
         // KB distances+parents for KB_SRC sources per workgroup -> key rows -> K2
@@ -719,8 +725,8 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
             c->keys_cap = need;
         }
         kb.dbg = c->d_dbg ? c->d_dbg + (size_t)ns * 8 : nullptr;
-        hipLaunchKernelGGL(sssp_batch_kernel<false>, dim3(gridb), dim3(KB_BLOCK), c->kb_lds, st, kb, d_src, ns,
-                           c->d_keys, (long long)c->n, c->d_err, d_tgt, nt, (long long)ld, d_lat, d_rel, d_row_min);
+        hipLaunchKernelGGL(sssp_batch_kernel, dim3(gridb), dim3(KB_BLOCK), c->kb_lds, st, kb, d_src, ns,
+                           c->d_keys, (long long)c->n, c->d_err);
         int rc = hip_check(hipGetLastError());
         if (rc) return rc;
         DevAttr at;

@@ -24,9 +24,10 @@ namespace shd {
 constexpr int KB_SRC = 8;     // sources per workgroup (u16 x 8 = 16 bytes per vertex)
 constexpr int KB_SEG = 16;    // max arcs per segment
 constexpr int KB_BLOCK = 1024;
-constexpr int KB_RIT = 3;     // fused: segments per thread whose parent records stay in registers
+constexpr int KB_RIT = 3;     // fused: segments per thread, held in registers
+constexpr int KB_CV = 16;     // fused: walk records per thread (KB_SRC * n <= KB_CV * KB_BLOCK)
 constexpr int KB_WQ = 4;      // fused: targets per lane walked together
-constexpr int KB_MAXD = 32;   // fused: arcs a walk collects in registers (deeper: slow path)
+constexpr int KB_MAXD = 32;   // fused: arcs a walk collects in registers (deeper: chunked refolds)
 constexpr int KB_ONE = 254;   // fused: rtab slot holding 1.0 (the source's own step)
 constexpr int KB_NAN = 255;   // fused: rtab slot holding NaN (unreachable vertices)
 
@@ -55,6 +56,7 @@ struct DevKB {
     const double* __restrict__ vf;
     const double* __restrict__ self_w;
     const double* __restrict__ self_r;
+    int tcap;                           // staged targets per chunk
 };
 #ifdef SHD_STAMPS
 #define KB_STAMP(slot) do { if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + (slot)] += __builtin_amdgcn_s_memtime(); } while (0)
@@ -64,22 +66,23 @@ struct DevKB {
 #define KB_COUNT(slot) do { } while (0)
 #endif
 
-// fused: once the parents are known the arc region is dead and holds the walk arrays
-// par u16[KB_SRC][n] and rix u8[KB_SRC][n]; the reliability table follows P.
+// fused: parent slots sl u16[KB_SRC][n] (absolute index of each vertex's first tight
+// in-arc, 0xFFFF at the source and at unreached vertices), the reliability table, and the
+// staged target list tg i32[tcap]; once the parents are known sl holds the parent
+// vertices and the arc region the parent arcs' reliability indices rix u8[KB_SRC][n].
 struct KBLayout {
-    size_t arc, par, rix, D, P, rt, total;
-    __host__ __device__ static KBLayout make(int n, int nnz, int npart, bool fused = false) {
+    size_t arc, D, P, sl, rt, tg, total;
+    __host__ __device__ static KBLayout make(int n, int nnz, int npart, bool fused = false, int tcap = 0) {
         KBLayout L;
         size_t o = 0;
-        L.arc = o;
-        L.par = o;
-        L.rix = o + a16((size_t)2 * KB_SRC * n);
         size_t arcb = a16(sizeof(uint32_t) * (size_t)nnz);
-        if (fused) arcb = arcb > L.rix + a16((size_t)KB_SRC * n) ? arcb : L.rix + a16((size_t)KB_SRC * n);
-        o += arcb;
+        if (fused && arcb < a16((size_t)KB_SRC * n)) arcb = a16((size_t)KB_SRC * n);  // rix
+        L.arc = o; o += arcb;
         L.D = o;   o += a16((size_t)16 * n);
         L.P = o;   o += a16((size_t)16 * npart);
+        L.sl = o;  o += fused ? a16((size_t)2 * KB_SRC * n) : 0;
         L.rt = o;  o += fused ? (size_t)8 * 256 : 0;
+        L.tg = o;  o += fused ? a16((size_t)4 * tcap) : 0;
         L.total = o;
         return L;
     }
@@ -182,33 +185,13 @@ __device__ inline void first_tight(const uint32_t* arc, const char* D, int a0, i
     }
 }
 
-// fused walk record of (v, source b): parent | rix << 16
-__device__ inline uint32_t kb_record(const uint32_t* arc, int v, int s, unsigned short db, int r0,
-                                     unsigned short slot) {
-    if (v == s) return (uint32_t)v | ((uint32_t)KB_ONE << 16);
-    if (db == 0xFFFFu || slot == 0xFFFFu) return (uint32_t)(s < 0 ? v : s) | ((uint32_t)KB_NAN << 16);
-    const uint32_t rec = arc[r0 + slot];
-    return (rec >> 16) | (((rec >> 8) & 0xFFu) << 16);
-}
-
-// kFused = false: distances + parents -> key rows (dist16 << 16 | slot16) for K2.
-// kFused = true : the whole row in one kernel.  Parent records stay in registers until the
-// arcs are dead, then become par u16 / rix u8 arrays in the arc region; two waves per
-// source write the lat row from D and the rel row by walking each target's tree path in
-// LDS and folding the factors source-first -- the multiplication order of K2's level
-// sweep (relv[v] = relv[parent] * r), so the bits agree.  Row minima as K2.
-template <bool kFused>
+// Distances + parents -> key rows (dist16 << 16 | slot16) for K2 (path_attr.hpp).
 __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int* __restrict__ src, int ns,
                                                               uint32_t* __restrict__ keys, long long kld,
-                                                              int* __restrict__ err,
-                                                              const int* __restrict__ tgt, int nt, long long ld,
-                                                              double* __restrict__ lat_out,
-                                                              double* __restrict__ rel_out,
-                                                              double* __restrict__ row_min) {
+                                                              int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int* changed = reinterpret_cast<int*>(smem);
-    unsigned long long* rmin = reinterpret_cast<unsigned long long*>(smem + 16);
-    const KBLayout L = KBLayout::make(g.n, g.nnz, g.npart, kFused);
+    const KBLayout L = KBLayout::make(g.n, g.nnz, g.npart);
     char* base = smem + kKBSmall;
     uint32_t* arc = reinterpret_cast<uint32_t*>(base + L.arc);
     char* D = base + L.D;
@@ -217,21 +200,15 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
     const int n = g.n;
 
     if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memtime();
-    double* rtl = reinterpret_cast<double*>(base + L.rt);
-    if constexpr (kFused) {
-        for (int k = tid; k < 256; k += KB_BLOCK)
-            rtl[k] = k < g.nrtab ? g.rtab[k] : k == KB_ONE ? 1.0 : NAN;
-    }
-    auto stage = [&]() {  // the in-CSR into LDS (16-byte loads)
+    // stage the in-CSR into LDS once per workgroup (16-byte loads)
+    {
         const int nq = (g.nnz + 3) / 4;
         const uint4* s4 = reinterpret_cast<const uint4*>(g.arc);
         uint4* d4 = reinterpret_cast<uint4*>(arc);
         for (int q = tid; q < nq; q += KB_BLOCK) d4[q] = s4[q];
-    };
-    if constexpr (!kFused) stage();
+    }
 
     for (int i0 = blockIdx.x * KB_SRC; i0 < ns; i0 += gridDim.x * KB_SRC) {
-        if constexpr (kFused) stage();  // the previous batch's walk arrays overwrote it
         int sb[KB_SRC];
 #pragma unroll
         for (int b = 0; b < KB_SRC; b++) {
@@ -251,7 +228,6 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
                 if (sb[b] == v) d.h[b >> 1][b & 1] = 0;
             st8(D + (size_t)16 * v, d);
         }
-        if (kFused && tid < KB_SRC) rmin[tid] = kInfBits;
         __syncthreads();
 
         if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memtime();
@@ -263,7 +239,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
             int ch = 0;
             for (int k = tid; k < g.nseg; k += KB_BLOCK) {
                 const KBSeg sg = g.seg[k];
-                const u16x8 acc = relax_row<kFused>(arc, D, sg.a0, sg.a1);
+                const u16x8 acc = relax_row<false>(arc, D, sg.a0, sg.a1);
                 if (sg.p < 0) {
                     const u16x8 old = ld8(D + (size_t)16 * sg.v);
                     const u16x8 nw = min8(old, acc);
@@ -288,7 +264,6 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
         }
 
         if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memtime();
-        if constexpr (!kFused) {
         // ---- parents: first tight arc of each in-row, per source -----------------
         for (int k = tid; k < g.nseg; k += KB_BLOCK) {
             const KBSeg sg = g.seg[k];
@@ -332,71 +307,195 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
             }
         }
         __syncthreads();
-        } else {
-        // ---- parents -> walk records, held in registers while the arcs are live ----
-        // (host guarantees nseg <= KB_RIT * KB_BLOCK and nhub <= KB_BLOCK)
-        uint32_t prec[KB_RIT][KB_SRC];
-        int pv[KB_RIT];
+        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memtime();
+    }
+}
+
+
+// KB with fused path attributes: the whole SOURCE rows of KB_SRC sources in one kernel
+// (no key rows, no K2).
+//  - each thread's <= KB_RIT segments and <= 1 hub stay in registers for the whole launch
+//    (packed, no per-sweep descriptor loads)
+//  - the parent pass stores, per (source, vertex), the absolute index of the first tight
+//    in-arc (nnz < 2^16 whenever the arcs fit the LDS), so no in-row offsets are read
+//  - the target list is staged in LDS once, before the sweeps, when it fits (else chunked)
+//  - slots become parent vertices (in place) and reliability indices (over the dead arc
+//    region); two waves per source write the lat row from D and the rel row by walking
+//    each target's tree path in LDS and folding the factors source-first: the
+//    multiplication order of K2's level sweep
+//    (relv[v] = relv[parent] * r), so the bits agree.  Row minima as K2.
+__global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, const int* __restrict__ src, int ns,
+                                                                   int* __restrict__ err,
+                                                                   const int* __restrict__ tgt, int nt, long long ld,
+                                                                   double* __restrict__ lat_out,
+                                                                   double* __restrict__ rel_out,
+                                                                   double* __restrict__ row_min) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int* changed = reinterpret_cast<int*>(smem);
+    unsigned long long* rmin = reinterpret_cast<unsigned long long*>(smem + 16);
+    const KBLayout L = KBLayout::make(g.n, g.nnz, g.npart, true, g.tcap);
+    char* base = smem + kKBSmall;
+    uint32_t* arc = reinterpret_cast<uint32_t*>(base + L.arc);
+    char* D = base + L.D;
+    char* P = base + L.P;
+    uint16_t* sl = reinterpret_cast<uint16_t*>(base + L.sl);
+    double* rtl = reinterpret_cast<double*>(base + L.rt);
+    int* tg = reinterpret_cast<int*>(base + L.tg);
+    const int tid = threadIdx.x;
+    const int n = g.n;
+    const int tcap = g.tcap;
+
+    if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memtime();
+    for (int k = tid; k < 256; k += KB_BLOCK)
+        rtl[k] = k < g.nrtab ? g.rtab[k] : k == KB_ONE ? 1.0 : NAN;
+    const bool one_chunk = nt <= tcap;
+    if (one_chunk)
+        for (int j = tid; j < nt; j += KB_BLOCK) tg[j] = tgt[j];
+    for (int i0 = blockIdx.x * KB_SRC; i0 < ns; i0 += gridDim.x * KB_SRC) {
+        {   // the in-CSR into LDS (16-byte loads); the previous batch's walk records overwrote it
+            const int nq = (g.nnz + 3) / 4;
+            const uint4* s4 = reinterpret_cast<const uint4*>(g.arc);
+            uint4* d4 = reinterpret_cast<uint4*>(arc);
+            for (int q = tid; q < nq; q += KB_BLOCK) d4[q] = s4[q];
+        }
+        // this thread's segments (reloaded per batch: nothing lives across the walk)
+        // (a0 | len << 16, v | p << 16; p = 0xFFFF: whole row) and hub
+        // (host guarantees nseg <= KB_RIT * KB_BLOCK, nhub <= KB_BLOCK, n and npart < 2^16)
+        uint32_t sa[KB_RIT], sv[KB_RIT];
 #pragma unroll
         for (int it = 0; it < KB_RIT; it++) {
             const int k = tid + it * KB_BLOCK;
-            pv[it] = -1;
-            if (k >= g.nseg) continue;
-            const KBSeg sg = g.seg[k];
-            const u16x8 dv = ld8(D + (size_t)16 * sg.v);
-            const int r0 = g.row_in[sg.v];
-            unsigned short slot[KB_SRC];
-            first_tight<true>(arc, D, sg.a0, sg.a1, r0, dv, slot);
-            if (sg.p < 0) {
-                pv[it] = sg.v;
+            sa[it] = 0u; sv[it] = 0xFFFFFFFFu;
+            if (k < g.nseg) {
+                const KBSeg sg = g.seg[k];
+                sa[it] = (uint32_t)sg.a0 | ((uint32_t)(sg.a1 - sg.a0) << 16);
+                sv[it] = (uint32_t)sg.v | ((uint32_t)(sg.p < 0 ? 0xFFFF : sg.p) << 16);
+            }
+        }
+        int hv = -1;
+        uint32_t hp = 0u;
+        if (tid < g.nhub) {
+            const KBHub h = g.hub[tid];
+            hv = h.v;
+            hp = (uint32_t)h.p0 | ((uint32_t)h.p1 << 16);
+        }
+        int sb[KB_SRC];
 #pragma unroll
-                for (int b = 0; b < KB_SRC; b++)
-                    prec[it][b] = kb_record(arc, sg.v, sb[b], dv.h[b >> 1][b & 1], r0, slot[b]);
+        for (int b = 0; b < KB_SRC; b++) {
+            const int i = i0 + b;
+            int s = -1;
+            if (i < ns) {
+                s = src[i];
+                if (s < 0 || s >= n) { if (tid == 0) raise_err(err, SHD_ROUTE_EINVAL); s = -1; }
+            }
+            sb[b] = s;
+        }
+        for (int v = tid; v < n; v += KB_BLOCK) {
+            u16x8 d = inf8();
+#pragma unroll
+            for (int b = 0; b < KB_SRC; b++)
+                if (sb[b] == v) d.h[b >> 1][b & 1] = 0;
+            st8(D + (size_t)16 * v, d);
+        }
+        if (tid < KB_SRC) rmin[tid] = kInfBits;
+        __syncthreads();
+
+        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memtime();
+        // ---- Gauss-Seidel pull sweeps to the fixed point -------------------------
+        for (;;) {
+            KB_COUNT(4);
+            if (tid == 0) *changed = 0;
+            __syncthreads();
+            int ch = 0;
+#pragma unroll
+            for (int it = 0; it < KB_RIT; it++) {
+                if (sv[it] == 0xFFFFFFFFu) continue;
+                const int a0 = (int)(sa[it] & 0xFFFFu), a1 = a0 + (int)(sa[it] >> 16);
+                const int v = (int)(sv[it] & 0xFFFFu), p = (int)(sv[it] >> 16);
+                const u16x8 acc = relax_row<true>(arc, D, a0, a1);
+                if (p == 0xFFFF) {
+                    const u16x8 old = ld8(D + (size_t)16 * v);
+                    const u16x8 nw = min8(old, acc);
+                    if (!eq8(nw, old)) { st8(D + (size_t)16 * v, nw); ch = 1; }
+                } else {
+                    st8(P + (size_t)16 * p, acc);
+                }
+            }
+            __syncthreads();
+            if (hv >= 0) {
+                u16x8 acc = ld8(D + (size_t)16 * hv);
+                const u16x8 old = acc;
+                for (int p = (int)(hp & 0xFFFFu); p < (int)(hp >> 16); p++) acc = min8(acc, ld8(P + (size_t)16 * p));
+                if (!eq8(acc, old)) { st8(D + (size_t)16 * hv, acc); ch = 1; }
+            }
+            if (ch) *changed = 1;
+            __syncthreads();
+            const int again = *changed;
+            __syncthreads();
+            if (!again) break;
+        }
+
+        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memtime();
+        // ---- parents: absolute index of the first tight in-arc, per source --------
+#pragma unroll
+        for (int it = 0; it < KB_RIT; it++) {
+            if (sv[it] == 0xFFFFFFFFu) continue;
+            const int a0 = (int)(sa[it] & 0xFFFFu), a1 = a0 + (int)(sa[it] >> 16);
+            const int v = (int)(sv[it] & 0xFFFFu), p = (int)(sv[it] >> 16);
+            const u16x8 dv = ld8(D + (size_t)16 * v);
+            unsigned short slot[KB_SRC];
+            first_tight<true>(arc, D, a0, a1, 0, dv, slot);  // 0xFFFF at the source / unreached
+            if (p == 0xFFFF) {
+#pragma unroll
+                for (int b = 0; b < KB_SRC; b++) sl[b * n + v] = slot[b];
             } else {
                 u16x8 ps;
 #pragma unroll
                 for (int b = 0; b < KB_SRC; b++) ps.h[b >> 1][b & 1] = slot[b];
-                st8(P + (size_t)16 * sg.p, ps);  // earlier segments hold lower slots
+                st8(P + (size_t)16 * p, ps);  // earlier segments hold lower arc indices
             }
         }
         __syncthreads();
-        uint32_t hrec[KB_SRC];
-        int hv = -1;
-        if (tid < g.nhub) {
-            const KBHub h = g.hub[tid];
-            hv = h.v;
-            const u16x8 dv = ld8(D + (size_t)16 * h.v);
-            const int r0 = g.row_in[h.v];
-            u16x8 acc = inf8();
-            for (int p = h.p0; p < h.p1; p++) acc = min8(acc, ld8(P + (size_t)16 * p));
-#pragma unroll
-            for (int b = 0; b < KB_SRC; b++)
-                hrec[b] = kb_record(arc, h.v, sb[b], dv.h[b >> 1][b & 1], r0, acc.h[b >> 1][b & 1]);
-        }
-        __syncthreads();  // every arc read done: the region becomes par / rix
-        uint16_t* par = reinterpret_cast<uint16_t*>(base + L.par);
-        uint8_t* rix = reinterpret_cast<uint8_t*>(base + L.rix);
-#pragma unroll
-        for (int it = 0; it < KB_RIT; it++) {
-            if (pv[it] < 0) continue;
-#pragma unroll
-            for (int b = 0; b < KB_SRC; b++) {
-                par[b * n + pv[it]] = (uint16_t)(prec[it][b] & 0xFFFFu);
-                rix[b * n + pv[it]] = (uint8_t)(prec[it][b] >> 16);
-            }
-        }
         if (hv >= 0) {
+            u16x8 acc = inf8();
+            for (int p = (int)(hp & 0xFFFFu); p < (int)(hp >> 16); p++) acc = min8(acc, ld8(P + (size_t)16 * p));
 #pragma unroll
-            for (int b = 0; b < KB_SRC; b++) {
-                par[b * n + hv] = (uint16_t)(hrec[b] & 0xFFFFu);
-                rix[b * n + hv] = (uint8_t)(hrec[b] >> 16);
-            }
+            for (int b = 0; b < KB_SRC; b++) sl[b * n + hv] = acc.h[b >> 1][b & 1];
         }
         __syncthreads();
         if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memtime();
 
-        // ---- rows: KB_BLOCK / 64 / KB_SRC waves per source ----------------------
+        // ---- slots -> walk arrays: sl[x] becomes the parent vertex in place, the arc's
+        // reliability index goes to rix u8[KB_SRC][n] over the dead arc region (the source
+        // and unreached vertices point at themselves with factor 1.0)
+        {
+            uint32_t rxp[KB_CV / 4];
+#pragma unroll
+            for (int k = 0; k < KB_CV / 4; k++) rxp[k] = 0u;
+#pragma unroll
+            for (int k = 0; k < KB_CV; k++) {
+                const int x = tid + k * KB_BLOCK;
+                if (x < KB_SRC * n) {
+                    const uint32_t a = sl[x];
+                    const uint32_t rec = arc[a == 0xFFFFu ? 0u : a];
+                    sl[x] = a == 0xFFFFu ? (uint16_t)(x % n) : (uint16_t)(rec >> 16);
+                    rxp[k >> 2] |= (a == 0xFFFFu ? (uint32_t)KB_ONE : (rec >> 8) & 0xFFu) << ((k & 3) * 8);
+                }
+            }
+            __syncthreads();  // every arc read done
+            uint8_t* rixw = reinterpret_cast<uint8_t*>(arc);
+#pragma unroll
+            for (int k = 0; k < KB_CV; k++) {
+                const int x = tid + k * KB_BLOCK;
+                if (x < KB_SRC * n) rixw[x] = (uint8_t)(rxp[k >> 2] >> ((k & 3) * 8));
+            }
+            __syncthreads();
+        }
+        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memtime();
+
+        // ---- rows: WPS waves per source ----------------------------------------------
         constexpr int WPS = KB_BLOCK / 64 / KB_SRC;
+        constexpr int STEP = WPS * 64;
         const int wv = tid >> 6, lane = tid & 63;
         const int b = wv % KB_SRC;
         const int i = i0 + b;
@@ -405,27 +504,38 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
             s = src[i];
             if (s < 0 || s >= n) s = -1;
         }
-        if (s >= 0) {
-            const double fs = g.vf[s];
-            const double cs = isnan(fs) ? 1.0 : 1.0 * fs;
-            const uint16_t* pb = par + b * n;
-            const uint8_t* xb = rix + b * n;
-            double* lrow = lat_out ? lat_out + (long long)i * ld : nullptr;
-            double* rrow = rel_out ? rel_out + (long long)i * ld : nullptr;
-            double lmin = INFINITY;
-            constexpr int STEP = WPS * 64;
-            for (int j0 = (wv / KB_SRC) * 64 + lane; j0 - lane < nt; j0 += STEP * KB_WQ) {
+        const double fs = s >= 0 ? g.vf[s] : NAN;
+        const double cs = isnan(fs) ? 1.0 : 1.0 * fs;
+        const double s_w = s >= 0 ? g.self_w[s] : NAN, s_r = s >= 0 ? g.self_r[s] : NAN;
+        const uint16_t* pb = sl + b * n;
+        const uint8_t* xb = reinterpret_cast<const uint8_t*>(arc) + b * n;
+        double* lrow = (lat_out && s >= 0) ? lat_out + (long long)i * ld : nullptr;
+        double* rrow = (rel_out && s >= 0) ? rel_out + (long long)i * ld : nullptr;
+        double lmin = INFINITY;
+        for (int c0 = 0; c0 < nt; c0 += tcap) {
+            const int cn = min(tcap, nt - c0);
+            if (!one_chunk) {
+                __syncthreads();  // the previous chunk's targets are consumed
+                for (int j = tid; j < cn; j += KB_BLOCK) tg[j] = tgt[c0 + j];
+                __syncthreads();
+            }
+            if (s < 0) continue;
+            for (int j0 = (wv / KB_SRC) * 64 + lane; j0 - lane < cn; j0 += STEP * KB_WQ) {
                 int tq[KB_WQ], cur[KB_WQ];
-                uint32_t pk[KB_WQ][KB_MAXD / 4];
+                double ft[KB_WQ];
+                uint32_t pk[KB_WQ][KB_MAXD / 4];  // rix of the arcs walked, 4 per word
 #pragma unroll
                 for (int q = 0; q < KB_WQ; q++) {
                     const int j = j0 + q * STEP;
-                    tq[q] = j < nt ? tgt[j] : -1;
-                    cur[q] = tq[q] >= 0 && tq[q] < n ? tq[q] : s;
+                    tq[q] = j < cn ? tg[j] : -1;
+                    const bool ok = tq[q] >= 0 && tq[q] < n;
+                    ft[q] = g.vf[ok ? tq[q] : s];  // in flight during the walk
+                    cur[q] = ok && *reinterpret_cast<const unsigned short*>(D + (size_t)16 * tq[q] + 2 * b) != 0xFFFFu
+                                 ? tq[q] : s;
 #pragma unroll
                     for (int k = 0; k < KB_MAXD / 4; k++) pk[q][k] = 0u;
                 }
-                // walk: a chain that reaches the source stays there (par[s] = s, factor 1.0)
+                // walk: a chain that reaches the source stays there (parent s, factor 1.0)
                 int kmax = 0;  // wave-uniform
 #pragma unroll
                 for (int k = 0; k < KB_MAXD; k++) {
@@ -458,34 +568,40 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
 #pragma unroll
                 for (int q = 0; q < KB_WQ; q++) {
                     if (cur[q] == s) continue;
-                    // deeper than KB_MAXD arcs (rare): fold depth by depth, re-walking from t
+                    // deeper than KB_MAXD arcs: depth L, then chunks of KB_MAXD factors from the
+                    // source side, each collected by re-walking from t (O(L^2 / KB_MAXD) steps)
                     const int t = tq[q];
                     int depth = 0;
                     for (int c = t; c != s && depth <= n; c = pb[c]) depth++;
                     double r = cs;
-                    for (int d = 1; d <= depth && d <= n; d++) {
+                    for (int lo = 1; lo <= depth && lo <= n; lo += 16) {
+                        const int hi = min(depth, lo + 15);
                         int c = t;
-                        for (int k = 0; k < depth - d; k++) c = pb[c];
-                        r *= rtl[xb[c]];
+                        for (int k = 0; k < depth - hi; k++) c = pb[c];
+                        unsigned long long f0 = 0ull, f1 = 0ull;  // factors of depths hi .. lo
+                        for (int k = 0; k <= hi - lo; k++) {
+                            const unsigned long long x = xb[c];
+                            if (k < 8) f0 |= x << (8 * k);
+                            else f1 |= x << (8 * (k - 8));
+                            c = pb[c];
+                        }
+                        for (int k = hi - lo; k >= 0; k--)
+                            r *= rtl[(k < 8 ? f0 >> (8 * k) : f1 >> (8 * (k - 8))) & 0xFFu];
                     }
                     rr[q] = r;
                 }
-                double ft[KB_WQ];
-#pragma unroll
-                for (int q = 0; q < KB_WQ; q++) ft[q] = g.vf[tq[q] >= 0 && tq[q] < n ? tq[q] : s];
 #pragma unroll
                 for (int q = 0; q < KB_WQ; q++) {
                     const int j = j0 + q * STEP;
-                    if (j >= nt) continue;
+                    if (j >= cn) continue;
                     const int t = tq[q];
                     double Lv, Rv;
                     if (t < 0 || t >= n) {
                         raise_err(err, SHD_ROUTE_EINVAL);
                         Lv = Rv = NAN;
                     } else if (t == s) {  // batch path [s]: one self-loop hop (topology.c:1471-1499)
-                        const double w = g.self_w[s];
-                        if (isnan(w)) { raise_err(err, SHD_ROUTE_ENOEDGE); Lv = Rv = NAN; }
-                        else { Lv = 0.0 + w; Rv = cs * g.self_r[s]; }
+                        if (isnan(s_w)) { raise_err(err, SHD_ROUTE_ENOEDGE); Lv = Rv = NAN; }
+                        else { Lv = 0.0 + s_w; Rv = cs * s_r; }
                     } else {
                         const unsigned short dt = *reinterpret_cast<const unsigned short*>(D + (size_t)16 * t + 2 * b);
                         if (dt == 0xFFFFu) {
@@ -496,18 +612,19 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
                             Rv = isnan(ft[q]) ? rr[q] : rr[q] * ft[q];
                         }
                     }
-                    if (lrow) __builtin_nontemporal_store(Lv, lrow + j);
-                    if (rrow) __builtin_nontemporal_store(Rv, rrow + j);
+                    if (lrow) __builtin_nontemporal_store(Lv, lrow + c0 + j);
+                    if (rrow) __builtin_nontemporal_store(Rv, rrow + c0 + j);
                     lmin = fmin(lmin, Lv);
                 }
             }
+        }
+        if (s >= 0) {
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) lmin = fmin(lmin, __shfl_xor(lmin, d, 64));
             if (lane == 0 && lmin < INFINITY) atomicMin(&rmin[b], as_u(lmin));
         }
         __syncthreads();
         if (tid < KB_SRC && i0 + tid < ns && row_min) row_min[i0 + tid] = as_d(rmin[tid]);
-        }  // kFused
         if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memtime();
     }
 }

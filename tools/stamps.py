@@ -50,7 +50,8 @@ if eng.info["kernel"] == 2:
     print(f"  KB sweeps  mean {np.mean(kb[:,2]-kb[:,1]):10.0f} cyc  max {np.max(kb[:,2]-kb[:,1])}  rounds mean {kb[:,4].mean():.1f} max {kb[:,4].max():.0f}")
     if fused:
         print(f"  KB parents mean {np.mean(kb[:,5]-kb[:,2]):10.0f} cyc")
-        print(f"  KB rows    mean {np.mean(kb[:,3]-kb[:,5]):10.0f} cyc  max {np.max(kb[:,3]-kb[:,5])}")
+        print(f"  KB convert mean {np.mean(kb[:,6]-kb[:,5]):10.0f} cyc")
+        print(f"  KB rows    mean {np.mean(kb[:,3]-kb[:,6]):10.0f} cyc  max {np.max(kb[:,3]-kb[:,6])}")
         t0 = kb[:, 0] - kb[:, 0].min()
         print(f"  total      mean {np.mean(kb[:,3]-kb[:,0]):10.0f} cyc  start spread max {t0.max()}  end max {(kb[:,3]-kb[:,0].min()).max()}")
         sys.exit(0)

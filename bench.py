@@ -172,12 +172,19 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for t in range(args.steps):
-        step(t)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     eng.sync(sh)  # raises on any device-side error
+    # dominant-kernel duration: HIP events on the launch stream around the rows kernel, in
+    # a second pass of the same K steps (an event pair per step costs ~10 us of stream time
+    # on this stack, so the throughput pass above carries none)
+    for t in range(args.steps):
+        step(t)
+    torch.cuda.synchronize()
+    eng.sync(sh)
     kms = [k_start[t].elapsed_time(k_end[t]) for t in range(args.steps)]
     dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:

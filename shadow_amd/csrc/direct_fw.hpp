@@ -89,6 +89,25 @@ __global__ __launch_bounds__(kBlock) void min_reduce_kernel(const double* __rest
     if ((threadIdx.x & 63) == 0 && m < INFINITY) atomicMin(out, as_u(m));
 }
 
+// K5 for up to kMinOneBlock values: one workgroup reduces and stores the result itself
+// (no clearing memset, no atomics): the same bits as min_reduce_kernel after a 0xFF fill.
+constexpr long long kMinOneBlock = 1 << 20;
+__global__ __launch_bounds__(1024) void min_reduce_block_kernel(const double* __restrict__ vals, long long count,
+                                                                unsigned long long* __restrict__ out) {
+    __shared__ double wm[16];
+    double m = INFINITY;
+    for (long long k = threadIdx.x; k < count; k += 1024) m = fmin(m, vals[k]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) m = fmin(m, __shfl_xor(m, d, 64));
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double r = wm[0];
+        for (int k = 1; k < 16; k++) r = fmin(r, wm[k]);
+        *out = r < INFINITY ? as_u(r) : ~0ull;
+    }
+}
+
 // Blocked min-plus Floyd-Warshall (K4), 32x32 tiles of doubles in LDS.
 constexpr int kT = 32;
 __global__ __launch_bounds__(kT * 8) void fw_diag_kernel(double* d, int n, int k0) {

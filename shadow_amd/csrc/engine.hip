@@ -899,8 +899,12 @@ int shd_route_min_reduce_async(shd_route_t* c, const double* d_vals, int64_t cou
     if (!c || count < 0 || !d_out || (count && !d_vals)) return SHD_ROUTE_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    if (count <= kMinOneBlock) {  // one launch, no clearing memset
+        hipLaunchKernelGGL(min_reduce_block_kernel, dim3(1), dim3(1024), 0, st, d_vals, (long long)count,
+                           (unsigned long long*)d_out);
+        return hip_check(hipGetLastError());
+    }
     if (hipMemsetAsync(d_out, 0xFF, sizeof(double), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
-    if (count == 0) return SHD_ROUTE_OK;
     long long blocks = std::min<long long>((count + kBlock - 1) / kBlock, 2048);
     hipLaunchKernelGGL(min_reduce_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, d_vals, (long long)count,
                        (unsigned long long*)d_out);

@@ -61,7 +61,12 @@ struct DevKB {
 #ifdef SHD_STAMPS
 #define KB_STAMP(slot) do { if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + (slot)] += __builtin_amdgcn_s_memtime(); } while (0)
 #define KB_COUNT(slot) do { if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + (slot)] += 1; } while (0)
+// fused rows phase, wave 0 of each workgroup: cycles of walk / fold / output, trips, steps
+#define KBT_MARK(v) unsigned long long v = 0; if (g.dbg) v = __builtin_amdgcn_s_memtime()
+#define KBT_ACC(slot, val) do { if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 16 + (slot)] += (val); } while (0)
 #else
+#define KBT_MARK(v) do { } while (0)
+#define KBT_ACC(slot, val) do { } while (0)
 #define KB_STAMP(slot) do { } while (0)
 #define KB_COUNT(slot) do { } while (0)
 #endif
@@ -87,7 +92,15 @@ struct KBLayout {
         return L;
     }
 };
-constexpr size_t kKBSmall = 80;  // changed flag + fused row minima (u64 x 8)
+// small: changed flag, fused unit counter | row minima u64[8] | per-source constants of the
+// fused rows phase: source, 1.0 * f_s (or 1.0), self-loop latency and reliability
+struct KBSmall {
+    int changed, units, pad0, pad1;
+    unsigned long long rmin[8];
+    int src[8];
+    double cs[8], sw[8], sr[8];
+};
+constexpr size_t kKBSmall = (sizeof(KBSmall) + 15) & ~size_t(15);
 
 struct u16x8 { us2 h[4]; };
 
@@ -331,8 +344,9 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
                                                                    double* __restrict__ rel_out,
                                                                    double* __restrict__ row_min) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    int* changed = reinterpret_cast<int*>(smem);
-    unsigned long long* rmin = reinterpret_cast<unsigned long long*>(smem + 16);
+    KBSmall* sm = reinterpret_cast<KBSmall*>(smem);
+    int* changed = &sm->changed;
+    unsigned long long* rmin = sm->rmin;
     const KBLayout L = KBLayout::make(g.n, g.nnz, g.npart, true, g.tcap);
     char* base = smem + kKBSmall;
     uint32_t* arc = reinterpret_cast<uint32_t*>(base + L.arc);
@@ -345,7 +359,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
     const int n = g.n;
     const int tcap = g.tcap;
 
-    if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memtime();
+    if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 16 + 0] = __builtin_amdgcn_s_memtime();
     for (int k = tid; k < 256; k += KB_BLOCK)
         rtl[k] = k < g.nrtab ? g.rtab[k] : k == KB_ONE ? 1.0 : NAN;
     const bool one_chunk = nt <= tcap;
@@ -397,13 +411,22 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
                 if (sb[b] == v) d.h[b >> 1][b & 1] = 0;
             st8(D + (size_t)16 * v, d);
         }
-        if (tid < KB_SRC) rmin[tid] = kInfBits;
+        if (tid < KB_SRC) {  // rows-phase constants (their loads overlap the sweeps)
+            rmin[tid] = kInfBits;
+            const int s = sb[tid];
+            sm->src[tid] = s;
+            const double fs = s >= 0 ? g.vf[s] : NAN;
+            sm->cs[tid] = isnan(fs) ? 1.0 : 1.0 * fs;
+            sm->sw[tid] = s >= 0 ? g.self_w[s] : NAN;
+            sm->sr[tid] = s >= 0 ? g.self_r[s] : NAN;
+        }
+        if (tid == 0) sm->units = 0;
         __syncthreads();
 
-        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memtime();
+        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 16 + 1] = __builtin_amdgcn_s_memtime();
         // ---- Gauss-Seidel pull sweeps to the fixed point -------------------------
         for (;;) {
-            KB_COUNT(4);
+            if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 16 + 4] += 1;
             if (tid == 0) *changed = 0;
             __syncthreads();
             int ch = 0;
@@ -435,7 +458,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
             if (!again) break;
         }
 
-        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memtime();
+        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 16 + 2] = __builtin_amdgcn_s_memtime();
         // ---- parents: absolute index of the first tight in-arc, per source --------
 #pragma unroll
         for (int it = 0; it < KB_RIT; it++) {
@@ -463,7 +486,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
             for (int b = 0; b < KB_SRC; b++) sl[b * n + hv] = acc.h[b >> 1][b & 1];
         }
         __syncthreads();
-        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memtime();
+        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 16 + 5] = __builtin_amdgcn_s_memtime();
 
         // ---- slots -> walk arrays: sl[x] becomes the parent vertex in place, the arc's
         // reliability index goes to rix u8[KB_SRC][n] over the dead arc region (the source
@@ -491,36 +514,36 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
             }
             __syncthreads();
         }
-        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memtime();
+        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 16 + 6] = __builtin_amdgcn_s_memtime();
 
-        // ---- rows: WPS waves per source ----------------------------------------------
-        constexpr int WPS = KB_BLOCK / 64 / KB_SRC;
-        constexpr int STEP = WPS * 64;
-        const int wv = tid >> 6, lane = tid & 63;
-        const int b = wv % KB_SRC;
-        const int i = i0 + b;
-        int s = -1;
-        if (i < ns) {
-            s = src[i];
-            if (s < 0 || s >= n) s = -1;
-        }
-        const double fs = s >= 0 ? g.vf[s] : NAN;
-        const double cs = isnan(fs) ? 1.0 : 1.0 * fs;
-        const double s_w = s >= 0 ? g.self_w[s] : NAN, s_r = s >= 0 ? g.self_r[s] : NAN;
-        const uint16_t* pb = sl + b * n;
-        const uint8_t* xb = reinterpret_cast<const uint8_t*>(arc) + b * n;
-        double* lrow = (lat_out && s >= 0) ? lat_out + (long long)i * ld : nullptr;
-        double* rrow = (rel_out && s >= 0) ? rel_out + (long long)i * ld : nullptr;
-        double lmin = INFINITY;
+        // ---- rows: a work queue of (source, KB_WQ * 64 targets) units over all waves, so
+        // a source with a deep tree does not hold up the workgroup -------------------------
+        const int lane = tid & 63;
+        constexpr int UT = KB_WQ * 64;  // targets per unit
         for (int c0 = 0; c0 < nt; c0 += tcap) {
             const int cn = min(tcap, nt - c0);
             if (!one_chunk) {
-                __syncthreads();  // the previous chunk's targets are consumed
+                __syncthreads();  // the previous chunk's units are done
                 for (int j = tid; j < cn; j += KB_BLOCK) tg[j] = tgt[c0 + j];
+                if (tid == 0) sm->units = 0;
                 __syncthreads();
             }
-            if (s < 0) continue;
-            for (int j0 = (wv / KB_SRC) * 64 + lane; j0 - lane < cn; j0 += STEP * KB_WQ) {
+            const int nch = (cn + UT - 1) / UT;
+            for (;;) {
+                int u = 0;
+                if (lane == 0) u = atomicAdd(&sm->units, 1);
+                u = __builtin_amdgcn_readfirstlane(__shfl(u, 0, 64));
+                if (u >= KB_SRC * nch) break;
+                const int b = u % KB_SRC, j0 = (u / KB_SRC) * UT + lane;
+                const int s = sm->src[b];
+                if (s < 0) continue;
+                constexpr int STEP = 64;
+                const double cs = sm->cs[b], s_w = sm->sw[b], s_r = sm->sr[b];
+                const uint16_t* pb = sl + b * n;
+                const uint8_t* xb = reinterpret_cast<const uint8_t*>(arc) + b * n;
+                double* lrow = lat_out ? lat_out + (long long)(i0 + b) * ld : nullptr;
+                double* rrow = rel_out ? rel_out + (long long)(i0 + b) * ld : nullptr;
+                double lmin = INFINITY;
                 int tq[KB_WQ], cur[KB_WQ];
                 double ft[KB_WQ];
                 uint32_t pk[KB_WQ][KB_MAXD / 4];  // rix of the arcs walked, 4 per word
@@ -535,6 +558,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
 #pragma unroll
                     for (int k = 0; k < KB_MAXD / 4; k++) pk[q][k] = 0u;
                 }
+                KBT_MARK(t_a);
                 // walk: a chain that reaches the source stays there (parent s, factor 1.0)
                 int kmax = 0;  // wave-uniform
 #pragma unroll
@@ -553,6 +577,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
                         cur[q] = (int)p[q];
                     }
                 }
+                KBT_MARK(t_b);
                 double rr[KB_WQ];
 #pragma unroll
                 for (int q = 0; q < KB_WQ; q++) rr[q] = cs;
@@ -590,6 +615,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
                     }
                     rr[q] = r;
                 }
+                KBT_MARK(t_c);
 #pragma unroll
                 for (int q = 0; q < KB_WQ; q++) {
                     const int j = j0 + q * STEP;
@@ -616,16 +642,16 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
                     if (rrow) __builtin_nontemporal_store(Rv, rrow + c0 + j);
                     lmin = fmin(lmin, Lv);
                 }
-            }
-        }
-        if (s >= 0) {
+                KBT_MARK(t_d);
+                KBT_ACC(8, t_b - t_a); KBT_ACC(9, t_c - t_b); KBT_ACC(10, t_d - t_c); KBT_ACC(11, 1); KBT_ACC(12, kmax);
 #pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) lmin = fmin(lmin, __shfl_xor(lmin, d, 64));
-            if (lane == 0 && lmin < INFINITY) atomicMin(&rmin[b], as_u(lmin));
+                for (int d = 32; d >= 1; d >>= 1) lmin = fmin(lmin, __shfl_xor(lmin, d, 64));
+                if (lane == 0 && lmin < INFINITY) atomicMin(&rmin[b], as_u(lmin));
+            }
         }
         __syncthreads();
         if (tid < KB_SRC && i0 + tid < ns && row_min) row_min[i0 + tid] = as_d(rmin[tid]);
-        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memtime();
+        if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 16 + 3] = __builtin_amdgcn_s_memtime();
     }
 }
 

@@ -43,8 +43,9 @@ d_all = dbg.cpu().numpy().astype(np.int64).reshape(-1, 32 if eng.info["kernel"] 
 d = d_all[: len(S)]
 if eng.info["kernel"] == 2:
     flat = dbg.cpu().numpy().astype(np.int64)
-    kb = flat[len(S) * 8: len(S) * 8 + nwg * 8].reshape(nwg, 8)
     fused = eng.info["reserved"] == 1
+    w = 16 if fused else 8
+    kb = flat[len(S) * 8: len(S) * 8 + nwg * w].reshape(nwg, w)
     print(f"config {a.config} n={g.n} nnz={g.nnz} sources={len(S)} kernel=KB{' fused' if fused else '+K2'}")
     print(f"  KB stage+init mean {np.mean(kb[:,1]-kb[:,0]):10.0f} cyc")
     print(f"  KB sweeps  mean {np.mean(kb[:,2]-kb[:,1]):10.0f} cyc  max {np.max(kb[:,2]-kb[:,1])}  rounds mean {kb[:,4].mean():.1f} max {kb[:,4].max():.0f}")
@@ -52,6 +53,8 @@ if eng.info["kernel"] == 2:
         print(f"  KB parents mean {np.mean(kb[:,5]-kb[:,2]):10.0f} cyc")
         print(f"  KB convert mean {np.mean(kb[:,6]-kb[:,5]):10.0f} cyc")
         print(f"  KB rows    mean {np.mean(kb[:,3]-kb[:,6]):10.0f} cyc  max {np.max(kb[:,3]-kb[:,6])}")
+        tr = max(kb[:, 11].mean(), 1)
+        print(f"  rows wave0: {tr:.1f} trips, {kb[:,12].mean()/tr:.1f} steps/trip; walk {kb[:,8].mean()/tr:.0f}  fold {kb[:,9].mean()/tr:.0f}  output {kb[:,10].mean()/tr:.0f} cyc/trip")
         t0 = kb[:, 0] - kb[:, 0].min()
         print(f"  total      mean {np.mean(kb[:,3]-kb[:,0]):10.0f} cyc  start spread max {t0.max()}  end max {(kb[:,3]-kb[:,0].min()).max()}")
         sys.exit(0)

@@ -73,15 +73,15 @@ struct DevKB {
 
 // fused: parent slots sl u16[KB_SRC][n] (absolute index of each vertex's first tight
 // in-arc, 0xFFFF at the source and at unreached vertices), the reliability table, and the
-// staged target list tg i32[tcap]; once the parents are known sl holds the parent
-// vertices and the arc region the parent arcs' reliability indices rix u8[KB_SRC][n].
+// staged target list tg i32[tcap]; once the parents are known the arc region holds the
+// walk records wrec u32[KB_SRC][n] = parent | rix << 16.
 struct KBLayout {
     size_t arc, D, P, sl, rt, tg, total;
     __host__ __device__ static KBLayout make(int n, int nnz, int npart, bool fused = false, int tcap = 0) {
         KBLayout L;
         size_t o = 0;
         size_t arcb = a16(sizeof(uint32_t) * (size_t)nnz);
-        if (fused && arcb < a16((size_t)KB_SRC * n)) arcb = a16((size_t)KB_SRC * n);  // rix
+        if (fused && arcb < a16((size_t)4 * KB_SRC * n)) arcb = a16((size_t)4 * KB_SRC * n);  // walk records
         L.arc = o; o += arcb;
         L.D = o;   o += a16((size_t)16 * n);
         L.P = o;   o += a16((size_t)16 * npart);
@@ -332,10 +332,10 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
 //  - the parent pass stores, per (source, vertex), the absolute index of the first tight
 //    in-arc (nnz < 2^16 whenever the arcs fit the LDS), so no in-row offsets are read
 //  - the target list is staged in LDS once, before the sweeps, when it fits (else chunked)
-//  - slots become parent vertices (in place) and reliability indices (over the dead arc
-//    region); two waves per source write the lat row from D and the rel row by walking
-//    each target's tree path in LDS and folding the factors source-first: the
-//    multiplication order of K2's level sweep
+//  - slots become walk records (parent | rix << 16) over the dead arc region; units of
+//    (source, 256 targets) from a workgroup queue write the lat row from D and the rel row
+//    by walking each target's tree path in LDS (one ds_read_b32 per arc) and folding the
+//    factors source-first: the multiplication order of K2's level sweep
 //    (relv[v] = relv[parent] * r), so the bits agree.  Row minima as K2.
 __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, const int* __restrict__ src, int ns,
                                                                    int* __restrict__ err,
@@ -488,29 +488,27 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
         __syncthreads();
         if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 16 + 5] = __builtin_amdgcn_s_memtime();
 
-        // ---- slots -> walk arrays: sl[x] becomes the parent vertex in place, the arc's
-        // reliability index goes to rix u8[KB_SRC][n] over the dead arc region (the source
-        // and unreached vertices point at themselves with factor 1.0)
+        // ---- slots -> walk records wrec u32[KB_SRC][n] = parent | rix << 16 over the dead
+        // arc region (the source and unreached vertices point at themselves, factor 1.0);
+        // held in registers across the barrier after which no arc is read
         {
-            uint32_t rxp[KB_CV / 4];
-#pragma unroll
-            for (int k = 0; k < KB_CV / 4; k++) rxp[k] = 0u;
+            uint32_t cv[KB_CV];
 #pragma unroll
             for (int k = 0; k < KB_CV; k++) {
                 const int x = tid + k * KB_BLOCK;
+                cv[k] = 0u;
                 if (x < KB_SRC * n) {
                     const uint32_t a = sl[x];
                     const uint32_t rec = arc[a == 0xFFFFu ? 0u : a];
-                    sl[x] = a == 0xFFFFu ? (uint16_t)(x % n) : (uint16_t)(rec >> 16);
-                    rxp[k >> 2] |= (a == 0xFFFFu ? (uint32_t)KB_ONE : (rec >> 8) & 0xFFu) << ((k & 3) * 8);
+                    cv[k] = a == 0xFFFFu ? ((uint32_t)(x % n) | ((uint32_t)KB_ONE << 16))
+                                         : ((rec >> 16) | (((rec >> 8) & 0xFFu) << 16));
                 }
             }
             __syncthreads();  // every arc read done
-            uint8_t* rixw = reinterpret_cast<uint8_t*>(arc);
 #pragma unroll
             for (int k = 0; k < KB_CV; k++) {
                 const int x = tid + k * KB_BLOCK;
-                if (x < KB_SRC * n) rixw[x] = (uint8_t)(rxp[k >> 2] >> ((k & 3) * 8));
+                if (x < KB_SRC * n) arc[x] = cv[k];
             }
             __syncthreads();
         }
@@ -539,8 +537,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
                 if (s < 0) continue;
                 constexpr int STEP = 64;
                 const double cs = sm->cs[b], s_w = sm->sw[b], s_r = sm->sr[b];
-                const uint16_t* pb = sl + b * n;
-                const uint8_t* xb = reinterpret_cast<const uint8_t*>(arc) + b * n;
+                const uint32_t* wb = arc + b * n;  // walk records of source b
                 double* lrow = lat_out ? lat_out + (long long)(i0 + b) * ld : nullptr;
                 double* rrow = rel_out ? rel_out + (long long)(i0 + b) * ld : nullptr;
                 double lmin = INFINITY;
@@ -559,36 +556,50 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
                     for (int k = 0; k < KB_MAXD / 4; k++) pk[q][k] = 0u;
                 }
                 KBT_MARK(t_a);
-                // walk: a chain that reaches the source stays there (parent s, factor 1.0)
-                int kmax = 0;  // wave-uniform
-#pragma unroll
-                for (int k = 0; k < KB_MAXD; k++) {
+                // walk in blocks of 4 arcs (a chain that reaches the source stays there: parent
+                // s, factor exactly 1.0, so the block padding is harmless); one packed word of
+                // reliability indices per chain and block
+                int nb = 0;  // blocks walked, wave-uniform
+#pragma unroll 1
+                for (; nb < KB_MAXD / 4; nb++) {
                     bool any = false;
 #pragma unroll
                     for (int q = 0; q < KB_WQ; q++) any = any || cur[q] != s;
                     if (!__any(any)) break;
-                    kmax = k + 1;
-                    uint32_t p[KB_WQ], rx[KB_WQ];
+                    uint32_t acc[KB_WQ];
 #pragma unroll
-                    for (int q = 0; q < KB_WQ; q++) { p[q] = pb[cur[q]]; rx[q] = xb[cur[q]]; }
+                    for (int e = 0; e < 4; e++) {
+                        uint32_t pr[KB_WQ];
 #pragma unroll
-                    for (int q = 0; q < KB_WQ; q++) {
-                        pk[q][k >> 2] |= rx[q] << ((k & 3) * 8);
-                        cur[q] = (int)p[q];
+                        for (int q = 0; q < KB_WQ; q++) pr[q] = wb[cur[q]];
+#pragma unroll
+                        for (int q = 0; q < KB_WQ; q++) {
+                            acc[q] = e == 0 ? (pr[q] >> 16) : (acc[q] | ((pr[q] >> 16) << (8 * e)));
+                            cur[q] = (int)(pr[q] & 0xFFFFu);
+                        }
                     }
+#pragma unroll
+                    for (int q = 0; q < KB_WQ; q++) pk[q][nb] = acc[q];
                 }
                 KBT_MARK(t_b);
+                const int kmax = 4 * nb;
+                // fold source-first: the last arc walked is the first factor
                 double rr[KB_WQ];
 #pragma unroll
                 for (int q = 0; q < KB_WQ; q++) rr[q] = cs;
+#pragma unroll 1
+                for (int k4 = nb - 1; k4 >= 0; k4--) {
+                    uint32_t wq[KB_WQ];
 #pragma unroll
-                for (int k = KB_MAXD - 1; k >= 0; k--) {
-                    if (k >= kmax) continue;
-                    double x[KB_WQ];
+                    for (int q = 0; q < KB_WQ; q++) wq[q] = pk[q][k4];
 #pragma unroll
-                    for (int q = 0; q < KB_WQ; q++) x[q] = rtl[(pk[q][k >> 2] >> ((k & 3) * 8)) & 0xFFu];
+                    for (int e = 3; e >= 0; e--) {
+                        double x[KB_WQ];
 #pragma unroll
-                    for (int q = 0; q < KB_WQ; q++) rr[q] *= x[q];
+                        for (int q = 0; q < KB_WQ; q++) x[q] = rtl[(wq[q] >> (8 * e)) & 0xFFu];
+#pragma unroll
+                        for (int q = 0; q < KB_WQ; q++) rr[q] *= x[q];
+                    }
                 }
 #pragma unroll
                 for (int q = 0; q < KB_WQ; q++) {
@@ -597,18 +608,18 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
                     // source side, each collected by re-walking from t (O(L^2 / KB_MAXD) steps)
                     const int t = tq[q];
                     int depth = 0;
-                    for (int c = t; c != s && depth <= n; c = pb[c]) depth++;
+                    for (int c = t; c != s && depth <= n; c = (int)(wb[c] & 0xFFFFu)) depth++;
                     double r = cs;
                     for (int lo = 1; lo <= depth && lo <= n; lo += 16) {
                         const int hi = min(depth, lo + 15);
                         int c = t;
-                        for (int k = 0; k < depth - hi; k++) c = pb[c];
+                        for (int k = 0; k < depth - hi; k++) c = (int)(wb[c] & 0xFFFFu);
                         unsigned long long f0 = 0ull, f1 = 0ull;  // factors of depths hi .. lo
                         for (int k = 0; k <= hi - lo; k++) {
-                            const unsigned long long x = xb[c];
+                            const unsigned long long x = wb[c] >> 16;
                             if (k < 8) f0 |= x << (8 * k);
                             else f1 |= x << (8 * (k - 8));
-                            c = pb[c];
+                            c = (int)(wb[c] & 0xFFFFu);
                         }
                         for (int k = hi - lo; k >= 0; k--)
                             r *= rtl[(k < 8 ? f0 >> (8 * k) : f1 >> (8 * (k - 8))) & 0xFFu];

@@ -922,22 +922,29 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
 #pragma unroll
                     for (int k = 0; k < KD_MAXD / 4; k++) pk[q][k] = 0u;
                 }
-                int kmax = 0;  // wave-uniform: steps taken
-#pragma unroll
-                for (int k = 0; k < KD_MAXD; k++) {
+                // blocks of 4 arcs (parked chains multiply an exact 1.0, so the padding is
+                // harmless): one packed word per chain and block keeps the loop off the VALU
+                int nb = 0;  // blocks walked, wave-uniform
+#pragma unroll 1
+                for (; nb < KD_MAXD / 4; nb++) {
                     bool any = false;
 #pragma unroll
                     for (int q = 0; q < KD_WQ; q++) any = any || cur[q] != s;
                     if (!__any(any)) break;
-                    kmax = k + 1;
-                    uint32_t p[KD_WQ], rx[KD_WQ];
+                    uint32_t acc[KD_WQ];
 #pragma unroll
-                    for (int q = 0; q < KD_WQ; q++) { p[q] = parv[cur[q]]; rx[q] = rixl[cur[q]]; }
+                    for (int e = 0; e < 4; e++) {
+                        uint32_t p[KD_WQ], rx[KD_WQ];
 #pragma unroll
-                    for (int q = 0; q < KD_WQ; q++) {
-                        pk[q][k >> 2] |= rx[q] << ((k & 3) * 8);
-                        cur[q] = (int)p[q];
+                        for (int q = 0; q < KD_WQ; q++) { p[q] = parv[cur[q]]; rx[q] = rixl[cur[q]]; }
+#pragma unroll
+                        for (int q = 0; q < KD_WQ; q++) {
+                            acc[q] = e == 0 ? rx[q] : (acc[q] | (rx[q] << (8 * e)));
+                            cur[q] = (int)p[q];
+                        }
                     }
+#pragma unroll
+                    for (int q = 0; q < KD_WQ; q++) pk[q][nb] = acc[q];
                 }
                 {
                     bool any = false;
@@ -948,14 +955,19 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                 double rr[KD_WQ];
 #pragma unroll
                 for (int q = 0; q < KD_WQ; q++) rr[q] = cs;
+#pragma unroll 1
+                for (int k4 = nb - 1; k4 >= 0; k4--) {  // source-first: the last arc walked first
+                    uint32_t wq[KD_WQ];
 #pragma unroll
-                for (int k = KD_MAXD - 1; k >= 0; k--) {
-                    if (k >= kmax) continue;
-                    double x[KD_WQ];
+                    for (int q = 0; q < KD_WQ; q++) wq[q] = pk[q][k4];
 #pragma unroll
-                    for (int q = 0; q < KD_WQ; q++) x[q] = rtl[(pk[q][k >> 2] >> ((k & 3) * 8)) & 0xFFu];
+                    for (int e = 3; e >= 0; e--) {
+                        double x[KD_WQ];
 #pragma unroll
-                    for (int q = 0; q < KD_WQ; q++) rr[q] *= x[q];
+                        for (int q = 0; q < KD_WQ; q++) x[q] = rtl[(wq[q] >> (8 * e)) & 0xFFu];
+#pragma unroll
+                        for (int q = 0; q < KD_WQ; q++) rr[q] *= x[q];
+                    }
                 }
                 double f2[KD_WQ];
 #pragma unroll

@@ -240,8 +240,9 @@ def main():
             "bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
             "traffic": load_traffic(args.config, ns),
             "kernel": {0: "sssp_rows_kernel", 1: "sssp_k32_kernel",
-                       2: "sssp_batch_kernel+path_attr_kernel", 3: "sssp_k16_kernel",
-                       4: "sssp_delta_kernel"}[eng.info["kernel"]],
+                       2: ("sssp_batch_rows_kernel" if eng.info["reserved"] == 1
+                           else "sssp_batch_kernel+path_attr_kernel"),
+                       3: "sssp_k16_kernel", 4: "sssp_delta_kernel"}[eng.info["kernel"]],
             "bytes_per_source": b_src(n, nnz, nt),
         },
         "verified_rows_vs_oracle": verified,

@@ -9,7 +9,7 @@ import json
 import os
 import sys
 
-HOT = ("sssp_batch_kernel", "path_attr_kernel", "sssp_k32_kernel", "sssp_rows_kernel", "sssp_k16", "sssp_delta_kernel")
+HOT = ("sssp_batch_kernel", "sssp_batch_rows_kernel", "path_attr_kernel", "sssp_k32_kernel", "sssp_rows_kernel", "sssp_k16", "sssp_delta_kernel")
 
 
 def load(path):

@@ -24,6 +24,9 @@ pmc() {  # cfg counter bench-args...
   cp gpurun_out/prof_$tag/pmc_$cfg/$ctr/run_counter_collection.csv gpurun_out/prof_$tag/pmc_$cfg/$(echo $ctr | tr A-Z a-z | sed 's/_size//')_counter_collection.csv
 }
 [ "${PROF_PMC:-1}" = 0 ] && { echo prof done; exit 0; }
+pmc c2 FETCH_SIZE --steps 5 --warmup 2
+pmc c2 WRITE_SIZE --steps 5 --warmup 2
+[ "${PROF_PMC}" = c2 ] && { echo prof done; exit 0; }
 pmc c4 FETCH_SIZE --config c4 --steps 2 --warmup 1 --sources 4096
 pmc c4 WRITE_SIZE --config c4 --steps 2 --warmup 1 --sources 4096
 pmc c3 FETCH_SIZE --config c3 --steps 2 --warmup 1

@@ -33,12 +33,18 @@ typedef struct shd_topology shd_topology_t;
 /* graphml -> igraph-numbered arrays (plain or .xz/.gz file).  On success the caller
  * owns *out (release with shd_graphml_free). Validation as topology.c:565-1185;
  * returns SHD_ROUTE_EINVAL with a message in errbuf on failure. */
+enum { SHD_VATTR_IP, SHD_VATTR_CITYCODE, SHD_VATTR_COUNTRYCODE, SHD_VATTR_GEOCODE, SHD_VATTR_TYPE, SHD_VATTR_N };
 typedef struct shd_graphml {
     shd_graph_t graph;         /* arrays owned by this struct */
     char** vertex_ids;         /* graphml node id of each vertex */
     double* bandwidth_down;    /* vertex attributes Shadow reads at attach time */
     double* bandwidth_up;
     int32_t has_vertex_packetloss;
+    /* string vertex attributes ip, citycode, countrycode, geocode, type (SHD_VATTR_*):
+     * has = the key is declared for nodes; values as igraph holds them (key default or
+     * "" where a node has no <data>); NULL arrays when the key is not declared */
+    int32_t has_vertex_str[SHD_VATTR_N];
+    char** vertex_str[SHD_VATTR_N];
 } shd_graphml_t;
 int shd_graphml_load(const char* path, shd_graphml_t* out, char* errbuf, size_t errlen);
 void shd_graphml_free(shd_graphml_t* g);
@@ -56,6 +62,31 @@ int32_t shd_topology_find_vertex(const shd_topology_t* top, const char* graphml_
  * verticesWithAttachedHosts; detach never shrinks it (topology.c:2437). */
 int shd_topology_attach_vertex(shd_topology_t* top, int32_t vertex);
 int32_t shd_topology_attached_count(const shd_topology_t* top);
+
+/* Host attachment: _topology_findAttachmentVertex (topology.c:2245-2366) with its
+ * per-vertex filter hook (topology.c:2094-2216) and longest-prefix match
+ * (topology.c:2218-2243).  The index precomputes each vertex's parsed IP and
+ * case-folded code hashes once, so a lookup is two linear passes of integer compares
+ * instead of 5 igraph string-attribute lookups per vertex.  Hints may be NULL.
+ * next_double(ctx) is called exactly where the reference calls
+ * random_nextDouble(randomSourcePool) (one draw, only when no longest-prefix match is
+ * used), so a caller passing Shadow's Random keeps its stream bit for bit.
+ * Returns the vertex index, or -1 (no vertices / bad arguments). */
+typedef struct shd_attach shd_attach_t;
+typedef double (*shd_next_double_fn)(void* ctx);
+int shd_attach_create(shd_attach_t** out, const shd_graphml_t* g);
+int32_t shd_attach_find_vertex(const shd_attach_t* a, shd_next_double_fn next_double, void* ctx,
+                               const char* ip_hint, const char* citycode_hint, const char* countrycode_hint,
+                               const char* geocode_hint, const char* type_hint);
+void shd_attach_destroy(shd_attach_t* a);
+
+/* topology_attach (topology.c:2371-2439) for a topology loaded from graphml: pick the
+ * vertex as above, attach it, return the vertex (-1 on error) and, when the out
+ * pointers are non-NULL, its bandwidths truncated to integers like (guint64) casts. */
+int32_t shd_topology_attach(shd_topology_t* top, shd_next_double_fn next_double, void* ctx,
+                            const char* ip_hint, const char* citycode_hint, const char* countrycode_hint,
+                            const char* geocode_hint, const char* type_hint,
+                            uint64_t* bw_down_out, uint64_t* bw_up_out);
 
 /* Public accessors (topology.c:2053-2092); fill the cache on the first miss. */
 double shd_topology_get_latency(shd_topology_t* top, int32_t src, int32_t dst);

@@ -17,7 +17,8 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-f
          "-Wall", "-Wno-unused-result"]
 
 
-FRONT_SOURCES = [os.path.join(HERE, "csrc", "graphml.c"), os.path.join(HERE, "csrc", "topology_front.c")]
+FRONT_SOURCES = [os.path.join(HERE, "csrc", "graphml.c"), os.path.join(HERE, "csrc", "topology_front.c"),
+                 os.path.join(HERE, "csrc", "attach.c")]
 FRONT_OUT = os.path.join(HERE, "libshd_topology.so")
 CC = os.environ.get("CC", "gcc")
 

@@ -95,6 +95,21 @@ static void ipush(ivec* v, int32_t x) {
     v->a[v->len++] = x;
 }
 
+typedef struct {
+    char** a;
+    size_t len, cap;
+} svec;
+static void spush(svec* v, char* x) {
+    if (v->len == v->cap) { v->cap = v->cap ? 2 * v->cap : 1024; v->a = realloc(v->a, v->cap * sizeof(char*)); }
+    v->a[v->len++] = x;
+}
+/* string vertex attributes read at attach time (topology.c:2094-2216), by SHD_VATTR_* */
+static const char* const kVstrName[SHD_VATTR_N] = {"ip", "citycode", "countrycode", "geocode", "type"};
+static int vstr_slot(const char* name) {
+    for (int a = 0; a < SHD_VATTR_N; a++) if (!strcmp(name, kVstrName[a])) return a;
+    return -1;
+}
+
 static double parse_num(const char* s) {
     if (!s) return NAN;
     while (*s == ' ' || *s == '\t' || *s == '\n' || *s == '\r') s++;
@@ -135,6 +150,7 @@ int shd_graphml_load(const char* path, shd_graphml_t* out, char* errbuf, size_t 
     char** vid = NULL;
     size_t vcap = 0;
     dvec va[VA_N] = {{0}};
+    svec vs[SHD_VATTR_N] = {{0}};
     ivec esrc = {0}, edst = {0};
     dvec ea[EA_N] = {{0}};
     int directed = 1; /* graphml default edgedefault is "directed" */
@@ -185,6 +201,7 @@ int shd_graphml_load(const char* path, shd_graphml_t* out, char* errbuf, size_t 
                         if ((size_t)n == vcap) { vcap = vcap ? 2 * vcap : 1024; vid = realloc(vid, vcap * sizeof(char*)); }
                         vid[n] = strdup(id);
                         for (int a = 0; a < VA_N; a++) dpush(&va[a], NAN);
+                        for (int a = 0; a < SHD_VATTR_N; a++) spush(&vs[a], NULL);
                         n++;
                     }
                     xmlFree(id);
@@ -202,6 +219,7 @@ int shd_graphml_load(const char* path, shd_graphml_t* out, char* errbuf, size_t 
                             if ((size_t)n == vcap) { vcap = vcap ? 2 * vcap : 1024; vid = realloc(vid, vcap * sizeof(char*)); }
                             vid[n] = strdup(id);
                             for (int a = 0; a < VA_N; a++) dpush(&va[a], NAN);
+                            for (int a = 0; a < SHD_VATTR_N; a++) spush(&vs[a], NULL);
                             n++;
                         }
                         xmlFree(id);
@@ -228,6 +246,10 @@ int shd_graphml_load(const char* path, shd_graphml_t* out, char* errbuf, size_t 
                         else if (!strcmp(k->name, "bandwidthup")) va[VA_BWUP].a[cur] = x;
                         else if (!strcmp(k->name, "packetloss")) va[VA_LOSS].a[cur] = x;
                         else if (!strcmp(k->name, "asn")) va[VA_ASN].a[cur] = x;
+                    } else if (cur_kind == K_NODE && k->type == T_STR && vstr_slot(k->name) >= 0) {
+                        char** slot = &vs[vstr_slot(k->name)].a[cur];
+                        free(*slot);
+                        *slot = strdup(text ? text : "");
                     } else if (cur_kind == K_EDGE && k->type == T_NUM) {
                         double x = parse_num(text);
                         if (!strcmp(k->name, "latency")) ea[EA_LAT].a[cur] = x;
@@ -249,7 +271,17 @@ int shd_graphml_load(const char* path, shd_graphml_t* out, char* errbuf, size_t 
     if (ret < 0 && !rc) { seterr(errbuf, errlen, "XML parse error in '%s'", path); rc = SHD_ROUTE_EINVAL; }
     xmlFreeTextReader(rd);
 
-    /* key defaults apply to elements lacking a <data> (igraph) */
+    /* key defaults apply to elements lacking a <data> (igraph); a declared string key
+     * without a default leaves "" (igraph), which topology.c treats as absent */
+    int has_vs[SHD_VATTR_N] = {0};
+    for (int i = 0; i < nkeys && !rc; i++) {
+        gkey* k = &keys[i];
+        if (!k->name || !(k->for_mask & K_NODE) || k->type != T_STR || vstr_slot(k->name) < 0) continue;
+        const int a = vstr_slot(k->name);
+        has_vs[a] = 1;
+        for (size_t j = 0; j < vs[a].len; j++)
+            if (!vs[a].a[j]) vs[a].a[j] = strdup(k->defval ? k->defval : "");
+    }
     for (int i = 0; i < nkeys && !rc; i++) {
         gkey* k = &keys[i];
         if (!k->defval || !k->name || k->type != T_NUM) continue;
@@ -351,9 +383,17 @@ int shd_graphml_load(const char* path, shd_graphml_t* out, char* errbuf, size_t 
         out->vertex_ids = vid; vid = NULL;
         out->bandwidth_down = va[VA_BWDOWN].a; va[VA_BWDOWN].a = NULL;
         out->bandwidth_up = va[VA_BWUP].a; va[VA_BWUP].a = NULL;
+        for (int a = 0; a < SHD_VATTR_N; a++) {
+            out->has_vertex_str[a] = has_vs[a];
+            out->vertex_str[a] = vs[a].a; vs[a].a = NULL;
+        }
     }
     if (vid) { for (int32_t v = 0; v < n; v++) free(vid[v]); free(vid); }
     for (int a = 0; a < VA_N; a++) free(va[a].a);
+    for (int a = 0; a < SHD_VATTR_N; a++) {
+        if (vs[a].a) for (size_t j = 0; j < vs[a].len; j++) free(vs[a].a[j]);
+        free(vs[a].a);
+    }
     for (int a = 0; a < EA_N; a++) free(ea[a].a);
     free(esrc.a); free(edst.a); free(prefer);
     for (int i = 0; i < nkeys; i++) {
@@ -374,5 +414,9 @@ void shd_graphml_free(shd_graphml_t* g) {
     free((void*)g->graph.edge_latency); free((void*)g->graph.edge_packetloss);
     free((void*)g->graph.vertex_packetloss);
     free(g->bandwidth_down); free(g->bandwidth_up);
+    for (int a = 0; a < SHD_VATTR_N; a++) {
+        if (g->vertex_str[a]) for (int32_t v = 0; v < g->graph.n_vertices; v++) free(g->vertex_str[a][v]);
+        free(g->vertex_str[a]);
+    }
     memset(g, 0, sizeof(*g));
 }

@@ -62,6 +62,7 @@ struct shd_topology {
     pthread_mutex_t lock;
     pcmap pc;
     pthread_mutex_t pclock;
+    shd_attach_t* at;    /* host attachment index (graphml topologies only) */
 };
 
 static inline size_t tri(int32_t na, int32_t i, int32_t j) { /* i <= j */
@@ -140,6 +141,7 @@ shd_topology_t* shd_topology_new(const char* graph_path, const int* devices, int
         return NULL;
     }
     t->g = t->gml.graph;
+    if (shd_attach_create(&t->at, &t->gml) != SHD_ROUTE_OK) t->at = NULL;
     return finish_new(t, devices, ndev);
 }
 
@@ -172,6 +174,7 @@ void shd_topology_free(shd_topology_t* t) {
         free((void*)t->g.edge_src); free((void*)t->g.edge_dst); free((void*)t->g.edge_latency);
         free((void*)t->g.edge_packetloss); free((void*)t->g.vertex_packetloss);
     }
+    shd_attach_destroy(t->at);
     shd_graphml_free(&t->gml);
     free(t->arow); free(t->acol); free(t->attached); free(t->A); free(t->cid);
     free(t->lat); free(t->rel);
@@ -198,6 +201,20 @@ int shd_topology_attach_vertex(shd_topology_t* t, int32_t v) {
     }
     pthread_mutex_unlock(&t->lock);
     return SHD_ROUTE_OK;
+}
+
+int32_t shd_topology_attach(shd_topology_t* t, shd_next_double_fn next_double, void* ctx,
+                            const char* ip_hint, const char* citycode_hint, const char* countrycode_hint,
+                            const char* geocode_hint, const char* type_hint,
+                            uint64_t* bw_down_out, uint64_t* bw_up_out) {
+    if (!t || !t->at) return -1;
+    const int32_t v = shd_attach_find_vertex(t->at, next_double, ctx, ip_hint, citycode_hint, countrycode_hint,
+                                             geocode_hint, type_hint);
+    if (v < 0 || shd_topology_attach_vertex(t, v) != SHD_ROUTE_OK) return -1;
+    /* topology.c:2394-2405: default cluster bandwidths, (guint64) casts */
+    if (bw_up_out) *bw_up_out = (uint64_t)t->gml.bandwidth_up[v];
+    if (bw_down_out) *bw_down_out = (uint64_t)t->gml.bandwidth_down[v];
+    return v;
 }
 
 int32_t shd_topology_attached_count(const shd_topology_t* t) { return t ? t->nattached : -1; }

@@ -27,13 +27,18 @@ EXPORTS = (
     "shd_topology_increment_path_packet_counter", "shd_topology_get_path_packet_count",
     "shd_topology_is_direct_path", "shd_topology_min_path_latency", "shd_topology_runahead_ns",
     "shd_topology_fill", "shd_topology_dump_paths",
+    "shd_attach_create", "shd_attach_find_vertex", "shd_attach_destroy", "shd_topology_attach",
 )
+
+VATTRS = ("ip", "citycode", "countrycode", "geocode", "type")  # SHD_VATTR_* order
+_NEXT_DOUBLE = C.CFUNCTYPE(C.c_double, C.c_void_p)
 
 
 class _GraphML(C.Structure):
     _fields_ = [("graph", _Graph), ("vertex_ids", C.POINTER(C.c_char_p)),
                 ("bandwidth_down", C.POINTER(C.c_double)), ("bandwidth_up", C.POINTER(C.c_double)),
-                ("has_vertex_packetloss", C.c_int32)]
+                ("has_vertex_packetloss", C.c_int32), ("has_vertex_str", C.c_int32 * 5),
+                ("vertex_str", C.POINTER(C.c_char_p) * 5)]
 
 
 _lib = None
@@ -82,6 +87,15 @@ def load_library():
     L.shd_topology_fill.argtypes = [P, C.POINTER(D)]
     L.shd_topology_dump_paths.restype = C.c_int
     L.shd_topology_dump_paths.argtypes = [P, P]
+    S = C.c_char_p
+    L.shd_attach_create.restype = C.c_int
+    L.shd_attach_create.argtypes = [C.POINTER(P), C.POINTER(_GraphML)]
+    L.shd_attach_find_vertex.restype = I32
+    L.shd_attach_find_vertex.argtypes = [P, _NEXT_DOUBLE, P, S, S, S, S, S]
+    L.shd_attach_destroy.argtypes = [P]
+    L.shd_topology_attach.restype = I32
+    L.shd_topology_attach.argtypes = [P, _NEXT_DOUBLE, P, S, S, S, S, S, C.POINTER(C.c_uint64),
+                                      C.POINTER(C.c_uint64)]
     _lib = L
     return L
 
@@ -110,6 +124,59 @@ def load_graphml(path: str) -> Graph:
                      name=os.path.basename(path))
     finally:
         L.shd_graphml_free(C.byref(out))
+
+
+def _enc(x):
+    return None if x is None else x.encode()
+
+
+class AttachIndex:
+    """Host attachment over a graphml file (shd_attach_*, no GPU): the vertex a host
+    with these hints joins, as _topology_findAttachmentVertex (topology.c:2245-2366).
+    ``next_double`` is called where the reference draws random_nextDouble."""
+
+    def __init__(self, path: str):
+        L = load_library()
+        self._gml = _GraphML()
+        err = C.create_string_buffer(512)
+        rc = L.shd_graphml_load(path.encode(), C.byref(self._gml), err, 512)
+        if rc != 0:
+            raise ValueError(err.value.decode() or f"graphml load failed ({rc})")
+        self._h = C.c_void_p()
+        rc = L.shd_attach_create(C.byref(self._h), C.byref(self._gml))
+        if rc != 0:
+            L.shd_graphml_free(C.byref(self._gml))
+            raise ValueError(f"shd_attach_create failed ({rc})")
+        self.n = self._gml.graph.n_vertices
+
+    def vertex_attrs(self):
+        """{name: [value or None per vertex] or None when the key is not declared}."""
+        out = {}
+        for a, name in enumerate(VATTRS):
+            if not self._gml.has_vertex_str[a]:
+                out[name] = None
+                continue
+            col = self._gml.vertex_str[a]
+            out[name] = [None if col[v] is None else col[v].decode() for v in range(self.n)]
+        return out
+
+    def find(self, next_double=None, ip=None, citycode=None, countrycode=None, geocode=None, type=None) -> int:
+        cb = _NEXT_DOUBLE((lambda _ctx: float(next_double()))) if next_double else _NEXT_DOUBLE()
+        return int(load_library().shd_attach_find_vertex(self._h, cb, None, _enc(ip), _enc(citycode),
+                                                          _enc(countrycode), _enc(geocode), _enc(type)))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L = load_library()
+            L.shd_attach_destroy(self._h)
+            L.shd_graphml_free(C.byref(self._gml))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Topology:
@@ -160,6 +227,19 @@ class Topology:
         rc = load_library().shd_topology_attach_vertex(self._h, int(vertex))
         if rc:
             raise ValueError(f"attach failed ({rc})")
+
+    def attach_host(self, next_double=None, ip=None, citycode=None, countrycode=None, geocode=None, type=None):
+        """topology_attach (topology.c:2371-2439): (vertex, bandwidth down, bandwidth up)."""
+        cb = _NEXT_DOUBLE((lambda _ctx: float(next_double()))) if next_double else _NEXT_DOUBLE()
+        down, up = C.c_uint64(), C.c_uint64()
+        v = load_library().shd_topology_attach(self._h, cb, None, _enc(ip), _enc(citycode), _enc(countrycode),
+                                               _enc(geocode), _enc(type), C.byref(down), C.byref(up))
+        if v < 0:
+            raise ValueError("attach failed (topology not loaded from graphml?)")
+        return int(v), int(down.value), int(up.value)
+
+    def attached_count(self) -> int:
+        return int(load_library().shd_topology_attached_count(self._h))
 
     def attach_all(self, vertices):
         for v in vertices:

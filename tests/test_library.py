@@ -54,7 +54,7 @@ def test_front_end_exports():
     from shadow_amd import build, topology
     build.build()
     text = open(os.path.join(ROOT, "include", "shd_topology.h")).read()
-    declared = sorted(set(re.findall(r"\b(shd_(?:topology|graphml)_[a-z_]+)\s*\(", text)))
+    declared = sorted(set(re.findall(r"\b(shd_(?:topology|graphml|attach)_[a-z_]+)\s*\(", text)))
     assert sorted(topology.EXPORTS) == declared
     lib = ctypes.CDLL(topology.LIB_PATH)
     for sym in declared:

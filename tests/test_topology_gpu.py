@@ -121,3 +121,32 @@ def test_dump_paths(topo, tmp_path):
     lines = out.read_text().splitlines()
     assert len(lines) == g.n * (g.n + 1) // 2
     assert lines[0].startswith("Found path 0<->0 in cache: SourceIndex=0 DestinationIndex=0 Latency=")
+
+
+def test_topology_attach_hosts(topo, tmp_path):
+    """topology_attach (topology.c:2371-2439) end to end: the vertex as the restatement of
+    _topology_findAttachmentVertex picks it, the vertex joins the routed set, and the
+    default bandwidths come back as (guint64) casts of the vertex attributes."""
+    import random
+    from oracle.attach_ref import ShadowRandom, find_attachment_vertex
+    from tests.test_attach import _graphml, _hints
+    p = tmp_path / "hosts.xml"
+    ips = _graphml(p, 60, 11)
+    idx = topo.AttachIndex(str(p))
+    attrs = idx.vertex_attrs()
+    t = topo.Topology.new(str(p))
+    rng = random.Random(5)
+    r1, r2 = ShadowRandom(42), ShadowRandom(42)   # one pool across hosts, as Shadow's
+    want_set = set()
+    for _ in range(30):
+        h = _hints(rng, ips)
+        v, down, up = t.attach_host(r1.next_double, **h)
+        w = find_attachment_vertex(attrs, 60, r2, ip_hint=h["ip"], citycode_hint=h["citycode"],
+                                   countrycode_hint=h["countrycode"], geocode_hint=h["geocode"], type_hint=h["type"])
+        assert v == w and (down, up) == (1000 + v, 2000 + 3 * v)
+        want_set.add(v)
+    assert r1.draws == r2.draws
+    A = sorted(want_set)
+    assert t.attached_count() == len(A)
+    assert all(t.is_routable(a, b) for a in A for b in A)
+    idx.close()

@@ -100,7 +100,9 @@ const char* shd_route_strerror(int code);
 /* Eager batch of SOURCE(s,.) rows: for i < ns, j < nt,
  *   lat_out[i*nt + j], rel_out[i*nt + j] = Path(src[i] -> tgt[j]);
  *   row_min_out[i] = min_j lat_out[i*nt + j]   (any of the three outputs may be NULL).
- * Host pointers; the call blocks. */
+ * Host pointers; the call blocks.  SHD_ROUTE_ENOEDGE / SHD_ROUTE_EUNREACH are per-entry
+ * failures: every row is still written, the failed entries are NaN (the reference skips
+ * storing those targets, topology.c:1812-1870) and the code is returned at the end. */
 int shd_route_rows(shd_route_t* ctx, const int32_t* src, int32_t ns, const int32_t* tgt,
                    int32_t nt, uint32_t flags, double* lat_out, double* rel_out,
                    double* row_min_out);

@@ -830,6 +830,7 @@ int host_rows(shd_route* c, const int32_t* src, int32_t ns, const int32_t* tgt, 
         return rc;
     if (nt && hipMemcpy(dtgt.p, tgt, sizeof(int32_t) * nt, hipMemcpyHostToDevice) != hipSuccess)
         return SHD_ROUTE_EDEVICE;
+    int soft = SHD_ROUTE_OK;
     for (int32_t i0 = 0; i0 < ns; i0 += chunk) {
         int32_t k = std::min(chunk, ns - i0);
         if (hipMemcpy(dsrc.p, src + i0, sizeof(int32_t) * k, hipMemcpyHostToDevice) != hipSuccess)
@@ -837,7 +838,10 @@ int host_rows(shd_route* c, const int32_t* src, int32_t ns, const int32_t* tgt, 
         rc = launch((const int32_t*)dsrc.p, k, (const int32_t*)dtgt.p, (double*)dlat.p, (double*)drel.p,
                     (double*)dmin.p);
         if (rc) return rc;
-        if ((rc = shd_route_sync(c, nullptr))) return rc;
+        // per-entry failures (missing self-loop, unreachable target) leave NaN in those
+        // entries only: the rows are still copied out and the code returned at the end
+        if ((rc = shd_route_sync(c, nullptr)) && rc != SHD_ROUTE_ENOEDGE && rc != SHD_ROUTE_EUNREACH) return rc;
+        if (rc && !soft) soft = rc;
         if (lat_out && hipMemcpy(lat_out + (size_t)i0 * nt, dlat.p, row_bytes * k, hipMemcpyDeviceToHost) != hipSuccess)
             return SHD_ROUTE_EDEVICE;
         if (rel_out && hipMemcpy(rel_out + (size_t)i0 * nt, drel.p, row_bytes * k, hipMemcpyDeviceToHost) != hipSuccess)
@@ -845,7 +849,7 @@ int host_rows(shd_route* c, const int32_t* src, int32_t ns, const int32_t* tgt, 
         if (row_min_out && hipMemcpy(row_min_out + i0, dmin.p, sizeof(double) * k, hipMemcpyDeviceToHost) != hipSuccess)
             return SHD_ROUTE_EDEVICE;
     }
-    return SHD_ROUTE_OK;
+    return soft;
 }
 }  // namespace
 

@@ -36,6 +36,9 @@ typedef struct {
     size_t cap, len;
 } pcmap;
 
+#define PC_STRIPES 64
+static inline unsigned pc_stripe(uint64_t key) { return (unsigned)((key * 0xD6E8FEB86659FD93ull) >> 58); }
+
 struct shd_topology {
     shd_graphml_t gml;   /* owns the arrays when loaded from a file */
     shd_graph_t g;       /* view used by the engine */
@@ -60,8 +63,10 @@ struct shd_topology {
     double min_lat;
     double fill_seconds;
     pthread_mutex_t lock;
-    pcmap pc;
-    pthread_mutex_t pclock;
+    /* packet counters: a sparse map striped over PC_STRIPES locks, so worker threads
+     * counting packets on different paths rarely meet (path.c:57-60 has no lock) */
+    pcmap pc[PC_STRIPES];
+    pthread_mutex_t pclock[PC_STRIPES];
     shd_attach_t* at;    /* host attachment index (graphml topologies only) */
 };
 
@@ -128,7 +133,7 @@ static shd_topology_t* finish_new(shd_topology_t* t, const int* devices, int nde
     for (int32_t v = 0; v < t->n; v++) t->cid[v] = -1;
     build_adjacency(t);
     pthread_mutex_init(&t->lock, NULL);
-    pthread_mutex_init(&t->pclock, NULL);
+    for (int k = 0; k < PC_STRIPES; k++) pthread_mutex_init(&t->pclock[k], NULL);
     return t;
 }
 
@@ -178,7 +183,7 @@ void shd_topology_free(shd_topology_t* t) {
     shd_graphml_free(&t->gml);
     free(t->arow); free(t->acol); free(t->attached); free(t->A); free(t->cid);
     free(t->lat); free(t->rel);
-    free(t->pc.keys); free(t->pc.vals);
+    for (int k = 0; k < PC_STRIPES; k++) { free(t->pc[k].keys); free(t->pc[k].vals); }
     free(t);
 }
 
@@ -243,7 +248,10 @@ static void* fill_worker(void* arg) {
         const int32_t nt = na - i0;
         int rc = shd_route_rows(t->eng[job->dev], t->A + i0, rows, t->A + i0, nt, SHD_ROUTE_DISPATCH,
                                 lbuf, rbuf, NULL);
-        if (rc) { job->rc = rc; break; }
+        /* ENOEDGE: a self pair without a self-loop; the rows are complete and that entry
+         * is NaN, i.e. not stored by the batch, as the reference skips the failed target
+         * (topology.c:1488-1495, 1812-1870); fill_locked resolves it below */
+        if (rc && rc != SHD_ROUTE_ENOEDGE) { job->rc = rc; break; }
         for (int32_t r = 0; r < rows; r++) {
             const int32_t i = i0 + r;
             const size_t base = tri(na, i, i);
@@ -292,9 +300,32 @@ static int fill_locked(shd_topology_t* t) {
         }
     }
     if (rc) return rc;
+    /* (s,s) pairs the batch could not store (no self-loop at s): the reference's next
+     * (s,s) lookup misses and computes _topology_computeShortestPathToSelf
+     * (topology.c:1674-1676, 1545-1653), i.e. 2*w_min and r_min^2 over s's out-edges */
+    {
+        int32_t nself = 0;
+        int32_t* sv = malloc(sizeof(int32_t) * ((size_t)t->na + 1));
+        for (int32_t i = 0; i < t->na; i++)
+            if (isnan(t->lat[tri(t->na, i, i)])) sv[nself++] = t->A[i];
+        if (nself) {
+            double* sl = malloc(sizeof(double) * (size_t)nself);
+            double* sr = malloc(sizeof(double) * (size_t)nself);
+            rc = shd_route_self(t->eng[0], sv, nself, sl, sr);
+            if (rc == SHD_ROUTE_ENOEDGE) rc = SHD_ROUTE_OK;  /* no out-edge: stays unstored */
+            for (int32_t q = 0; q < nself && !rc; q++) {
+                const size_t k = tri(t->na, t->cid[sv[q]], t->cid[sv[q]]);
+                t->lat[k] = sl[q];
+                t->rel[k] = sr[q];
+            }
+            free(sl); free(sr);
+        }
+        free(sv);
+        if (rc) return rc;
+    }
     double mn = 0;
     for (size_t k = 0; k < ntri; k++)  /* topology.c:1375: minLat == 0 means unset */
-        if (mn == 0 || t->lat[k] < mn) mn = t->lat[k];
+        if (!isnan(t->lat[k]) && (mn == 0 || t->lat[k] < mn)) mn = t->lat[k];
     t->min_lat = mn;
     t->fill_seconds += now_s() - t0;
     __atomic_store_n(&t->filled, 1, __ATOMIC_RELEASE);
@@ -321,7 +352,8 @@ static int64_t entry(shd_topology_t* t, int32_t s, int32_t d) {
     }
     const int32_t i = t->cid[s], j = t->cid[d];
     if (i < 0 || j < 0) return -1;  /* address not connected to the topology */
-    return (int64_t)(i <= j ? tri(t->na, i, j) : tri(t->na, j, i));
+    const int64_t k = (int64_t)(i <= j ? tri(t->na, i, j) : tri(t->na, j, i));
+    return isnan(t->lat[k]) ? -1 : k;  /* never stored (topology.c:2040-2046) */
 }
 
 double shd_topology_get_latency(shd_topology_t* t, int32_t s, int32_t d) {
@@ -364,21 +396,35 @@ static uint64_t* pc_slot(pcmap* m, uint64_t key) {
     return &m->vals[j];
 }
 
+/* read without inserting */
+static uint64_t pc_get(shd_topology_t* t, uint64_t key) {
+    const unsigned st = pc_stripe(key);
+    uint64_t v = 0;
+    pthread_mutex_lock(&t->pclock[st]);
+    const pcmap* m = &t->pc[st];
+    if (m->cap) {
+        size_t j = (key * 0x9E3779B97F4A7C15ull) & (m->cap - 1);
+        while (m->keys[j] && m->keys[j] != key) j = (j + 1) & (m->cap - 1);
+        if (m->keys[j]) v = m->vals[j];
+    }
+    pthread_mutex_unlock(&t->pclock[st]);
+    return v;
+}
+
 void shd_topology_increment_path_packet_counter(shd_topology_t* t, int32_t s, int32_t d) {
     int64_t k = entry(t, s, d);
     if (k < 0) return;
-    pthread_mutex_lock(&t->pclock);
-    (*pc_slot(&t->pc, (uint64_t)k + 1))++;
-    pthread_mutex_unlock(&t->pclock);
+    const uint64_t key = (uint64_t)k + 1;
+    const unsigned st = pc_stripe(key);
+    pthread_mutex_lock(&t->pclock[st]);
+    (*pc_slot(&t->pc[st], key))++;
+    pthread_mutex_unlock(&t->pclock[st]);
 }
 
 uint64_t shd_topology_get_path_packet_count(shd_topology_t* t, int32_t s, int32_t d) {
     int64_t k = entry(t, s, d);
     if (k < 0) return 0;
-    pthread_mutex_lock(&t->pclock);
-    uint64_t v = *pc_slot(&t->pc, (uint64_t)k + 1);
-    pthread_mutex_unlock(&t->pclock);
-    return v;
+    return pc_get(t, (uint64_t)k + 1);
 }
 
 double shd_topology_min_path_latency(shd_topology_t* t) {
@@ -406,10 +452,7 @@ int shd_topology_dump_paths(shd_topology_t* t, FILE* out) {
             char na_[32], nb_[32];
             if (!ia) { snprintf(na_, sizeof na_, "%d", a); ia = na_; }
             if (!ib) { snprintf(nb_, sizeof nb_, "%d", b); ib = nb_; }
-            uint64_t pc = 0;
-            pthread_mutex_lock(&t->pclock);
-            if (t->pc.cap) pc = *pc_slot(&t->pc, (uint64_t)k + 1);
-            pthread_mutex_unlock(&t->pclock);
+            const uint64_t pc = pc_get(t, (uint64_t)k + 1);
             /* path_toString (path.c:62-74) inside _topology_logAllCachedPathsHelper2 */
             fprintf(out, "Found path %s%s%s in cache: SourceIndex=%d DestinationIndex=%d Latency=%f "
                          "Reliability=%f PacketCount=%llu isDirect=%s\n",

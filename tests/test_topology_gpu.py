@@ -148,5 +148,19 @@ def test_topology_attach_hosts(topo, tmp_path):
     assert r1.draws == r2.draws
     A = sorted(want_set)
     assert t.attached_count() == len(A)
-    assert all(t.is_routable(a, b) for a in A for b in A)
+    # the ring has no self-loops: the batch cannot store (a, a) (topology.c:1488-1495), so
+    # the reference's (a, a) lookup computes the path to self, 2 * the lightest out-edge
+    # (topology.c:1674-1676, 1545-1653); every other pair is the ring distance
+    w = [1 + v % 7 for v in range(60)]   # edge v -- v+1 (mod 60)
+    def ring(a, b):
+        if a == b:
+            return 2.0 * min(w[a], w[a - 1])
+        lo, hi = min(a, b), max(a, b)
+        d = float(sum(w[lo:hi]))
+        return min(d, float(sum(w)) - d)
+    for a in A:
+        for b in A:
+            assert t.is_routable(a, b)
+            assert t.get_latency(a, b) == ring(a, b) and t.get_reliability(a, b) == 1.0
+    assert t.min_path_latency() == min(ring(a, b) for a in A for b in A)
     idx.close()

@@ -95,7 +95,7 @@ struct KBLayout {
 // small: changed flag, fused unit counter | row minima u64[8] | per-source constants of the
 // fused rows phase: source, 1.0 * f_s (or 1.0), self-loop latency and reliability
 struct KBSmall {
-    int changed, units, pad0, pad1;
+    int changed, flag1, flag2, units;  // KBF sweeps: changed/flag1/flag2 rotate
     unsigned long long rmin[8];
     int src[8];
     double cs[8], sw[8], sr[8];
@@ -345,7 +345,9 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
                                                                    double* __restrict__ row_min) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     KBSmall* sm = reinterpret_cast<KBSmall*>(smem);
-    int* changed = &sm->changed;
+    // three sweep flags in rotation: a sweep resets the next one's flag before its first
+    // barrier, when every thread has read the flag of two sweeps ago (2 barriers a sweep)
+    int* flags = &sm->changed;  // changed, flag1, flag2
     unsigned long long* rmin = sm->rmin;
     const KBLayout L = KBLayout::make(g.n, g.nnz, g.npart, true, g.tcap);
     char* base = smem + kKBSmall;
@@ -420,15 +422,15 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
             sm->sw[tid] = s >= 0 ? g.self_w[s] : NAN;
             sm->sr[tid] = s >= 0 ? g.self_r[s] : NAN;
         }
-        if (tid == 0) sm->units = 0;
+        if (tid == 0) { sm->units = 0; sm->changed = 0; }
         __syncthreads();
 
         if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 16 + 1] = __builtin_amdgcn_s_memtime();
         // ---- Gauss-Seidel pull sweeps to the fixed point -------------------------
-        for (;;) {
+        for (int fi = 0;; fi = fi == 2 ? 0 : fi + 1) {
             if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 16 + 4] += 1;
-            if (tid == 0) *changed = 0;
-            __syncthreads();
+            if (tid == 0) flags[fi == 2 ? 0 : fi + 1] = 0;
+            int* changed = flags + fi;
             int ch = 0;
 #pragma unroll
             for (int it = 0; it < KB_RIT; it++) {
@@ -453,9 +455,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
             }
             if (ch) *changed = 1;
             __syncthreads();
-            const int again = *changed;
-            __syncthreads();
-            if (!again) break;
+            if (!*changed) break;
         }
 
         if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 16 + 2] = __builtin_amdgcn_s_memtime();

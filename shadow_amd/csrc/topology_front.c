@@ -31,10 +31,14 @@
 #include "../../include/shd_topology.h"
 
 typedef struct {
-    uint64_t* keys;  /* (i << 32 | j) + 1, 0 = empty */
-    uint64_t* vals;
+    uint64_t key;    /* triangle index + 1, 0 = empty */
+    uint64_t val;
+} pcslot;
+typedef struct {
+    pthread_mutex_t lock;
+    pcslot* s;       /* key and count in one slot: one cache miss per probe */
     size_t cap, len;
-} pcmap;
+} __attribute__((aligned(64))) pcmap;  /* one stripe per cache line: no false sharing */
 
 #define PC_STRIPES 64
 static inline unsigned pc_stripe(uint64_t key) { return (unsigned)((key * 0xD6E8FEB86659FD93ull) >> 58); }
@@ -57,18 +61,20 @@ struct shd_topology {
     int32_t na;
     int32_t* A;
     int32_t* cid;
-    double* lat;
-    double* rel;
+    double* lr;          /* (lat, rel) pairs: one cache line serves both getters */
+    uint32_t* cnt;       /* packet counters per pair (calloc: pages commit on first touch);
+                          * each 2^32 wrap adds 2^32 to the striped spill map pc */
     int filled;
     double min_lat;
     double fill_seconds;
     pthread_mutex_t lock;
-    /* packet counters: a sparse map striped over PC_STRIPES locks, so worker threads
-     * counting packets on different paths rarely meet (path.c:57-60 has no lock) */
+    /* spill map for counters past 2^32, striped over PC_STRIPES locks */
     pcmap pc[PC_STRIPES];
-    pthread_mutex_t pclock[PC_STRIPES];
     shd_attach_t* at;    /* host attachment index (graphml topologies only) */
 };
+
+#define LAT(t, k) ((t)->lr[2 * (size_t)(k)])
+#define REL(t, k) ((t)->lr[2 * (size_t)(k) + 1])
 
 static inline size_t tri(int32_t na, int32_t i, int32_t j) { /* i <= j */
     return (size_t)i * (size_t)na - ((size_t)i * (size_t)(i - 1)) / 2 + (size_t)(j - i);
@@ -133,12 +139,20 @@ static shd_topology_t* finish_new(shd_topology_t* t, const int* devices, int nde
     for (int32_t v = 0; v < t->n; v++) t->cid[v] = -1;
     build_adjacency(t);
     pthread_mutex_init(&t->lock, NULL);
-    for (int k = 0; k < PC_STRIPES; k++) pthread_mutex_init(&t->pclock[k], NULL);
+    for (int k = 0; k < PC_STRIPES; k++) pthread_mutex_init(&t->pc[k].lock, NULL);
+    return t;
+}
+
+/* the counter stripes are cache-line aligned: allocate the struct that way */
+static shd_topology_t* alloc_top(void) {
+    const size_t sz = (sizeof(shd_topology_t) + 63) & ~(size_t)63;
+    shd_topology_t* t = aligned_alloc(64, sz);
+    if (t) memset(t, 0, sz);
     return t;
 }
 
 shd_topology_t* shd_topology_new(const char* graph_path, const int* devices, int ndev) {
-    shd_topology_t* t = calloc(1, sizeof(*t));
+    shd_topology_t* t = alloc_top();
     char err[512];
     if (shd_graphml_load(graph_path, &t->gml, err, sizeof(err)) != SHD_ROUTE_OK) {
         fprintf(stderr, "shd_topology_new: %s\n", err);
@@ -152,7 +166,7 @@ shd_topology_t* shd_topology_new(const char* graph_path, const int* devices, int
 
 shd_topology_t* shd_topology_new_from_graph(const shd_graph_t* g, const int* devices, int ndev) {
     if (!g || g->n_vertices <= 0) return NULL;
-    shd_topology_t* t = calloc(1, sizeof(*t));
+    shd_topology_t* t = alloc_top();
     t->owns_copy = 1;
     t->g = *g;
     size_t m = (size_t)g->n_edges, n = (size_t)g->n_vertices;
@@ -182,8 +196,8 @@ void shd_topology_free(shd_topology_t* t) {
     shd_attach_destroy(t->at);
     shd_graphml_free(&t->gml);
     free(t->arow); free(t->acol); free(t->attached); free(t->A); free(t->cid);
-    free(t->lat); free(t->rel);
-    for (int k = 0; k < PC_STRIPES; k++) { free(t->pc[k].keys); free(t->pc[k].vals); }
+    free(t->lr); free(t->cnt);
+    for (int k = 0; k < PC_STRIPES; k++) { pthread_mutex_destroy(&t->pc[k].lock); free(t->pc[k].s); }
     free(t);
 }
 
@@ -256,8 +270,10 @@ static void* fill_worker(void* arg) {
             const int32_t i = i0 + r;
             const size_t base = tri(na, i, i);
             /* row i stores targets j >= i: offsets (j - i0) in the returned row */
-            memcpy(t->lat + base, lbuf + (size_t)r * nt + r, sizeof(double) * (size_t)(na - i));
-            memcpy(t->rel + base, rbuf + (size_t)r * nt + r, sizeof(double) * (size_t)(na - i));
+            const double* lr_ = lbuf + (size_t)r * nt + r;
+            const double* rr_ = rbuf + (size_t)r * nt + r;
+            double* o = t->lr + 2 * base;
+            for (int32_t q = 0; q < na - i; q++) { o[2 * q] = lr_[q]; o[2 * q + 1] = rr_[q]; }
         }
     }
     free(lbuf); free(rbuf);
@@ -273,8 +289,15 @@ static double now_s(void) {
 static int fill_locked(shd_topology_t* t) {
     if (t->filled) return SHD_ROUTE_OK;
     const double t0 = now_s();
-    free(t->A); free(t->lat); free(t->rel);
-    t->A = NULL; t->lat = t->rel = NULL;
+    free(t->A); free(t->lr); free(t->cnt);
+    t->A = NULL; t->lr = NULL; t->cnt = NULL;
+    /* a refill renumbers the pairs: counters restart (Shadow attaches every host before
+     * the first packet, so this only happens in tests) */
+    for (int k = 0; k < PC_STRIPES; k++) {
+        pthread_mutex_lock(&t->pc[k].lock);
+        free(t->pc[k].s); t->pc[k].s = NULL; t->pc[k].cap = t->pc[k].len = 0;
+        pthread_mutex_unlock(&t->pc[k].lock);
+    }
     t->na = 0;
     t->A = malloc(sizeof(int32_t) * ((size_t)t->nattached + 1));
     for (int32_t v = 0; v < t->n; v++) {
@@ -282,9 +305,9 @@ static int fill_locked(shd_topology_t* t) {
         if (t->attached[v]) { t->cid[v] = t->na; t->A[t->na++] = v; }
     }
     const size_t ntri = (size_t)t->na * ((size_t)t->na + 1) / 2;
-    t->lat = malloc(sizeof(double) * (ntri ? ntri : 1));
-    t->rel = malloc(sizeof(double) * (ntri ? ntri : 1));
-    if (!t->lat || !t->rel) return SHD_ROUTE_ENOMEM;
+    t->lr = malloc(2 * sizeof(double) * (ntri ? ntri : 1));
+    t->cnt = calloc(ntri ? ntri : 1, sizeof(uint32_t));
+    if (!t->lr || !t->cnt) return SHD_ROUTE_ENOMEM;
     int rc = SHD_ROUTE_OK;
     if (t->na) {
         pthread_t th[64];
@@ -307,7 +330,7 @@ static int fill_locked(shd_topology_t* t) {
         int32_t nself = 0;
         int32_t* sv = malloc(sizeof(int32_t) * ((size_t)t->na + 1));
         for (int32_t i = 0; i < t->na; i++)
-            if (isnan(t->lat[tri(t->na, i, i)])) sv[nself++] = t->A[i];
+            if (isnan(LAT(t, tri(t->na, i, i)))) sv[nself++] = t->A[i];
         if (nself) {
             double* sl = malloc(sizeof(double) * (size_t)nself);
             double* sr = malloc(sizeof(double) * (size_t)nself);
@@ -315,8 +338,8 @@ static int fill_locked(shd_topology_t* t) {
             if (rc == SHD_ROUTE_ENOEDGE) rc = SHD_ROUTE_OK;  /* no out-edge: stays unstored */
             for (int32_t q = 0; q < nself && !rc; q++) {
                 const size_t k = tri(t->na, t->cid[sv[q]], t->cid[sv[q]]);
-                t->lat[k] = sl[q];
-                t->rel[k] = sr[q];
+                LAT(t, k) = sl[q];
+                REL(t, k) = sr[q];
             }
             free(sl); free(sr);
         }
@@ -325,7 +348,7 @@ static int fill_locked(shd_topology_t* t) {
     }
     double mn = 0;
     for (size_t k = 0; k < ntri; k++)  /* topology.c:1375: minLat == 0 means unset */
-        if (!isnan(t->lat[k]) && (mn == 0 || t->lat[k] < mn)) mn = t->lat[k];
+        if (!isnan(LAT(t, k)) && (mn == 0 || LAT(t, k) < mn)) mn = LAT(t, k);
     t->min_lat = mn;
     t->fill_seconds += now_s() - t0;
     __atomic_store_n(&t->filled, 1, __ATOMIC_RELEASE);
@@ -353,17 +376,17 @@ static int64_t entry(shd_topology_t* t, int32_t s, int32_t d) {
     const int32_t i = t->cid[s], j = t->cid[d];
     if (i < 0 || j < 0) return -1;  /* address not connected to the topology */
     const int64_t k = (int64_t)(i <= j ? tri(t->na, i, j) : tri(t->na, j, i));
-    return isnan(t->lat[k]) ? -1 : k;  /* never stored (topology.c:2040-2046) */
+    return isnan(LAT(t, k)) ? -1 : k;  /* never stored (topology.c:2040-2046) */
 }
 
 double shd_topology_get_latency(shd_topology_t* t, int32_t s, int32_t d) {
     int64_t k = entry(t, s, d);
-    return k < 0 ? -1.0 : t->lat[k];
+    return k < 0 ? -1.0 : LAT(t, k);
 }
 
 double shd_topology_get_reliability(shd_topology_t* t, int32_t s, int32_t d) {
     int64_t k = entry(t, s, d);
-    return k < 0 ? -1.0 : t->rel[k];
+    return k < 0 ? -1.0 : REL(t, k);
 }
 
 int shd_topology_is_routable(shd_topology_t* t, int32_t s, int32_t d) {
@@ -379,52 +402,54 @@ int shd_topology_is_direct_path(shd_topology_t* t, int32_t s, int32_t d) {
 static uint64_t* pc_slot(pcmap* m, uint64_t key) {
     if (m->len * 2 + 2 > m->cap) {
         size_t nc = m->cap ? m->cap * 2 : 4096;
-        uint64_t* nk = calloc(nc, sizeof(uint64_t));
-        uint64_t* nv = calloc(nc, sizeof(uint64_t));
+        pcslot* ns = calloc(nc, sizeof(pcslot));
         for (size_t i = 0; i < m->cap; i++)
-            if (m->keys[i]) {
-                size_t j = (m->keys[i] * 0x9E3779B97F4A7C15ull) & (nc - 1);
-                while (nk[j]) j = (j + 1) & (nc - 1);
-                nk[j] = m->keys[i]; nv[j] = m->vals[i];
+            if (m->s[i].key) {
+                size_t j = (m->s[i].key * 0x9E3779B97F4A7C15ull) & (nc - 1);
+                while (ns[j].key) j = (j + 1) & (nc - 1);
+                ns[j] = m->s[i];
             }
-        free(m->keys); free(m->vals);
-        m->keys = nk; m->vals = nv; m->cap = nc;
+        free(m->s);
+        m->s = ns; m->cap = nc;
     }
     size_t j = (key * 0x9E3779B97F4A7C15ull) & (m->cap - 1);
-    while (m->keys[j] && m->keys[j] != key) j = (j + 1) & (m->cap - 1);
-    if (!m->keys[j]) { m->keys[j] = key; m->len++; }
-    return &m->vals[j];
+    while (m->s[j].key && m->s[j].key != key) j = (j + 1) & (m->cap - 1);
+    if (!m->s[j].key) { m->s[j].key = key; m->len++; }
+    return &m->s[j].val;
 }
 
 /* read without inserting */
 static uint64_t pc_get(shd_topology_t* t, uint64_t key) {
     const unsigned st = pc_stripe(key);
     uint64_t v = 0;
-    pthread_mutex_lock(&t->pclock[st]);
-    const pcmap* m = &t->pc[st];
+    pcmap* m = &t->pc[st];
+    pthread_mutex_lock(&m->lock);
     if (m->cap) {
         size_t j = (key * 0x9E3779B97F4A7C15ull) & (m->cap - 1);
-        while (m->keys[j] && m->keys[j] != key) j = (j + 1) & (m->cap - 1);
-        if (m->keys[j]) v = m->vals[j];
+        while (m->s[j].key && m->s[j].key != key) j = (j + 1) & (m->cap - 1);
+        if (m->s[j].key) v = m->s[j].val;
     }
-    pthread_mutex_unlock(&t->pclock[st]);
+    pthread_mutex_unlock(&m->lock);
     return v;
 }
 
 void shd_topology_increment_path_packet_counter(shd_topology_t* t, int32_t s, int32_t d) {
     int64_t k = entry(t, s, d);
     if (k < 0) return;
+    /* path_incrementPacketCount (path.c:57-60) without its data race: one relaxed
+     * atomic add on the pair's own counter, no lock */
+    if (__atomic_fetch_add(&t->cnt[k], 1u, __ATOMIC_RELAXED) != UINT32_MAX) return;
     const uint64_t key = (uint64_t)k + 1;
     const unsigned st = pc_stripe(key);
-    pthread_mutex_lock(&t->pclock[st]);
-    (*pc_slot(&t->pc[st], key))++;
-    pthread_mutex_unlock(&t->pclock[st]);
+    pthread_mutex_lock(&t->pc[st].lock);
+    *pc_slot(&t->pc[st], key) += 1ull << 32;
+    pthread_mutex_unlock(&t->pc[st].lock);
 }
 
 uint64_t shd_topology_get_path_packet_count(shd_topology_t* t, int32_t s, int32_t d) {
     int64_t k = entry(t, s, d);
     if (k < 0) return 0;
-    return pc_get(t, (uint64_t)k + 1);
+    return pc_get(t, (uint64_t)k + 1) + __atomic_load_n(&t->cnt[k], __ATOMIC_RELAXED);
 }
 
 double shd_topology_min_path_latency(shd_topology_t* t) {
@@ -452,11 +477,11 @@ int shd_topology_dump_paths(shd_topology_t* t, FILE* out) {
             char na_[32], nb_[32];
             if (!ia) { snprintf(na_, sizeof na_, "%d", a); ia = na_; }
             if (!ib) { snprintf(nb_, sizeof nb_, "%d", b); ib = nb_; }
-            const uint64_t pc = pc_get(t, (uint64_t)k + 1);
+            const uint64_t pc = pc_get(t, (uint64_t)k + 1) + __atomic_load_n(&t->cnt[k], __ATOMIC_RELAXED);
             /* path_toString (path.c:62-74) inside _topology_logAllCachedPathsHelper2 */
             fprintf(out, "Found path %s%s%s in cache: SourceIndex=%d DestinationIndex=%d Latency=%f "
                          "Reliability=%f PacketCount=%llu isDirect=%s\n",
-                    ia, t->directed ? "->" : "<->", ib, a, b, t->lat[k], t->rel[k], (unsigned long long)pc,
+                    ia, t->directed ? "->" : "<->", ib, a, b, LAT(t, k), REL(t, k), (unsigned long long)pc,
                     (t->complete || (t->prefer_direct && adjacent(t, a, b))) ? "True" : "False");
         }
     return SHD_ROUTE_OK;

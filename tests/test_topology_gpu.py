@@ -91,6 +91,30 @@ def test_unattached_and_counters(topo):
     assert t.get_latency(1, 2) > 0
 
 
+def test_counters_concurrent(topo):
+    """Worker threads count packets at once (worker.c:279 from every worker): the per-pair
+    atomic counters lose nothing, either orientation lands on the same Path."""
+    import threading
+    g = internet_like(40, 2, seed=9)
+    t = topo.Topology.from_graph(g)
+    t.attach_all(range(g.n))
+    pairs = [(a, b) for a in range(0, 40, 7) for b in range(0, 40, 5)]
+    def work(seed):
+        for k in range(4000):
+            a, b = pairs[(seed * 31 + k) % len(pairs)]
+            t.increment_path_packet_counter(a, b) if k & 1 else t.increment_path_packet_counter(b, a)
+    th = [threading.Thread(target=work, args=(i,)) for i in range(8)]
+    [x.start() for x in th]; [x.join() for x in th]
+    want = {}
+    for i in range(8):
+        for k in range(4000):
+            a, b = pairs[(i * 31 + k) % len(pairs)]
+            key = (min(a, b), max(a, b))
+            want[key] = want.get(key, 0) + 1
+    for (a, b), c in want.items():
+        assert t.packet_count(a, b) == c and t.packet_count(b, a) == c
+
+
 def test_multi_context_fill_equals_single(topo):
     g = config("c2")
     A = np.arange(0, g.n, 3)

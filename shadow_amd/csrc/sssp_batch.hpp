@@ -203,7 +203,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
                                                               uint32_t* __restrict__ keys, long long kld,
                                                               int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    int* changed = reinterpret_cast<int*>(smem);
+    int* flags = reinterpret_cast<int*>(smem);  // three rotating sweep flags (see KBF)
     const KBLayout L = KBLayout::make(g.n, g.nnz, g.npart);
     char* base = smem + kKBSmall;
     uint32_t* arc = reinterpret_cast<uint32_t*>(base + L.arc);
@@ -241,14 +241,15 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
                 if (sb[b] == v) d.h[b >> 1][b & 1] = 0;
             st8(D + (size_t)16 * v, d);
         }
+        if (tid == 0) flags[0] = 0;
         __syncthreads();
 
         if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memtime();
         // ---- Gauss-Seidel pull sweeps to the fixed point -------------------------
-        for (;;) {
+        for (int fi = 0;; fi = fi == 2 ? 0 : fi + 1) {
             KB_COUNT(4);
-            if (tid == 0) *changed = 0;
-            __syncthreads();
+            if (tid == 0) flags[fi == 2 ? 0 : fi + 1] = 0;
+            int* changed = flags + fi;
             int ch = 0;
             for (int k = tid; k < g.nseg; k += KB_BLOCK) {
                 const KBSeg sg = g.seg[k];
@@ -271,9 +272,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
             }
             if (ch) *changed = 1;
             __syncthreads();
-            const int again = *changed;
-            __syncthreads();
-            if (!again) break;
+            if (!*changed) break;
         }
 
         if (tid == 0 && g.dbg) g.dbg[(size_t)blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memtime();

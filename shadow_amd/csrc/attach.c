@@ -22,8 +22,8 @@
  *     2218-2243), over every candidate including those without an IP (INADDR_NONE);
  *   - otherwise one random_nextDouble draw picks element round((len-1) * d) in list
  *     order (topology.c:2333-2339).
- * What changes: the per-vertex strings are parsed and case-folded once into integers
- * (IP values, 64-bit hashes confirmed by a string compare), and the lists are counted
+ * What changes: the per-vertex strings are parsed and interned case-folded once into
+ * integers (IP values, dictionary ids per attribute), and the lists are counted
  * in one pass and materialised for the chosen list only, instead of 8 GQueues filled
  * through 5 igraph attribute lookups per vertex per host under the graph lock.
  */
@@ -44,8 +44,12 @@ struct shd_attach {
     int has_ip;
     uint32_t* ip;        /* inet_pton value (network order) of the ip string, INADDR_NONE if none */
     uint8_t* ip_usable;  /* found and not NONE / ANY / LOOPBACK (as compared at topology.c:2126) */
-    uint64_t* h[4];      /* case-folded hash of citycode, countrycode, geocode, type; 0 = not found */
-    char** s[4];         /* the strings themselves (views into a private copy) */
+    /* citycode, countrycode, geocode, type interned case-folded: id[k][v] in 1..nid[k],
+     * 0 = not found / empty; dictionary str[k][id] (folded) with hashes hs[k][id] */
+    uint32_t* id[4];
+    uint32_t nid[4];
+    char** str[4];
+    uint64_t* hs[4];
 };
 
 static int fold(int c) { return (c >= 'A' && c <= 'Z') ? c + ('a' - 'A') : c; }
@@ -69,6 +73,15 @@ static int ip_usable(uint32_t ip) {
     return ip != (uint32_t)INADDR_NONE && ip != (uint32_t)INADDR_ANY && ip != (uint32_t)INADDR_LOOPBACK;
 }
 
+/* id of the case-folded string x among attribute k's values, 0 if absent (the
+ * dictionaries are small: a few hundred codes) */
+static uint32_t intern_find(const shd_attach_t* a, int k, const char* x) {
+    const uint64_t h = fold_hash(x);
+    for (uint32_t i = 1; i <= a->nid[k]; i++)
+        if (a->hs[k][i] == h && ascii_caseeq(a->str[k][i], x)) return i;
+    return 0;
+}
+
 int shd_attach_create(shd_attach_t** out, const shd_graphml_t* g) {
     if (!out || !g || g->graph.n_vertices <= 0) return SHD_ROUTE_EINVAL;
     shd_attach_t* a = calloc(1, sizeof(*a));
@@ -84,14 +97,21 @@ int shd_attach_create(shd_attach_t** out, const shd_graphml_t* g) {
     }
     const int slot[4] = {SHD_VATTR_CITYCODE, SHD_VATTR_COUNTRYCODE, SHD_VATTR_GEOCODE, SHD_VATTR_TYPE};
     for (int k = 0; k < 4; k++) {
-        a->h[k] = calloc((size_t)n, sizeof(uint64_t));
-        a->s[k] = calloc((size_t)n, sizeof(char*));
+        a->id[k] = calloc((size_t)n, sizeof(uint32_t));
+        a->str[k] = calloc((size_t)n + 1, sizeof(char*));
+        a->hs[k] = calloc((size_t)n + 1, sizeof(uint64_t));
         const int has = g->has_vertex_str[slot[k]] && g->vertex_str[slot[k]];
         for (int32_t v = 0; v < n && has; v++) {
-            const char* s = g->vertex_str[slot[k]][v];
-            if (s && s[0]) {
-                a->s[k][v] = strdup(s);
-                a->h[k][v] = fold_hash(s);
+            const char* x = g->vertex_str[slot[k]][v];
+            if (x && x[0]) {
+                uint32_t i = intern_find(a, k, x);
+                if (!i) {
+                    i = ++a->nid[k];
+                    a->str[k][i] = strdup(x);
+                    for (char* c = a->str[k][i]; *c; c++) *c = (char)fold((unsigned char)*c);
+                    a->hs[k][i] = fold_hash(x);
+                }
+                a->id[k][v] = i;
             }
         }
     }
@@ -102,24 +122,22 @@ int shd_attach_create(shd_attach_t** out, const shd_graphml_t* g) {
 void shd_attach_destroy(shd_attach_t* a) {
     if (!a) return;
     for (int k = 0; k < 4; k++) {
-        if (a->s[k]) for (int32_t v = 0; v < a->n; v++) free(a->s[k][v]);
-        free(a->s[k]);
-        free(a->h[k]);
+        if (a->str[k]) for (uint32_t i = 1; i <= a->nid[k]; i++) free(a->str[k][i]);
+        free(a->str[k]);
+        free(a->hs[k]);
+        free(a->id[k]);
     }
     free(a->ip);
     free(a->ip_usable);
     free(a);
 }
 
-/* list membership bits of vertex v (bit L_*) for the given hints */
-static unsigned lists_of(const shd_attach_t* a, int32_t v, const uint64_t hh[4], const char* const hs[4]) {
-    int m[4];
-    for (int k = 0; k < 4; k++)
-        m[k] = hh[k] && a->h[k][v] == hh[k] && ascii_caseeq(a->s[k][v], hs[k]);
-    const int city = m[0], country = m[1], geo = m[2], type = m[3];
-    return (city && type ? 1u << L_CITY_TYPE : 0u) | (city ? 1u << L_CITY : 0u) |
-           (country && type ? 1u << L_COUNTRY_TYPE : 0u) | (country ? 1u << L_COUNTRY : 0u) |
-           (geo && type ? 1u << L_GEO_TYPE : 0u) | (geo ? 1u << L_GEO : 0u) | (type ? 1u << L_TYPE : 0u) |
+/* list membership bits of vertex v (bit L_*) for the interned hint ids */
+static inline unsigned lists_of(const shd_attach_t* a, int32_t v, const uint32_t hid[4]) {
+    const unsigned city = a->id[0][v] == hid[0], country = a->id[1][v] == hid[1];
+    const unsigned geo = a->id[2][v] == hid[2], type = a->id[3][v] == hid[3];
+    return ((city & type) << L_CITY_TYPE) | (city << L_CITY) | ((country & type) << L_COUNTRY_TYPE) |
+           (country << L_COUNTRY) | ((geo & type) << L_GEO_TYPE) | (geo << L_GEO) | (type << L_TYPE) |
            (1u << L_ALL);
 }
 
@@ -135,18 +153,27 @@ int32_t shd_attach_find_vertex(const shd_attach_t* a, shd_next_double_fn next_do
         const uint32_t ip = str_to_ip(ip_hint);
         if (ip_usable(ip)) { req = ip; req_usable = 1; }
     }
-    const char* hs[4] = {citycode_hint, countrycode_hint, geocode_hint, type_hint};
-    uint64_t hh[4];
-    for (int k = 0; k < 4; k++) hh[k] = hs[k] ? fold_hash(hs[k]) : 0;
+    /* a hint matches the vertices holding its interned id; an absent, empty or unknown
+     * hint matches none (UINT32_MAX is never an id) */
+    const char* hint[4] = {citycode_hint, countrycode_hint, geocode_hint, type_hint};
+    uint32_t hid[4];
+    for (int k = 0; k < 4; k++) {
+        const uint32_t i = (hint[k] && hint[k][0]) ? intern_find(a, k, hint[k]) : 0;
+        hid[k] = i ? i : UINT32_MAX;
+    }
 
     /* pass 1: exact IP matches, else per-list sizes and usable-IP counts */
     int32_t cnt[L_N] = {0}, nip[L_N] = {0}, nexact = 0;
     for (int32_t v = 0; v < n; v++) {
         if (req_usable && a->ip_usable[v] && a->ip[v] == req) { nexact++; continue; }
         if (nexact) continue;  /* after the first exact match only exact matches count */
-        const unsigned m = lists_of(a, v, hh, hs);
-        for (int l = 0; l < L_N; l++)
-            if (m & (1u << l)) { cnt[l]++; nip[l] += a->ip_usable[v]; }
+        const unsigned m = lists_of(a, v, hid);
+        const int32_t u = a->ip_usable[v];
+        for (int l = 0; l < L_N; l++) {
+            const int32_t in = (int32_t)((m >> l) & 1u);
+            cnt[l] += in;
+            nip[l] += in & u;
+        }
     }
     int list = L_ALL, lpm = 0;
     int32_t len;
@@ -164,7 +191,7 @@ int32_t shd_attach_find_vertex(const shd_attach_t* a, shd_next_double_fn next_do
         /* _topology_getLongestPrefixMatch over the list in order (topology.c:2218-2243) */
         uint32_t best = 0;
         for (int32_t v = 0; v < n; v++) {
-            if (!(lists_of(a, v, hh, hs) & (1u << list))) continue;
+            if (!(lists_of(a, v, hid) & (1u << list))) continue;
             const uint32_t match = ~(a->ip[v] ^ req);
             if (match > best || best == 0) { best = match; pick = v; }
         }
@@ -178,7 +205,7 @@ int32_t shd_attach_find_vertex(const shd_attach_t* a, shd_next_double_fn next_do
     if (k > range) k = range;
     for (int32_t v = 0, seen = 0; v < n; v++) {
         const int in = nexact ? (req_usable && a->ip_usable[v] && a->ip[v] == req)
-                              : ((lists_of(a, v, hh, hs) >> list) & 1u);
+                              : ((lists_of(a, v, hid) >> list) & 1u);
         if (in && seen++ == k) { pick = v; break; }
     }
     return pick;

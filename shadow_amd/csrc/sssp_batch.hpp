@@ -142,6 +142,19 @@ __device__ inline u16x8 addsat8(const u16x8& a, us2 w) {
     return r;
 }
 
+// min over hub partials [p0, p1): four independent LDS reads in flight (a hub row of
+// 11 segments was 11 dependent round trips at the end of every sweep)
+__device__ inline u16x8 min_parts(const char* P, int p0, int p1, u16x8 acc) {
+    int p = p0;
+    for (; p + 4 <= p1; p += 4) {
+        const u16x8 x0 = ld8(P + (size_t)16 * p), x1 = ld8(P + (size_t)16 * (p + 1));
+        const u16x8 x2 = ld8(P + (size_t)16 * (p + 2)), x3 = ld8(P + (size_t)16 * (p + 3));
+        acc = min8(acc, min8(min8(x0, x1), min8(x2, x3)));
+    }
+    for (; p < p1; p++) acc = min8(acc, ld8(P + (size_t)16 * p));
+    return acc;
+}
+
 // arc weight as a u16 pair: low 16 bits (u << 16 | w), or the low byte of the fused
 // record (u << 16 | ridx << 8 | w)
 template <bool kFused>
@@ -267,7 +280,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
                 const KBHub h = g.hub[k];
                 u16x8 acc = ld8(D + (size_t)16 * h.v);
                 const u16x8 old = acc;
-                for (int p = h.p0; p < h.p1; p++) acc = min8(acc, ld8(P + (size_t)16 * p));
+                acc = min_parts(P, h.p0, h.p1, acc);
                 if (!eq8(acc, old)) { st8(D + (size_t)16 * h.v, acc); ch = 1; }
             }
             if (ch) *changed = 1;
@@ -306,7 +319,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_kernel(DevKB g, const int
             const KBHub h = g.hub[k];
             const u16x8 dv = ld8(D + (size_t)16 * h.v);
             u16x8 acc = inf8();
-            for (int p = h.p0; p < h.p1; p++) acc = min8(acc, ld8(P + (size_t)16 * p));
+            acc = min_parts(P, h.p0, h.p1, acc);
 #pragma unroll
             for (int b = 0; b < KB_SRC; b++) {
                 if (sb[b] < 0) continue;
@@ -449,7 +462,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
             if (hv >= 0) {
                 u16x8 acc = ld8(D + (size_t)16 * hv);
                 const u16x8 old = acc;
-                for (int p = (int)(hp & 0xFFFFu); p < (int)(hp >> 16); p++) acc = min8(acc, ld8(P + (size_t)16 * p));
+                acc = min_parts(P, (int)(hp & 0xFFFFu), (int)(hp >> 16), acc);
                 if (!eq8(acc, old)) { st8(D + (size_t)16 * hv, acc); ch = 1; }
             }
             if (ch) *changed = 1;
@@ -480,7 +493,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
         __syncthreads();
         if (hv >= 0) {
             u16x8 acc = inf8();
-            for (int p = (int)(hp & 0xFFFFu); p < (int)(hp >> 16); p++) acc = min8(acc, ld8(P + (size_t)16 * p));
+            acc = min_parts(P, (int)(hp & 0xFFFFu), (int)(hp >> 16), acc);
 #pragma unroll
             for (int b = 0; b < KB_SRC; b++) sl[b * n + hv] = acc.h[b >> 1][b & 1];
         }

@@ -594,7 +594,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
                     for (int q = 0; q < KB_WQ; q++) pk[q][nb] = acc[q];
                 }
                 KBT_MARK(t_b);
-                const int kmax = 4 * nb;
+                [[maybe_unused]] const int kmax = 4 * nb;  // stamps only
                 // fold source-first: the last arc walked is the first factor
                 double rr[KB_WQ];
 #pragma unroll

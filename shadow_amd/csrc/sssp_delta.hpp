@@ -328,7 +328,6 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
     uint2* rrec = reinterpret_cast<uint2*>(smem + L.rrec);
     uint16_t* qv = reinterpret_cast<uint16_t*>(smem + L.qv);
     int* qbeg = reinterpret_cast<int*>(smem + L.qbeg);
-    const unsigned bound = (unsigned)g.bound;
     const unsigned delta = (unsigned)g.delta;
     const int qcap = L.qcap;
     const unsigned wmask = g.packed ? 0xFFu : 0xFFFFu;

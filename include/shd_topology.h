@@ -65,9 +65,10 @@ int32_t shd_topology_attached_count(const shd_topology_t* top);
 
 /* Host attachment: _topology_findAttachmentVertex (topology.c:2245-2366) with its
  * per-vertex filter hook (topology.c:2094-2216) and longest-prefix match
- * (topology.c:2218-2243).  The index precomputes each vertex's parsed IP and
- * case-folded code hashes once, so a lookup is two linear passes of integer compares
- * instead of 5 igraph string-attribute lookups per vertex.  Hints may be NULL.
+ * (topology.c:2218-2243).  The index interns each vertex's parsed IP and case-folded
+ * codes once, with posting lists per code and sorted IPs, so a lookup touches only the
+ * candidates of the chosen list instead of making 5 igraph string-attribute lookups
+ * per vertex.  Hints may be NULL.
  * next_double(ctx) is called exactly where the reference calls
  * random_nextDouble(randomSourcePool) (one draw, only when no longest-prefix match is
  * used), so a caller passing Shadow's Random keeps its stream bit for bit.

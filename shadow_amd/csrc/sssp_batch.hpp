@@ -186,12 +186,15 @@ __device__ inline u16x8 relax_row(const uint32_t* arc, const char* D, int a0, in
 }
 
 // first tight arc of in-arcs [a0, a1) for each of the batch's sources: slot (a - r0) or
-// 0xFFFF when none (or when the vertex is unreached for that source)
+// 0xFFFF when none (or when the vertex is unreached for that source).  Packed: per arc
+// and u16 pair, x = c ^ dv is 0 where tight; min(x, 1) * 0xFFFF is 0 there and 0xFFFF
+// elsewhere; max with the arc's slot and a running min keep the first tight slot (arcs
+// ascend) -- 5 packed ops per pair instead of 8 scalar compare/selects per arc.
 template <bool kFused>
 __device__ inline void first_tight(const uint32_t* arc, const char* D, int a0, int a1, int r0,
                                    const u16x8& dv, unsigned short (&slot)[KB_SRC]) {
-#pragma unroll
-    for (int b = 0; b < KB_SRC; b++) slot[b] = 0xFFFFu;
+    u16x8 sl = inf8();
+    const us2 one = {1, 1}, ffff = {0xFFFF, 0xFFFF};
     for (int a = a0; a < a1; a += 4) {
         u16x8 c[4];
 #pragma unroll
@@ -202,12 +205,21 @@ __device__ inline void first_tight(const uint32_t* arc, const char* D, int a0, i
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             if (a + q >= a1) break;
+            const unsigned short idx = (unsigned short)(a + q - r0);
+            const us2 iv = {idx, idx};
 #pragma unroll
-            for (int b = 0; b < KB_SRC; b++) {
-                const unsigned short cb = c[q].h[b >> 1][b & 1], db = dv.h[b >> 1][b & 1];
-                if (slot[b] == 0xFFFFu && db != 0xFFFFu && cb == db) slot[b] = (unsigned short)(a + q - r0);
+            for (int k = 0; k < 4; k++) {
+                const us2 x = __builtin_bit_cast(
+                    us2, __builtin_bit_cast(uint32_t, c[q].h[k]) ^ __builtin_bit_cast(uint32_t, dv.h[k]));
+                const us2 cand = __builtin_elementwise_max(__builtin_elementwise_min(x, one) * ffff, iv);
+                sl.h[k] = __builtin_elementwise_min(sl.h[k], cand);
             }
         }
+    }
+#pragma unroll
+    for (int b = 0; b < KB_SRC; b++) {
+        const unsigned short db = dv.h[b >> 1][b & 1];
+        slot[b] = db == 0xFFFFu ? (unsigned short)0xFFFFu : sl.h[b >> 1][b & 1];
     }
 }
 

@@ -85,6 +85,42 @@ def test_attach_matches_restatement(topo, tmp_path, seed, n, default_city, decla
     idx.close()
 
 
+def test_attach_many_distinct_codes(topo, tmp_path):
+    """Every vertex with its own geocode and most with their own citycode (the interning
+    table at its fullest), hints drawn from those codes in mixed case."""
+    n = 500
+    rng = random.Random(77)
+    keys = ''.join(f'<key attr.name="{a}" attr.type="string" for="node" id="{a}" />'
+                   for a in ("ip", "citycode", "geocode", "type"))
+    keys += ('<key attr.name="latency" attr.type="double" for="edge" id="el" />'
+             '<key attr.name="packetloss" attr.type="double" for="edge" id="ep" />'
+             '<key attr.name="bandwidthup" attr.type="int" for="node" id="bu" />'
+             '<key attr.name="bandwidthdown" attr.type="int" for="node" id="bd" />')
+    city = [f"c{rng.randrange(400)}" for _ in range(n)]
+    nodes = "".join(f'<node id="v{v}"><data key="bd">1</data><data key="bu">1</data>'
+                    f'<data key="ip">11.{v % 7}.{v % 5}.{v % 250}</data><data key="citycode">{city[v]}</data>'
+                    f'<data key="geocode">g{v}</data><data key="type">{rng.choice(TYPES)}</data></node>'
+                    for v in range(n))
+    edges = "".join(f'<edge source="v{v}" target="v{(v + 1) % n}"><data key="el">1</data><data key="ep">0</data></edge>'
+                    for v in range(n))
+    p = tmp_path / "many.xml"
+    p.write_text(f'<graphml xmlns="http://graphml.graphdrawing.org/xmlns">{keys}<graph edgedefault="undirected">'
+                 f'{nodes}{edges}</graph></graphml>')
+    idx = topo.AttachIndex(str(p))
+    attrs = idx.vertex_attrs()
+    for trial in range(300):
+        v = rng.randrange(n)
+        h = {"citycode": rng.choice([city[v], city[v].upper(), "nowhere", None]),
+             "geocode": rng.choice([f"G{v}", f"g{rng.randrange(n)}", None]),
+             "type": rng.choice(TYPES + [None]),
+             "ip": rng.choice([None, f"11.{v % 7}.{v % 5}.{v % 250}", f"11.{v % 7}.9.9"])}
+        r1, r2 = ShadowRandom(trial), ShadowRandom(trial)
+        want = find_attachment_vertex(attrs, n, r2, ip_hint=h["ip"], citycode_hint=h["citycode"],
+                                      geocode_hint=h["geocode"], type_hint=h["type"])
+        assert idx.find(r1.next_double, **h) == want and r1.draws == r2.draws, (trial, h)
+    idx.close()
+
+
 def test_attach_reference_configs_one_vertex(topo, tmp_path):
     """Every host of the reference's test/example configs joins vertex 0 (1-vertex graphs,
     e.g. src/test/tcp/tcp-blocking-lossy.test.shadow.config.xml with countrycode US)."""

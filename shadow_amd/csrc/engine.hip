@@ -439,6 +439,42 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
         // equal-length segments side by side: a wave's lanes finish their rows together
         std::stable_sort(segs.begin(), segs.end(),
                          [](const KBSeg& x, const KBSeg& y) { return (x.a1 - x.a0) > (y.a1 - y.a0); });
+        // thread t takes segments t, t + KB_BLOCK, ...: a sweep lasts as long as the wave
+        // whose lanes' longest segments add up most.  Each block of KB_BLOCK segments may
+        // run long->short or short->long over the threads; pick the directions with the
+        // smallest such wave time (C2: 29 -> 22 arc steps; the mean is 20)
+        {
+            const int nb = ((int)segs.size() + KB_BLOCK - 1) / KB_BLOCK;
+            constexpr int kWaves = KB_BLOCK / 64;
+            auto cost = [&](unsigned dirs) {
+                int wt[kWaves] = {0};
+                for (int b = 0; b < nb; b++) {
+                    const int k0 = b * KB_BLOCK, cnt = std::min((int)segs.size() - k0, KB_BLOCK);
+                    for (int w = 0; w < kWaves; w++) {
+                        int mx = 0;
+                        for (int l = w * 64; l < std::min(cnt, w * 64 + 64); l++) {
+                            const KBSeg& sg = segs[k0 + (((dirs >> b) & 1u) ? cnt - 1 - l : l)];
+                            mx = std::max(mx, sg.a1 - sg.a0);
+                        }
+                        wt[w] += mx;
+                    }
+                }
+                return *std::max_element(wt, wt + kWaves);
+            };
+            unsigned best = 0;
+            if (nb <= 12) {
+                int bc = cost(0);
+                for (unsigned d = 1; d < (1u << nb); d++) {
+                    const int c2 = cost(d);
+                    if (c2 < bc) { bc = c2; best = d; }
+                }
+            }
+            for (int b = 0; b < nb; b++)
+                if ((best >> b) & 1u) {
+                    const int k0 = b * KB_BLOCK, cnt = std::min((int)segs.size() - k0, KB_BLOCK);
+                    std::reverse(segs.begin() + k0, segs.begin() + k0 + cnt);
+                }
+        }
         const KBLayout KL = KBLayout::make(n, c->nnz, npart);
         const size_t kbl = kKBSmall + KL.total;
         if (kbl <= kLdsBudget) {

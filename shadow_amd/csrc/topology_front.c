@@ -264,8 +264,9 @@ static void* fill_worker(void* arg) {
                                 lbuf, rbuf, NULL);
         /* ENOEDGE: a self pair without a self-loop; the rows are complete and that entry
          * is NaN, i.e. not stored by the batch, as the reference skips the failed target
-         * (topology.c:1488-1495, 1812-1870); fill_locked resolves it below */
-        if (rc && rc != SHD_ROUTE_ENOEDGE) { job->rc = rc; break; }
+         * (topology.c:1488-1495, 1812-1870); fill_locked resolves it below.  EUNREACH
+         * (not after the strong-connectivity check at load) leaves the pair unstored */
+        if (rc && rc != SHD_ROUTE_ENOEDGE && rc != SHD_ROUTE_EUNREACH) { job->rc = rc; break; }
         for (int32_t r = 0; r < rows; r++) {
             const int32_t i = i0 + r;
             const size_t base = tri(na, i, i);

@@ -64,6 +64,7 @@ struct shd_route {
     double* d_kd_rtab = nullptr;    // distinct reliabilities
     int kd_nlight = 0, kd_nrtab = 1, kd_walk = 0, kd_packed = 0, kd_fused = 0;
     char* d_kd_ws = nullptr;
+    int* d_kd_next = nullptr;  // KD source queue counter
     int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD
     uint64_t device_bytes = 0;
     // host copies needed for lazy dense build
@@ -414,6 +415,8 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 if (hipMalloc((void**)&c->d_kd_ws, c->kd_stride * (size_t)c->kd_slots) != hipSuccess)
                     return SHD_ROUTE_ENOMEM;
                 c->allocs.push_back(c->d_kd_ws);
+                if (hipMalloc((void**)&c->d_kd_next, sizeof(int)) != hipSuccess) return SHD_ROUTE_ENOMEM;
+                c->allocs.push_back(c->d_kd_next);
                 const void* fn = kd_dispatch(blk, [&](auto B) { return (const void*)sssp_delta_kernel<decltype(B)::value>; });
                 rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
                 if (rc) return rc;
@@ -783,6 +786,8 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab; k.walk = c->kd_walk; k.packed = c->kd_packed;
         k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;
         const int grid = std::min(ns, c->kd_slots);
+        k.next = c->d_kd_next;
+        if (hipMemsetAsync(c->d_kd_next, 0, sizeof(int), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
         kd_dispatch(c->kd_block, [&](auto B) {
             constexpr int b = decltype(B)::value;
             hipLaunchKernelGGL(sssp_delta_kernel<b>, dim3(grid), dim3(b), c->kd_lds, st, k, d_src, ns, d_tgt,

@@ -66,6 +66,7 @@ constexpr uint32_t KD_NONE = 0xFFFFFFFFu;      // no parent recorded
 constexpr uint32_t KD_SRC_MARK = 0xFFFFFFFEu;  // parent record of the source itself
 
 struct DevDelta {
+    int* next;                          // source queue counter (zeroed before each launch)
     int n, nw;
     int nlight;                         // light in-arcs
     int nnz;                            // out-arcs
@@ -119,6 +120,7 @@ struct KDSmall {
     int qcur[2];        // phase B long-tail list lengths
     unsigned long long rmin;
     int deep;           // phase C path walk: some target deeper than KD_MAXD
+    int next;           // the workgroup's next source index
 #ifdef SHD_STAMPS
     unsigned long long acc[32];
 #endif
@@ -305,6 +307,14 @@ __device__ inline void kd_relax_list(const uint32_t* wimp, int cnt, int lane, un
     __builtin_amdgcn_wave_barrier();
 }
 
+__device__ inline int kd_next_source(int* ctr, int* slot, int tid) {
+    if (tid == 0) *slot = (int)gridDim.x + atomicAdd(ctr, 1);
+    __syncthreads();
+    const int i = *slot;
+    __syncthreads();  // every thread has read it before thread 0 writes the next one
+    return i;
+}
+
 template <int B>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sssp_delta_kernel(DevDelta g, const int* __restrict__ src, int ns,
                                                        const int* __restrict__ tgt, int nt, long long ld,
@@ -344,7 +354,10 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
 #endif
     const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
 
-    for (int i = blockIdx.x; i < ns; i += gridDim.x) {
+    // sources: one each to start, then from a queue, so workgroups that drew cheap
+    // sources take more and the launch ends within about one source of the mean
+    // (a static stride ended with the workgroups holding ceil(ns / grid) sources)
+    for (int i = blockIdx.x; i < ns; i = kd_next_source(g.next, &sm->next, tid)) {
         const int s = src[i];
         if (s < 0 || s >= n) {
             if (tid == 0) raise_err(err, SHD_ROUTE_EINVAL);

@@ -2,20 +2,25 @@
 """Benchmark: all-pairs topology routing (source-paths/s, GTEPS) on MI355X.
 
 One step = the hot path over one synthetic topology: every attached source's
-SOURCE(s,.) row (batched SSSP + path attributes, K1+K2) written to HBM, plus the
-device-wide runahead min (K5).  Inputs (graph, source/target lists) are resident in
-HBM before the timed region; outputs stay in HBM.
+SOURCE(s,.) row (batched SSSP + path attributes) written to HBM, plus the device-wide
+runahead min (K5).  Inputs (graph, source/target lists) are resident in HBM before the
+timed region; outputs stay in HBM.
 
-Default workload (N=1): BASELINE.json configs[1] = C2, a 2,000-vertex Barabasi-Albert
-Internet-like topology, all 2,000 vertices attached, full 2,000 x 2,000 table.
+Default workload: BASELINE.json configs[3] = C4, the 50,000-vertex / 500,000-edge
+synthetic AS graph, all 50,000 vertices attached: the full 50k x 50k latency and
+reliability table (2.5e9 pairs, 40 GB of f64 in HBM) per step.  --config c2 / c3
+select the smaller configs, --config c5 the dense complete graph (K3 direct fill + K5,
+with the K4 Floyd-Warshall timed beside it).
 
 Multi-GPU (one process per GPU, launched by torch.distributed.run):
-  --scaling weak   (default) every rank computes the full table of its own C2-shaped
-                   topology (seed 1 + rank; rank 0 is exactly C2): independent objects,
-                   no data-path collective.
-  --scaling strong one topology, attached sources sharded in contiguous blocks; the
-                   runahead min is combined with an RCCL all-reduce(MIN) each step and,
-                   with --allgather, the row shards are all-gathered over xGMI.
+  --scaling strong (default) one topology, attached sources in contiguous blocks per
+                   rank; the runahead min is combined with an RCCL all-reduce(MIN) each
+                   step.  The all-gather of the latency AND reliability row shards into
+                   the full table on every GPU is timed separately (it is needed only
+                   where a device-resident full matrix is; Shadow's host cache is filled
+                   per rank by D2H of its own shard); --allgather puts it in every step.
+  --scaling weak   every rank computes the full table of its own topology (seed 1 +
+                   rank): independent objects, no data-path collective.
 """
 from __future__ import annotations
 
@@ -23,7 +28,7 @@ import argparse
 import glob
 import json
 import os
-import platform
+import subprocess
 import sys
 import time
 
@@ -31,6 +36,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
+
+CFG_INDEX = {"c2": 1, "c3": 2, "c4": 3, "c5": 4}
 
 
 def b_src(n, nnz, nt):
@@ -50,28 +57,58 @@ def workload_graph(cfg: str, seed_offset: int):
                            name=f"{cfg}_rank{seed_offset}")
 
 
+def cpu_info():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count()
+    try:
+        out = subprocess.run(["ldconfig", "-p"], capture_output=True, text=True, timeout=20).stdout
+        igraph = "libigraph present: " + ",".join(sorted({l.split()[0] for l in out.splitlines() if "igraph" in l})) \
+            if "igraph" in out else "libigraph absent (ldconfig -p): reference not linkable, oracle port timed"
+    except Exception as e:  # noqa: BLE001
+        igraph = f"ldconfig probe failed: {e}"
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff, "igraph_probe": igraph}
+
+
 def cpu_baseline(g, sources, targets, budget_s: float):
-    """Oracle port timed on this box's host cores (rank 0, N=1 only)."""
+    """Oracle port timed on this box's host cores (rank 0, N=1 only), on a bounded seeded
+    sample of the same workload; the rate is per source row, so it extrapolates to the
+    full table linearly (every row is one full SSSP + |T| path products)."""
     from oracle.oracle import OracleGraph
     og = OracleGraph(g)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    # parallel restatement: the whole source set if it fits the budget, else a prefix sample
-    probe = sources[: max(1, min(len(sources), 64))]
+    rng = np.random.default_rng(12345)
+    probe = np.sort(rng.choice(sources, size=min(len(sources), 32), replace=False)).astype(np.int32)
     dt, _, used = og.bench_parallel(probe, targets, threads)
     per_src = dt / len(probe)
     k = int(min(len(sources), max(len(probe), budget_s / max(per_src, 1e-9))))
-    sample = sources[:k]
+    sample = np.sort(rng.choice(sources, size=k, replace=False)).astype(np.int32) if k < len(sources) else sources
     dt, _, used = og.bench_parallel(sample, targets, threads)
+    info = cpu_info()
     par = {"value": k / dt, "unit": "source-paths/s", "cores": int(used), "kind": "port",
-           "sample": f"{k} of {len(sources)} sources x {len(targets)} targets (oracle/oracle.c "
-                     f"orc_bench_parallel: OpenMP binary-heap Dijkstra + forward-order path products)",
-           "cpu": platform.processor() or platform.machine()}
+           "sample": f"{k} of {len(sources)} sources (seeded uniform sample) x {len(targets)} targets, "
+                     f"{dt:.2f} s on {used} threads (oracle/oracle.c orc_bench_parallel: OpenMP binary-heap "
+                     f"Dijkstra + forward-order path products); full table extrapolated "
+                     f"{len(sources) / (k / dt):.1f} s",
+           "extrapolated": k < len(sources), **info}
     # reference-faithful: 1 thread, igraph-order Dijkstra + per-hop get_eid + string formatting
-    kf = max(1, min(len(sources), int(0.25 * budget_s / max(per_src * used, 1e-9))))
-    dtf, _ = og.bench_faithful(sources[:kf], targets)
+    t1, _ = og.bench_faithful(sample[:1], targets)
+    kf = int(max(1, min(len(sources), 0.3 * budget_s / max(t1, 1e-9))))
+    dtf, _ = og.bench_faithful(sample[:kf], targets)
     faithful = {"value": kf / dtf, "unit": "source-paths/s", "cores": 1, "kind": "port",
-                "sample": f"{kf} sources x {len(targets)} targets, igraph-0.7.1-order Dijkstra with "
-                          "topology.c:1449,1502,1831 path/log formatting, serialised as under graphLock"}
+                "sample": f"{kf} sources x {len(targets)} targets in {dtf:.2f} s, igraph-0.7.1-order Dijkstra "
+                          "with topology.c:1449,1502,1831 path/log formatting, serialised as under graphLock",
+                "extrapolated": kf < len(sources)}
     return par, faithful
 
 
@@ -79,30 +116,44 @@ def load_traffic(cfg: str, n_src: int):
     """HBM bytes per launch of the dominant kernel from the committed PMC summary
     (profiles/*pmc*<cfg>*.json written by tools/pmc_traffic.py), or None."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc*{cfg}*.json")))
-    if not files:
-        return None
-    try:
-        d = json.load(open(files[-1]))
-        if int(d.get("sources_per_launch", -1)) != n_src:
-            return None
-        return float(d["hbm_bytes_per_launch"])
-    except Exception:
-        return None
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+            if int(d.get("sources_per_launch", -1)) == n_src:
+                return float(d["hbm_bytes_per_launch"])
+        except Exception:
+            continue
+    return None
+
+
+def timed(fn, reps, sync, barrier=None):
+    """Wall time of `reps` calls bracketed by barrier + device sync on both sides."""
+    if barrier:
+        barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    sync()
+    if barrier:
+        barrier()
+    return time.perf_counter() - t0
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"])
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
-    ap.add_argument("--allgather", action="store_true", help="strong: all-gather row shards each step")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"])
+    ap.add_argument("--allgather", action="store_true", help="strong: all-gather lat+rel shards in every step")
+    ap.add_argument("--gather-reps", type=int, default=2, help="strong, N>1: separately timed all-gathers")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--verify", type=int, default=8, help="rows checked against the oracle after timing")
-    ap.add_argument("--sources", type=int, default=0, help="limit sources per rank (0 = all)")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "f64", "k32", "kb", "k16", "kd"], help="force an SSSP kernel")
+    ap.add_argument("--sources", type=int, default=0, help="limit sources (0 = all)")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "f64", "k32", "kb", "kd"], help="force an SSSP kernel")
     args = ap.parse_args()
     if args.kernel != "auto":
         os.environ["SHD_ROUTE_KERNEL"] = args.kernel
@@ -113,16 +164,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("launch N>1 with torch.distributed.run (one process per GPU)")
+    if world == 1 and args.gpus > 1:
+        raise SystemExit("launch N>1 with torch.distributed.run (one process per GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
+    barrier = dist.barrier if world > 1 else None
+
+    if args.config == "c5":
+        return bench_c5(args, torch, dist, world, rank, dev, barrier)
 
     from shadow_amd.route import RouteEngine
+    from shadow_amd.shard import allgather_inplace, full_table, runahead_min, shard_range
 
     weak = args.scaling == "weak"
     g = workload_graph(args.config, rank if weak else 0)
@@ -130,12 +185,11 @@ def main():
     all_sources = targets.copy()
     if args.sources:
         all_sources = all_sources[: args.sources]
-    from shadow_amd.shard import allgather_rows, runahead_min, shard_range
     if weak or world == 1:
-        my_sources = all_sources
+        lo, hi = 0, len(all_sources)
     else:
         lo, hi = shard_range(len(all_sources), world, rank)
-        my_sources = all_sources[lo:hi]
+    my_sources = all_sources[lo:hi]
     ns, nt = len(my_sources), len(targets)
 
     eng = RouteEngine(g, device=local)
@@ -143,49 +197,64 @@ def main():
     sh = stream.cuda_stream
     d_src = torch.from_numpy(np.ascontiguousarray(my_sources, np.int32)).to(dev)
     d_tgt = torch.from_numpy(np.ascontiguousarray(targets, np.int32)).to(dev)
-    d_lat = torch.empty((max(ns, 1), nt), dtype=torch.float64, device=dev)
-    d_rel = torch.empty((max(ns, 1), nt), dtype=torch.float64, device=dev)
-    d_rmin = torch.empty(max(ns, 1), dtype=torch.float64, device=dev)
-    d_min = torch.empty(1, dtype=torch.float64, device=dev)
+    gather = world > 1 and not weak
+    proto = torch.empty(0, dtype=torch.float64, device=dev)
+    if gather:
+        # shards are views into the full tables: rows land in place, the gather is in place
+        f_lat, d_lat = full_table(len(all_sources), nt, world, rank, proto)
+        f_rel, d_rel = full_table(len(all_sources), nt, world, rank, proto)
+        d_lat, d_rel = d_lat[: max(ns, 1)], d_rel[: max(ns, 1)]
+    else:
+        d_lat = torch.empty((max(ns, 1), nt), dtype=torch.float64, device=dev)
+        d_rel = torch.empty((max(ns, 1), nt), dtype=torch.float64, device=dev)
+    # +inf: a rank with an empty shard contributes nothing to the runahead MIN
+    d_rmin = torch.full((max(ns, 1),), float("inf"), dtype=torch.float64, device=dev)
+    d_min = torch.full((1,), float("inf"), dtype=torch.float64, device=dev)
     torch.cuda.synchronize()
 
     k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     k_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
 
+    def gather_tables():
+        allgather_inplace(f_lat, dist)
+        allgather_inplace(f_rel, dist)
+
     def step(t=None):
         if t is not None:
             k_start[t].record(stream)
-        eng.rows_async(d_src, d_tgt, d_lat, d_rel, d_rmin, stream=sh)
+        if ns:
+            eng.rows_async(d_src, d_tgt, d_lat, d_rel, d_rmin, stream=sh)
         if t is not None:
             k_end[t].record(stream)
         eng.min_reduce_async(d_rmin, d_min, stream=sh)
         if world > 1 and not weak:
             runahead_min(d_min, dist)                         # RCCL all-reduce MIN
-            if args.allgather:                                # full latency table on every GPU
-                allgather_rows(d_lat[:ns], len(all_sources), dist)
+            if args.allgather:
+                gather_tables()
 
     for _ in range(args.warmup):
         step()
     eng.sync(sh)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for t in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    dt = timed(step, args.steps, torch.cuda.synchronize, barrier)
     eng.sync(sh)  # raises on any device-side error
-    # dominant-kernel duration: HIP events on the launch stream around the rows kernel, in
-    # a second pass of the same K steps (an event pair per step costs ~10 us of stream time
-    # on this stack, so the throughput pass above carries none)
+    # dominant-kernel duration: HIP events on the launch stream around the rows launch, in
+    # a second pass of the same K steps (the throughput pass above carries no events)
     for t in range(args.steps):
         step(t)
     torch.cuda.synchronize()
     eng.sync(sh)
     kms = [k_start[t].elapsed_time(k_end[t]) for t in range(args.steps)]
+    split = None
+    if gather:
+        # compute / collective split: the runahead all-reduce and the table
+        # all-gather, each timed on its own
+        ar_s = timed(lambda: runahead_min(d_min, dist), 20, torch.cuda.synchronize, barrier) / 20
+        ag_s = None
+        if not args.allgather and args.gather_reps > 0:
+            gather_tables()
+            ag_s = timed(gather_tables, args.gather_reps, torch.cuda.synchronize, barrier) / args.gather_reps
+        split = torch.tensor([float(np.mean(kms)) / 1e3, ar_s, ag_s or 0.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(split, op=dist.ReduceOp.MAX)
     dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
@@ -202,6 +271,7 @@ def main():
         rel_h = d_rel[torch.from_numpy(pick).to(dev)].cpu().numpy()
         olat, orel, _, _ = og.source_rows(my_sources[pick], targets, TIE_MINKEY)
         verified = bool(np.array_equal(lat_h, olat) and np.array_equal(rel_h, orel))
+    runahead = float(d_min.item())
 
     if rank != 0:
         if world > 1:
@@ -228,10 +298,12 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": f"{g.name}: Barabasi-Albert Internet-like topology, all-pairs latency/reliability "
-                        f"table (BASELINE.json configs[{ {'c2': 1, 'c3': 2, 'c4': 3}[args.config] }])",
+                        f"table (BASELINE.json configs[{CFG_INDEX[args.config]}])",
             "n_vertices": n, "n_edges": g.m, "n_edges_nonloop": g.m_nonloop, "csr_arcs": nnz,
-            "sources_per_gpu": ns, "targets": nt,
-            "parallelism": (f"replicas x{world} (independent topologies)" if weak else f"sources sharded /{world}"),
+            "sources_total": total_src, "sources_per_gpu": ns, "targets": nt,
+            "table_bytes": 16 * total_src * nt,
+            "parallelism": (f"replicas x{world} (independent topologies)" if weak
+                            else f"sources sharded in contiguous blocks /{world}"),
         },
         "gteps": total_src * g.m_nonloop * args.steps / dt / 1e9,
         "pairs_per_s": total_src * nt * args.steps / dt,
@@ -242,11 +314,21 @@ def main():
             "kernel": {0: "sssp_rows_kernel", 1: "sssp_k32_kernel",
                        2: ("sssp_batch_rows_kernel" if eng.info["reserved"] == 1
                            else "sssp_batch_kernel+path_attr_kernel"),
-                       3: "sssp_k16_kernel", 4: "sssp_delta_kernel"}[eng.info["kernel"]],
+                       4: "sssp_delta_kernel"}.get(eng.info["kernel"], str(eng.info["kernel"])),
             "bytes_per_source": b_src(n, nnz, nt),
+            "model": "SURVEY 8(d) B_src = 4(n+1) + 12 nnz + 12 n + 16 |T| per source row",
         },
+        "runahead_min_latency_ms": runahead,
         "verified_rows_vs_oracle": verified,
     }
+    if split is not None:
+        c_s, ar_s, ag_s = (float(x) for x in split.tolist())
+        gb = 16 * len(all_sources) * nt * (world - 1) / world
+        res["split"] = {"compute_ms": c_s * 1e3, "allreduce_min_ms": ar_s * 1e3,
+                        "allgather_lat_rel_ms": (ag_s * 1e3) if ag_s else None,
+                        "allgather_in_step": bool(args.allgather),
+                        "allgather_bytes_per_gpu": gb,
+                        "allgather_GBps_per_gpu": (gb / ag_s / 1e9) if ag_s else None}
     if not args.no_cpu_baseline and world == 1:
         par, faithful = cpu_baseline(g, all_sources, targets, args.cpu_budget)
         res["cpu_baseline"] = par
@@ -256,6 +338,13 @@ def main():
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_c5(args, torch, dist, world, rank, dev, barrier):
+    """C5: dense K4000 + self-loops.  A step is the reference semantics for a complete
+    graph: every pair DIRECT (K3 direct fill, topology.c:1877-1927) + the runahead
+    min (K5); the K4 blocked min-plus Floyd-Warshall all-pairs is timed beside it."""
+    raise SystemExit("c5 bench: not built yet")
 
 
 if __name__ == "__main__":

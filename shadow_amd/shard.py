@@ -30,7 +30,7 @@ def runahead_min(local_min, dist, group=None):
 
 
 def allgather_rows(local_rows, n_total: int, dist, group=None):
-    """All-gather row shards (each [rows_r, nt]) into the full [n_total, nt] table.
+    """All-gather row shards (each [rows_r, nt]) into a new full [n_total, nt] table.
     Shards are padded to the common block size for the collective."""
     import torch
     world = dist.get_world_size(group) if dist is not None and dist.is_initialized() else 1
@@ -39,6 +39,27 @@ def allgather_rows(local_rows, n_total: int, dist, group=None):
     blk = block_rows(n_total, world)
     pad = blk - local_rows.shape[0]
     send = local_rows if pad == 0 else torch.nn.functional.pad(local_rows, (0, 0, 0, pad))
-    out = [torch.empty_like(send) for _ in range(world)]
-    dist.all_gather(out, send.contiguous(), group=group)
-    return torch.cat(out, 0)[:n_total]
+    out = torch.empty((blk * world,) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
+    dist.all_gather_into_tensor(out, send.contiguous(), group=group)
+    return out[:n_total]
+
+
+def full_table(n_total: int, nt: int, world: int, rank: int, like):
+    """A [ceil(n_total/world) * world, nt] table whose rank block is this rank's shard:
+    rows are computed straight into `shard` and gathered in place (allgather_inplace),
+    so the C4 table (20 GB per f64 array) never needs a second copy."""
+    import torch
+    blk = block_rows(n_total, world)
+    full = torch.empty((blk * world, nt), dtype=like.dtype, device=like.device)
+    return full, full[rank * blk:(rank + 1) * blk]
+
+
+def allgather_inplace(full, dist, group=None):
+    """In-place all-gather of a full_table(): every rank's block to every rank."""
+    world = dist.get_world_size(group) if dist is not None and dist.is_initialized() else 1
+    if world == 1:
+        return full
+    rank = dist.get_rank(group)
+    blk = full.shape[0] // world
+    dist.all_gather_into_tensor(full, full[rank * blk:(rank + 1) * blk], group=group)
+    return full

@@ -154,9 +154,12 @@ def main():
     ap.add_argument("--verify", type=int, default=8, help="rows checked against the oracle after timing")
     ap.add_argument("--sources", type=int, default=0, help="limit sources (0 = all)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "f64", "k32", "kb", "kd"], help="force an SSSP kernel")
+    ap.add_argument("--no-seed", action="store_true", help="plain KD rows (no seeded plan)")
     args = ap.parse_args()
     if args.kernel != "auto":
         os.environ["SHD_ROUTE_KERNEL"] = args.kernel
+    if args.no_seed:
+        os.environ["SHD_ROUTE_SEED"] = "0"
 
     import torch
     import torch.distributed as dist
@@ -177,7 +180,7 @@ def main():
         return bench_c5(args, torch, dist, world, rank, dev, barrier)
 
     from shadow_amd.route import RouteEngine
-    from shadow_amd.shard import allgather_inplace, full_table, runahead_min, shard_range
+    from shadow_amd.shard import allgather_inplace, full_table, runahead_min
 
     weak = args.scaling == "weak"
     g = workload_graph(args.config, rank if weak else 0)
@@ -185,17 +188,16 @@ def main():
     all_sources = targets.copy()
     if args.sources:
         all_sources = all_sources[: args.sources]
-    if weak or world == 1:
-        lo, hi = 0, len(all_sources)
-    else:
-        lo, hi = shard_range(len(all_sources), world, rank)
-    my_sources = all_sources[lo:hi]
-    ns, nt = len(my_sources), len(targets)
-
     eng = RouteEngine(g, device=local)
+    # the rows of this rank (strong: a contiguous block of the source list) under one
+    # seeded plan: rows whose source has an already-computed neighbour start from it
+    t_plan = time.perf_counter()
+    plan = eng.plan(all_sources, 1 if weak else world, 0 if weak else rank)
+    t_plan = time.perf_counter() - t_plan
+    my_sources = plan.sources
+    ns, nt = len(my_sources), len(targets)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
-    d_src = torch.from_numpy(np.ascontiguousarray(my_sources, np.int32)).to(dev)
     d_tgt = torch.from_numpy(np.ascontiguousarray(targets, np.int32)).to(dev)
     gather = world > 1 and not weak
     proto = torch.empty(0, dtype=torch.float64, device=dev)
@@ -223,7 +225,7 @@ def main():
         if t is not None:
             k_start[t].record(stream)
         if ns:
-            eng.rows_async(d_src, d_tgt, d_lat, d_rel, d_rmin, stream=sh)
+            plan.rows_async(d_tgt, d_lat, d_rel, d_rmin, stream=sh)
         if t is not None:
             k_end[t].record(stream)
         eng.min_reduce_async(d_rmin, d_min, stream=sh)
@@ -316,8 +318,10 @@ def main():
                            else "sssp_batch_kernel+path_attr_kernel"),
                        4: "sssp_delta_kernel"}.get(eng.info["kernel"], str(eng.info["kernel"])),
             "bytes_per_source": b_src(n, nnz, nt),
+            "launches_per_step": plan.info["launches"],
             "model": "SURVEY 8(d) B_src = 4(n+1) + 12 nnz + 12 n + 16 |T| per source row",
         },
+        "plan": {**plan.info, "plan_seconds": t_plan},
         "runahead_min_latency_ms": runahead,
         "verified_rows_vs_oracle": verified,
     }

@@ -131,6 +131,46 @@ int shd_route_self(shd_route_t* ctx, const int32_t* v, int32_t nv, double* lat_o
 int shd_route_min_reduce_async(shd_route_t* ctx, const double* d_vals, int64_t count,
                                double* d_out, void* stream);
 
+/* ---- planned (seeded) rows: the eager fill of many sources at once -----------------
+ * Replaces the same reference work as shd_route_rows (one SOURCE(s,.) row per source,
+ * topology.c:1655-1875), planned over the whole source list.  A row whose source s has
+ * a neighbour u among the planned sources may start from u's finished row: distances
+ * w(s,u) + d_u(v) are path lengths that already satisfy every arc, so only the vertices
+ * that improve on them are expanded, and the rows come out bit-identical to unseeded
+ * rows (same distances, same engine tie rule for parents, same source-first products).
+ * The plan orders the rows by depth in the seed forest into one launch, where a row
+ * waits for its seed row's ready flag, and keeps the seeding rows (u16 distances +
+ * parent records per vertex) in a device row store.
+ * Rows of a multi-GPU job: with world > 1 this rank's output rows are the contiguous
+ * block rank of the caller's list (shd_route_plan_rows gives their positions).  Plans
+ * need the KD kernel on an undirected integer-latency topology (else the plan falls
+ * back to plain rows); SHD_ROUTE_SEED=0 in the environment disables seeding. */
+typedef struct shd_route_plan shd_route_plan_t;
+
+typedef struct shd_route_plan_info {
+    int32_t rows;          /* output rows of this rank */
+    int32_t seeded;        /* 1 = seeded launches, 0 = plain rows */
+    int32_t launches;      /* kernel launches per shd_route_rows_planned_async */
+    int32_t levels;        /* depth of the seed forest (longest chain of seeded rows) */
+    int32_t roots;         /* rows computed from scratch */
+    int32_t helpers;       /* rows computed only to seed others (no output) */
+    int32_t stored_rows;   /* rows kept in the row store */
+    int32_t world, rank;
+    uint64_t store_bytes;  /* device bytes of the row store */
+} shd_route_plan_info_t;
+
+int shd_route_plan_create(shd_route_t* ctx, const int32_t* src, int32_t ns, int32_t world, int32_t rank,
+                          shd_route_plan_t** out);
+void shd_route_plan_destroy(shd_route_plan_t* plan);
+int shd_route_plan_get_info(const shd_route_plan_t* plan, shd_route_plan_info_t* info);
+/* positions (in the caller's source list) of this rank's output rows, in row order */
+int shd_route_plan_rows(const shd_route_plan_t* plan, int32_t* pos_out);
+/* this rank's rows of the plan: row r of d_lat / d_rel / d_row_min = source
+ * src[pos[r]]; device pointers as shd_route_rows_async */
+int shd_route_rows_planned_async(shd_route_t* ctx, const shd_route_plan_t* plan, const int32_t* d_tgt,
+                                 int32_t nt, int64_t ld, uint32_t flags, double* d_lat, double* d_rel,
+                                 double* d_row_min, void* stream);
+
 /* Dense all-pairs shortest latencies by blocked min-plus Floyd-Warshall over all
  * vertices: d_dist is n x n (device, row-major).  Bit-exact against Dijkstra only
  * for integer-valued latencies (fl sums of subpaths are not left folds otherwise). */

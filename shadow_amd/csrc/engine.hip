@@ -2,6 +2,8 @@
 #include "common.hpp"
 
 #include <map>
+#include <memory>
+#include <thread>
 #include "sssp_f64.hpp"
 #include "sssp_k32.hpp"
 #include "sssp_batch.hpp"
@@ -65,6 +67,12 @@ struct shd_route {
     int kd_nlight = 0, kd_nrtab = 1, kd_walk = 0, kd_packed = 0, kd_fused = 0;
     char* d_kd_ws = nullptr;
     int* d_kd_next = nullptr;  // KD source queue counter
+    // host copies for seeded planning (shd_route_plan_*): out-CSR, rtab index per arc and
+    // the landmark closeness of every vertex (computed on the first plan)
+    std::vector<int> h_row, h_col;
+    std::vector<double> h_w;
+    std::vector<uint16_t> h_ridx;
+    std::vector<double> close;
     int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD
     uint64_t device_bytes = 0;
     // host copies needed for lazy dense build
@@ -398,6 +406,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                     lrow[v + 1] = (int)(lrec.size() / 2);
                 }
                 if (lrec.empty()) lrec.assign(2, 0u);
+                c->h_row = row; c->h_col = col; c->h_w = w; c->h_ridx = ridx_out;
                 rc = upload(c, &c->d_kd_lstart, lrow);
                 if (!rc) rc = upload(c, &c->d_kd_orec, orec);
                 if (!rc) rc = upload(c, &c->d_kd_oridx, ridx_out);
@@ -533,8 +542,39 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
             if (const char* e = getenv("SHD_ROUTE_KBGRID")) c->kb_grid_cap = std::max(1, atoi(e));
         }
     }
-    c->sel = c->kb ? 2 : c->kd ? 4 : c->k32 ? 1 : c->k16 ? 3 : 0;  // K32 still beats KD on C3-class graphs
+    c->sel = c->kb ? 2 : c->kd ? 4 : c->k32 ? 1 : c->k16 ? 3 : 0;  // KB (C2-class), else KD (C3/C4-class)
     return SHD_ROUTE_OK;
+}
+
+DevDelta kd_args(const shd_route* c) {
+    DevDelta k;
+    k.n = c->n; k.nw = (c->n + 63) / 64; k.bound = c->k32_bound; k.delta = c->kd_delta;
+    k.fused = c->kd_fused; k.rc = c->kd_qcap;
+    k.row = c->d_row; k.orec = c->d_kd_orec; k.oridx = c->d_kd_oridx;
+    k.nnz = c->nnz; k.lrow = c->d_kd_lstart; k.lrec = reinterpret_cast<const uint2*>(c->d_kd_lrec); k.nlight = c->kd_nlight;
+    k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab; k.walk = c->kd_walk; k.packed = c->kd_packed;
+    k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;
+    k.jobs = nullptr; k.drow = nullptr; k.drow_out = nullptr; k.prow = nullptr; k.rstride = 0; k.evcap = c->n;
+    k.done = nullptr;
+    // tests shrink the tie-event list to force the unseeded rerun of overflowing rows
+    if (const char* e = getenv("SHD_ROUTE_EVCAP")) k.evcap = std::max(0, std::min(c->n, atoi(e)));
+    k.next = nullptr;
+    return k;
+}
+
+// one KD launch of ns sources (k.jobs: planned jobs, else d_src); `next` is zeroed
+int kd_launch(shd_route* c, DevDelta k, int* next, const int32_t* d_src, int ns, const int32_t* d_tgt, int nt,
+              int64_t ld, double* d_lat, double* d_rel, double* d_row_min, hipStream_t st) {
+    if (ns <= 0) return SHD_ROUTE_OK;
+    k.next = next;
+    const int grid = std::min(ns, c->kd_slots);
+    kd_dispatch(c->kd_block, [&](auto B) {
+        constexpr int b = decltype(B)::value;
+        hipLaunchKernelGGL(sssp_delta_kernel<b>, dim3(grid), dim3(b), c->kd_lds, st, k, d_src, ns, d_tgt,
+                           nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kd_ws, c->kd_stride);
+        return 0;
+    });
+    return hip_check(hipGetLastError());
 }
 
 int take_err(shd_route* c) {
@@ -778,23 +818,9 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         return hip_check(hipGetLastError());
     }
     if (c->sel == 4 && !(dispatch && c->prefer_direct)) {
-        DevDelta k;
-        k.n = c->n; k.nw = (c->n + 63) / 64; k.bound = c->k32_bound; k.delta = c->kd_delta;
-        k.fused = c->kd_fused; k.rc = c->kd_qcap;
-        k.row = c->d_row; k.orec = c->d_kd_orec; k.oridx = c->d_kd_oridx;
-        k.nnz = c->nnz; k.lrow = c->d_kd_lstart; k.lrec = reinterpret_cast<const uint2*>(c->d_kd_lrec); k.nlight = c->kd_nlight;
-        k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab; k.walk = c->kd_walk; k.packed = c->kd_packed;
-        k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;
-        const int grid = std::min(ns, c->kd_slots);
-        k.next = c->d_kd_next;
+        DevDelta k = kd_args(c);
         if (hipMemsetAsync(c->d_kd_next, 0, sizeof(int), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
-        kd_dispatch(c->kd_block, [&](auto B) {
-            constexpr int b = decltype(B)::value;
-            hipLaunchKernelGGL(sssp_delta_kernel<b>, dim3(grid), dim3(b), c->kd_lds, st, k, d_src, ns, d_tgt,
-                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kd_ws, c->kd_stride);
-            return 0;
-        });
-        return hip_check(hipGetLastError());
+        return kd_launch(c, k, c->d_kd_next, d_src, ns, d_tgt, nt, ld, d_lat, d_rel, d_row_min, st);
     }
     if (c->sel == 3 && !(dispatch && c->prefer_direct)) {
         DevK16 k;
@@ -894,10 +920,21 @@ int host_rows(shd_route* c, const int32_t* src, int32_t ns, const int32_t* tgt, 
 }
 }  // namespace
 
+namespace {
+int planned_host_rows(shd_route* c, const int32_t* src, int32_t ns, const int32_t* tgt, int32_t nt,
+                      uint32_t flags, double* lat_out, double* rel_out, double* row_min_out);
+}
+
 extern "C" {
 
 int shd_route_rows(shd_route_t* c, const int32_t* src, int32_t ns, const int32_t* tgt, int32_t nt,
                    uint32_t flags, double* lat_out, double* rel_out, double* row_min_out) {
+    // many KD rows: one seeded plan over all of them when the whole table fits the device
+    if (c && c->sel == 4 && c->kd_fused && ns >= 2 && nt >= 1 && src && tgt &&
+        !((flags & SHD_ROUTE_DISPATCH) && (c->complete || c->prefer_direct))) {
+        const int rc = planned_host_rows(c, src, ns, tgt, nt, flags, lat_out, rel_out, row_min_out);
+        if (rc != SHD_ROUTE_EUNSUPPORTED) return rc;
+    }
     return host_rows(c, src, ns, tgt, nt, lat_out, rel_out, row_min_out,
                      [&](const int32_t* ds, int32_t k, const int32_t* dt, double* dl, double* dr, double* dm) {
                          return shd_route_rows_async(c, ds, k, dt, nt, nt, flags, dl, dr, dm, nullptr);
@@ -973,6 +1010,269 @@ int shd_route_fw_async(shd_route_t* c, double* d_dist, void* stream) {
 }
 
 }  // extern "C"
+
+// =============================================================================
+// Seeded planning (shd_route_plan_*): which row seeds which, and in which launch.
+// =============================================================================
+struct shd_route_plan {
+    shd_route* c = nullptr;
+    int world = 1, rank = 0, ns_all = 0;
+    int seeded = 0, nroots = 0, nhelpers = 0, nslots = 0;
+    std::vector<int32_t> row_pos;  // caller-list position of each output row of this rank
+    std::vector<int> lvl_off;      // jobs of launch k: [lvl_off[k], lvl_off[k + 1])
+    KDJob* d_jobs = nullptr;
+    int* d_next = nullptr;         // the launch's job-queue counter + one ready flag per kept row
+    int32_t* d_src = nullptr;      // unseeded plans: the source vertex of each row
+    uint16_t* d_drow = nullptr;    // row store
+    uint32_t* d_prow = nullptr;
+    uint64_t store_bytes = 0;
+    ~shd_route_plan() {
+        for (void* q : {(void*)d_jobs, (void*)d_next, (void*)d_src, (void*)d_drow, (void*)d_prow})
+            if (q) (void)hipFree(q);
+    }
+};
+
+namespace {
+
+// Dijkstra over the host out-CSR (all distances from `src`)
+void host_dijkstra(const shd_route* c, int src, std::vector<double>& d) {
+    const int n = c->n;
+    d.assign(n, INFINITY);
+    std::vector<std::pair<double, int>> h;
+    auto cmp = [](const std::pair<double, int>& a, const std::pair<double, int>& b) { return a.first > b.first; };
+    d[src] = 0;
+    h.push_back({0.0, src});
+    while (!h.empty()) {
+        std::pop_heap(h.begin(), h.end(), cmp);
+        auto [du, u] = h.back();
+        h.pop_back();
+        if (du > d[u]) continue;
+        for (int a = c->h_row[u]; a < c->h_row[u + 1]; a++) {
+            const double nd = du + c->h_w[a];
+            if (nd < d[c->h_col[a]]) { d[c->h_col[a]] = nd; h.push_back({nd, c->h_col[a]}); std::push_heap(h.begin(), h.end(), cmp); }
+        }
+    }
+}
+
+// closeness estimate: mean distance from 16 pseudo-random landmarks (deterministic)
+void ensure_close(shd_route* c) {
+    if (!c->close.empty()) return;
+    const int n = c->n, L = std::min(n, 16);
+    std::vector<int> lm;
+    uint64_t x = 0x243F6A8885A308D3ull;
+    while ((int)lm.size() < L) {
+        x += 0x9E3779B97F4A7C15ull;
+        uint64_t z = x;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        const int v = (int)(z % (uint64_t)n);
+        if (std::find(lm.begin(), lm.end(), v) == lm.end()) lm.push_back(v);
+    }
+    std::vector<std::vector<double>> D(L);
+    {
+        std::vector<std::thread> th;
+        for (int k = 0; k < L; k++) th.emplace_back([&, k] { host_dijkstra(c, lm[k], D[k]); });
+        for (auto& t : th) t.join();
+    }
+    c->close.assign(n, 0.0);
+    for (int v = 0; v < n; v++) {
+        double sum = 0;
+        for (int k = 0; k < L; k++) sum += D[k][v];
+        c->close[v] = sum / L;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_t world, int32_t rank,
+                          shd_route_plan_t** out) {
+    if (!c || !out || ns < 0 || (ns && !src) || world < 1 || rank < 0 || rank >= world) return SHD_ROUTE_EINVAL;
+    *out = nullptr;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    for (int p = 0; p < ns; p++) if (src[p] < 0 || src[p] >= c->n) return SHD_ROUTE_EINVAL;
+    auto P = std::make_unique<shd_route_plan>();
+    P->c = c; P->world = world; P->rank = rank; P->ns_all = ns;
+    const int n = c->n;
+    // rows of this rank: a contiguous block of the caller's list (world 1: all of it)
+    const int blk = (ns + world - 1) / world, lo = std::min(ns, rank * blk), hi = std::min(ns, lo + blk);
+    for (int p = lo; p < hi; p++) P->row_pos.push_back(p);
+    const int nr = (int)P->row_pos.size();
+    const char* env = getenv("SHD_ROUTE_SEED");
+    const bool want = (!env || atoi(env) != 0) && c->sel == 4 && c->kd_fused && !c->complete && !c->prefer_direct &&
+                      nr >= 2 && !c->h_row.empty();
+    std::vector<KDJob> jobs;
+    if (want) {
+        ensure_close(c);
+        // rank of every vertex by (closeness, id): a row may only be seeded by a row of
+        // smaller rank, so the seed graph is a forest and its depth orders the launches
+        std::vector<int> ord(n), rk(n);
+        std::iota(ord.begin(), ord.end(), 0);
+        std::sort(ord.begin(), ord.end(), [&](int a, int b) {
+            return c->close[a] != c->close[b] ? c->close[a] < c->close[b] : a < b;
+        });
+        for (int q = 0; q < n; q++) rk[ord[q]] = q;
+        std::vector<int> first(n, -1);  // first row of each source vertex
+        for (int r = 0; r < nr; r++) if (first[src[P->row_pos[r]]] < 0) first[src[P->row_pos[r]]] = r;
+        // rows in rank order: a row's seed (smaller rank) is settled before it
+        std::vector<int> rows(nr), lvl(nr, 0), slot(nr, -1), seedrow(nr, -1), su(nr, -1), wr(nr, 0);
+        std::iota(rows.begin(), rows.end(), 0);
+        std::sort(rows.begin(), rows.end(), [&](int a, int b) {
+            const int va = src[P->row_pos[a]], vb = src[P->row_pos[b]];
+            return rk[va] != rk[vb] ? rk[va] < rk[vb] : a < b;
+        });
+        // options: the `roots` most central rows start unseeded (fills the machine at the
+        // start of the launch), and seed chains are at most `depth` rows long
+        int nroot_min = 0, depth = 1 << 30;
+        if (const char* e = getenv("SHD_ROUTE_SEED_ROOTS")) nroot_min = std::max(0, atoi(e));
+        if (const char* e = getenv("SHD_ROUTE_SEED_DEPTH")) depth = std::max(1, atoi(e));
+        // seed of each row: the neighbour u (a row of this rank, smaller rank, level below
+        // the cap) minimising w(s,u) + closeness(u), i.e. the likely gateway of most
+        // shortest paths from s
+        int nlev = 1, q = 0;
+        for (int r : rows) {
+            const int s = src[P->row_pos[r]];
+            double best = INFINITY;
+            if (q++ >= nroot_min)
+                for (int a = c->h_row[s]; a < c->h_row[s + 1]; a++) {
+                    const int u = c->h_col[a];
+                    if (u == s || first[u] < 0 || rk[u] >= rk[s] || lvl[first[u]] + 1 >= depth) continue;
+                    const double sc = c->h_w[a] + c->close[u];
+                    if (sc < best || (sc == best && u < su[r])) {
+                        best = sc; su[r] = u; seedrow[r] = first[u];
+                        wr[r] = (int)c->h_w[a] | ((int)c->h_ridx[a] << 16);
+                    }
+                }
+            if (seedrow[r] >= 0) {
+                lvl[r] = lvl[seedrow[r]] + 1;
+                if (slot[seedrow[r]] < 0) slot[seedrow[r]] = P->nslots++;
+            } else P->nroots++;
+            nlev = std::max(nlev, lvl[r] + 1);
+        }
+        const long long rs = kd_row_stride(n);
+        P->store_bytes = (uint64_t)P->nslots * (uint64_t)rs * 6u;
+        bool ok = P->nslots > 0 &&
+                  hipMalloc((void**)&P->d_drow, sizeof(uint16_t) * (size_t)rs * P->nslots) == hipSuccess &&
+                  hipMalloc((void**)&P->d_prow, sizeof(uint32_t) * (size_t)rs * P->nslots) == hipSuccess;
+        if (ok) {
+            std::vector<int> cnt(nlev + 1, 0);
+            for (int r = 0; r < nr; r++) cnt[lvl[r] + 1]++;
+            for (int k = 0; k < nlev; k++) cnt[k + 1] += cnt[k];
+            P->lvl_off = cnt;
+            jobs.resize(nr);
+            for (int r = 0; r < nr; r++) {  // rows of a level in row order
+                KDJob& J = jobs[cnt[lvl[r]]++];
+                J.row = r; J.s = src[P->row_pos[r]];
+                J.seed = seedrow[r] >= 0 ? slot[seedrow[r]] : -1;
+                J.store = slot[r]; J.u = su[r]; J.wr = wr[r]; J.pad0 = J.pad1 = 0;
+            }
+            P->seeded = 1;
+        } else {
+            if (P->d_drow) (void)hipFree(P->d_drow);
+            P->d_drow = nullptr;
+            P->nslots = 0; P->nroots = 0; P->store_bytes = 0;
+        }
+    }
+    int rc = SHD_ROUTE_OK;
+    if (P->seeded) {
+        if (hipMalloc((void**)&P->d_jobs, sizeof(KDJob) * jobs.size()) != hipSuccess ||
+            hipMalloc((void**)&P->d_next, sizeof(int) * (1 + (size_t)P->nslots)) != hipSuccess)
+            return SHD_ROUTE_ENOMEM;
+        if (hipMemcpy(P->d_jobs, jobs.data(), sizeof(KDJob) * jobs.size(), hipMemcpyHostToDevice) != hipSuccess)
+            return SHD_ROUTE_EDEVICE;
+    } else {
+        std::vector<int32_t> sv(std::max(nr, 1), 0);
+        for (int r = 0; r < nr; r++) sv[r] = src[P->row_pos[r]];
+        if (hipMalloc((void**)&P->d_src, sizeof(int32_t) * sv.size()) != hipSuccess) return SHD_ROUTE_ENOMEM;
+        if (hipMemcpy(P->d_src, sv.data(), sizeof(int32_t) * sv.size(), hipMemcpyHostToDevice) != hipSuccess)
+            return SHD_ROUTE_EDEVICE;
+        P->nroots = nr;
+    }
+    *out = P.release();
+    return rc;
+}
+
+void shd_route_plan_destroy(shd_route_plan_t* P) {
+    if (!P) return;
+    (void)hipSetDevice(P->c->device);
+    delete P;
+}
+
+int shd_route_plan_get_info(const shd_route_plan_t* P, shd_route_plan_info_t* info) {
+    if (!P || !info) return SHD_ROUTE_EINVAL;
+    info->rows = (int32_t)P->row_pos.size();
+    info->seeded = P->seeded;
+    info->launches = 1;
+    info->levels = P->seeded ? (int32_t)P->lvl_off.size() - 1 : 1;
+    info->roots = P->nroots;
+    info->helpers = P->nhelpers;
+    info->stored_rows = P->nslots;
+    info->world = P->world;
+    info->rank = P->rank;
+    info->store_bytes = P->store_bytes;
+    return SHD_ROUTE_OK;
+}
+
+int shd_route_plan_rows(const shd_route_plan_t* P, int32_t* pos_out) {
+    if (!P || !pos_out) return SHD_ROUTE_EINVAL;
+    std::copy(P->row_pos.begin(), P->row_pos.end(), pos_out);
+    return SHD_ROUTE_OK;
+}
+
+int shd_route_rows_planned_async(shd_route_t* c, const shd_route_plan_t* P, const int32_t* d_tgt, int32_t nt,
+                                 int64_t ld, uint32_t flags, double* d_lat, double* d_rel, double* d_row_min,
+                                 void* stream) {
+    if (!c || !P || P->c != c || nt < 0 || (nt && !d_tgt) || ld < nt) return SHD_ROUTE_EINVAL;
+    const int nr = (int)P->row_pos.size();
+    if (!P->seeded) return shd_route_rows_async(c, P->d_src, nr, d_tgt, nt, ld, flags, d_lat, d_rel, d_row_min, stream);
+    hipStream_t st = (hipStream_t)stream;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    // one launch: jobs in level order from one queue; a seeded job waits for its seed's
+    // ready flag (set once the kept row is complete, before that row's phase C)
+    if (hipMemsetAsync(P->d_next, 0, sizeof(int) * (1 + (size_t)P->nslots), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    DevDelta k = kd_args(c);
+    k.drow = P->d_drow; k.drow_out = P->d_drow; k.prow = P->d_prow; k.rstride = kd_row_stride(c->n);
+    k.jobs = P->d_jobs;
+    k.done = P->d_next + 1;
+    return kd_launch(c, k, P->d_next, nullptr, nr, d_tgt, nt, ld, d_lat, d_rel, d_row_min, st);
+}
+
+}  // extern "C"
+
+
+namespace {
+// shd_route_rows through a seeded plan: every row in one device table (EUNSUPPORTED when
+// the plan is not seeded or the table does not fit, so the caller takes the chunked path)
+int planned_host_rows(shd_route* c, const int32_t* src, int32_t ns, const int32_t* tgt, int32_t nt,
+                      uint32_t flags, double* lat_out, double* rel_out, double* row_min_out) {
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    const size_t table = sizeof(double) * (size_t)ns * (size_t)nt;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || 2 * table + ((size_t)ns << 20) > fr / 2) return SHD_ROUTE_EUNSUPPORTED;
+    shd_route_plan_t* P = nullptr;
+    int rc = shd_route_plan_create(c, src, ns, 1, 0, &P);
+    if (rc) return rc;
+    std::unique_ptr<shd_route_plan, void (*)(shd_route_plan*)> guard(P, shd_route_plan_destroy);
+    if (!P->seeded) return SHD_ROUTE_EUNSUPPORTED;
+    DevBuf dtgt, dlat, drel, dmin;
+    if ((rc = dtgt.alloc(sizeof(int32_t) * nt)) || (rc = dlat.alloc(table)) || (rc = drel.alloc(table)) ||
+        (rc = dmin.alloc(sizeof(double) * ns)))
+        return rc;
+    if (hipMemcpy(dtgt.p, tgt, sizeof(int32_t) * nt, hipMemcpyHostToDevice) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    rc = shd_route_rows_planned_async(c, P, (const int32_t*)dtgt.p, nt, nt, flags, (double*)dlat.p, (double*)drel.p,
+                                      (double*)dmin.p, nullptr);
+    if (rc) return rc;
+    const int soft = shd_route_sync(c, nullptr);
+    if (soft && soft != SHD_ROUTE_ENOEDGE && soft != SHD_ROUTE_EUNREACH) return soft;
+    if ((lat_out && hipMemcpy(lat_out, dlat.p, table, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (rel_out && hipMemcpy(rel_out, drel.p, table, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (row_min_out && hipMemcpy(row_min_out, dmin.p, sizeof(double) * ns, hipMemcpyDeviceToHost) != hipSuccess))
+        return SHD_ROUTE_EDEVICE;
+    return soft;
+}
+}  // namespace
 
 #ifdef SHD_STAMPS
 // Diagnostic builds only (not part of include/shd_route.h): per-source phase stamps.

@@ -65,8 +65,37 @@ constexpr int KD_IMP = 192;  // per-wave list of improving arcs (v | nd << 16), 
 constexpr uint32_t KD_NONE = 0xFFFFFFFFu;      // no parent recorded
 constexpr uint32_t KD_SRC_MARK = 0xFFFFFFFEu;  // parent record of the source itself
 
+// Seeded rows (planned launches, engine.hip shd_route_plan_*).  A source s whose
+// neighbour u already has its row (dist d_u and parent records p_u, kept in a row
+// store) starts from D0(v) = w(s,u) + d_u(v) instead of infinity.  D0 is a set of
+// path lengths that is already consistent (d_u(x) <= d_u(v) + w(v,x) for every arc),
+// so only s and the vertices that improve on D0 are ever expanded: on the BA
+// topologies 15-18% of them (C3/C4) instead of all.  Parents of the vertices that do
+// not improve: their tight in-arcs are exactly u's tight in-arcs (all of whose tails
+// also kept D0) plus tight arcs from improved vertices, so the parent is the better
+// (engine tie rule) of p_u(v) and the tight improved in-neighbours, which the
+// expansion reports as tie events (dist[x] + w == dist[v], found by the same reads).
+struct KDJob {
+    int row;    // output row
+    int s;      // source vertex
+    int seed;   // row-store slot of the seed's row, -1 = unseeded (a root)
+    int store;  // row-store slot this row is kept in for later seeds, -1 = not kept
+    int u;      // seed vertex (a neighbour of s)
+    int wr;     // w(s,u) | ridx(s,u) << 16
+    int pad0, pad1;
+};
+constexpr uint32_t KD_EVTAG = 0xFFFF0000u;  // ring record y of a tie event: v | KD_EVTAG
+typedef unsigned short kd_us2 __attribute__((ext_vector_type(2)));
+
 struct DevDelta {
     int* next;                          // source queue counter (zeroed before each launch)
+    const KDJob* __restrict__ jobs;     // planned launch: job j instead of src[j] / row j
+    const uint16_t* __restrict__ drow;  // row store: dist u16 [slot * rstride + v]
+    uint16_t* drow_out;                 // (the same store, written)
+    uint32_t* prow;                     // row store: parent records [slot * rstride + v]
+    long long rstride;
+    int evcap;                          // tie events per source held in the workgroup slice
+    int* done;                          // per row-store slot: 1 once the kept row is complete
     int n, nw;
     int nlight;                         // light in-arcs
     int nnz;                            // out-arcs
@@ -121,6 +150,8 @@ struct KDSmall {
     unsigned long long rmin;
     int deep;           // phase C path walk: some target deeper than KD_MAXD
     int next;           // the workgroup's next source index
+    int nev;            // seeded: tie events the writer wave stored
+    int evovf;          // seeded: more tie events than the slice holds (rerun unseeded)
 #ifdef SHD_STAMPS
     unsigned long long acc[32];
 #endif
@@ -170,8 +201,12 @@ template <int B>
 constexpr int kd_rr() { return B >= 1024 ? KD_RR : 256; }
 
 // per-workgroup HBM slice: relv f64[n] | wpr u32[n], the parent record of every vertex:
-// parent | ridx << 16 of the parent arc (KD_SRC_MARK for the source)
-__host__ __device__ inline size_t kd_ws_stride(int n) { return a16(sizeof(double) * n) + a16(sizeof(uint32_t) * n) + 256; }
+// parent | ridx << 16 of the parent arc (KD_SRC_MARK for the source) | tie events
+// {p | ridx << 16 | w << 24, v} x n (seeded rows).  Seeded rows use relv as u32 keys.
+__host__ __device__ inline size_t kd_ws_stride(int n) {
+    return a16(sizeof(double) * n) + a16(sizeof(uint32_t) * n) + a16(8 * (size_t)n) + 256;
+}
+__host__ __device__ inline long long kd_row_stride(int n) { return ((long long)n + 2 + 7) & ~7ll; }
 
 // LDS-only workgroup barrier: outstanding global stores (output rows) stay in flight.
 __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -307,8 +342,10 @@ __device__ inline void kd_relax_list(const uint32_t* wimp, int cnt, int lane, un
     __builtin_amdgcn_wave_barrier();
 }
 
-__device__ inline int kd_next_source(int* ctr, int* slot, int tid) {
-    if (tid == 0) *slot = (int)gridDim.x + atomicAdd(ctr, 1);
+// planned launches (jobs): every job from the queue, in queue order, so a job a workgroup
+// waits on (its seed) was taken earlier by a running workgroup: no residency assumption
+__device__ inline int kd_next_source(int* ctr, int* slot, int tid, bool all_queued = false) {
+    if (tid == 0) *slot = (all_queued ? 0 : (int)gridDim.x) + atomicAdd(ctr, 1);
     __syncthreads();
     const int i = *slot;
     __syncthreads();  // every thread has read it before thread 0 writes the next one
@@ -347,7 +384,9 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
     constexpr int NW = B / 64;
     const bool writer = wid == NW - 1;  // drains parent records; never waits on a global load
     double* relv = reinterpret_cast<double*>(ws + (size_t)blockIdx.x * ws_stride);
-    uint32_t* wpr = reinterpret_cast<uint32_t*>(ws + (size_t)blockIdx.x * ws_stride + a16(sizeof(double) * n));
+    uint32_t* const wslice = reinterpret_cast<uint32_t*>(ws + (size_t)blockIdx.x * ws_stride + a16(sizeof(double) * n));
+    uint2* const evl = reinterpret_cast<uint2*>(ws + (size_t)blockIdx.x * ws_stride + a16(sizeof(double) * n) +
+                                                a16(sizeof(uint32_t) * n));
 #ifdef SHD_STAMPS
     if (tid < 32) sm->acc[tid] = 0;
     __syncthreads();
@@ -357,22 +396,67 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
     // sources: one each to start, then from a queue, so workgroups that drew cheap
     // sources take more and the launch ends within about one source of the mean
     // (a static stride ended with the workgroups holding ceil(ns / grid) sources)
-    for (int i = blockIdx.x; i < ns; i = kd_next_source(g.next, &sm->next, tid)) {
-        const int s = src[i];
-        if (s < 0 || s >= n) {
+    const bool queued = g.jobs != nullptr;
+    for (int jb = queued ? kd_next_source(g.next, &sm->next, tid, true) : (int)blockIdx.x; jb < ns;
+         jb = kd_next_source(g.next, &sm->next, tid, queued)) {
+        int i = jb, s, seed = -1, store = -1, su = -1;
+        unsigned wsu = 0, rsu = 0;
+        if (g.jobs) {
+            const KDJob J = g.jobs[jb];
+            i = J.row; s = J.s; seed = J.seed; store = J.store; su = J.u;
+            wsu = (unsigned)J.wr & 0xFFFFu; rsu = (unsigned)J.wr >> 16;
+        } else s = src[jb];
+        if (s < 0 || s >= n || (seed >= 0 && (su < 0 || su >= n))) {
             if (tid == 0) raise_err(err, SHD_ROUTE_EINVAL);
             continue;
         }
+        // the row kept for later seeds is this source's own parent-record array
+        uint32_t* const wpr = store >= 0 ? g.prow + (size_t)store * g.rstride : wslice;
+        const uint16_t* const sdrow = seed >= 0 ? g.drow + (size_t)seed * g.rstride : nullptr;
+        const uint32_t* const sprow = seed >= 0 ? g.prow + (size_t)seed * g.rstride : nullptr;
         KD_STAMP(0);
         const double fs = g.vf[s];
         const double cs = isnan(fs) ? 1.0 : 1.0 * fs;
-        for (int v = tid; v < (n + 2) / 2; v += B) reinterpret_cast<uint32_t*>(dist)[v] = 0xFFFFFFFFu;
+    kd_restart:
+        const bool seeded = seed >= 0;
+        if (seeded) {
+            // the seed's row is ready: one relaxed poll of its flag, one agent-scope acquire
+            // (this CU's L1 invalidated), then every wave reads it with plain loads
+            if (tid == 0) {
+                int spin = 0;
+                while (__hip_atomic_load(&g.done[seed], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+                       spin < (1 << 22)) {
+                    __builtin_amdgcn_s_sleep(8);
+                    spin++;
+                }
+                if (spin >= (1 << 22)) raise_err(err, SHD_ROUTE_EDEVICE);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            // D0(v) = w(s,u) + d_u(v), saturating at 0xFFFF (= unreached); entries past n too
+            const uint32_t* sd32 = reinterpret_cast<const uint32_t*>(sdrow);
+            const kd_us2 wv = {(unsigned short)wsu, (unsigned short)wsu};
+#pragma unroll 4
+            for (int v = tid; v < (n + 2) / 2; v += B) {
+                uint32_t x = 0xFFFFFFFFu;
+                if (2 * v < n) {
+                    const kd_us2 d2 = __builtin_bit_cast(kd_us2, sd32[v]);
+                    x = __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(d2, wv));
+                    if (2 * v + 1 >= n) x |= 0xFFFF0000u;
+                }
+                reinterpret_cast<uint32_t*>(dist)[v] = x;
+            }
+        } else {
+            for (int v = tid; v < (n + 2) / 2; v += B) reinterpret_cast<uint32_t*>(dist)[v] = 0xFFFFFFFFu;
+        }
         for (int k = tid; k < nw; k += B) { pend[k] = 0ull; wmin[k] = 0xFFFFFFFFu; fix[k] = 0ull; }
         for (int q = tid; q < RR; q += B) rrec[q] = make_uint2(0u, 0xFFFFFFFFu);  // phases B/C reuse the area
         if (lane < 2 * KD_P) wmark[lane] = 0u;  // phase C reuses it
         if (tid == 0) {
             sm->gmin[0] = sm->gmin[1] = 0xFFFFFFFFu;
             sm->rtail = sm->rdone = 0;
+            sm->nev = 0; sm->evovf = 0;
             wpr[s] = KD_SRC_MARK;
         }
         lds_barrier();
@@ -394,6 +478,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         unsigned T = delta;
         int par = 0;
         const int ncomp = NW - 1;
+        int wnev = 0;  // writer wave: tie events stored so far
 #ifdef SHD_STAMPS
         unsigned long long kd_t = 0;
 #endif
@@ -468,6 +553,25 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             KD_ACC(8);
             if (!writer) {
                 // ---- compute wave: pull slices until the round drains ----------------
+                // records {x, y} for the writer's ring from the lanes in `m` (wave-uniform
+                // call): one reservation, then one 64-bit LDS write per record, so the
+                // writer never sees half a record
+                auto push_rec = [&](unsigned long long m, bool mine, uint32_t x, uint32_t y) __attribute__((always_inline)) {
+                    const int nr = __popcll(m);
+                    int rb = 0;
+                    if (lane == 0) {
+                        rb = atomicAdd(&sm->rtail, nr);
+                        for (int w8 = 0; rb + nr - __hip_atomic_load(&sm->rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > RR
+                                         && w8 < (1 << 22); w8++)
+                            __builtin_amdgcn_s_sleep(1);
+                    }
+                    rb = __builtin_amdgcn_readfirstlane(rb);
+                    if (mine) {
+                        const int slot = (rb + __popcll(m & (upto >> 1))) & (RR - 1);
+                        *reinterpret_cast<volatile unsigned long long*>(&rrec[slot]) =
+                            (unsigned long long)x | ((unsigned long long)y << 32);
+                    }
+                };
                 int spins = 0;
                 for (;;) {
                     int h = 0, nn = 0;
@@ -629,6 +733,17 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                             // (255 - w) << 24 | v << 8 | ridx is one byte permutation of ~rec / rec
                             if (g.fused && valid && dv + w == odu)
                                 atomicMin(&wkey[W.odo[p] >> 16], __builtin_amdgcn_perm(~W.rx[p], W.rx[p], 0x06010003u));
+                            if (seeded) {
+                                // tie event: the owner x is a tight in-neighbour of v (x improved:
+                                // only improved vertices are expanded); v's parent is settled
+                                // after phase A if v keeps its seeded distance
+                                const bool tie = valid && nd == dv;
+                                const unsigned long long tm = __ballot(tie);
+                                if (tm) {
+                                    const int pv = __shfl(u, (int)(W.odo[p] >> 16), 64);
+                                    push_rec(tm, tie, (uint32_t)pv | ((W.rx[p] >> 24) << 16) | (w << 24), v | KD_EVTAG);
+                                }
+                            }
                         };
                         // the list holds KD_IMP >= 3 x 64 entries: a flush check every second step
                         static_assert(KD_IMP >= 192, "two steps between flush checks");
@@ -682,22 +797,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                             prec = ((kk >> 8) & 0xFFFFu) | ((kk & 0xFFu) << 16);
                     }
                     const unsigned long long rm = __ballot(hasrec);
-                    const int nr = __popcll(rm);
-                    if (nr) {
-                        int rb = 0;
-                        if (lane == 0) {
-                            rb = atomicAdd(&sm->rtail, nr);
-                            for (int w8 = 0; rb + nr - __hip_atomic_load(&sm->rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > RR
-                                             && w8 < (1 << 22); w8++)
-                                __builtin_amdgcn_s_sleep(1);
-                        }
-                        rb = __builtin_amdgcn_readfirstlane(rb);
-                        if (hasrec) {  // one 64-bit LDS write: the writer never sees half a record
-                            const int slot = (rb + __popcll(rm & (upto >> 1))) & (RR - 1);
-                            *reinterpret_cast<volatile unsigned long long*>(&rrec[slot]) =
-                                (unsigned long long)prec | ((unsigned long long)((uint32_t)u | (du0 << 16)) << 32);
-                        }
-                    }
+                    if (rm) push_rec(rm, hasrec, prec, (uint32_t)u | (du0 << 16));
                     if (lane == 0) atomicSub(&sm->busy, 1);
 #ifdef SHD_STAMPS
                     if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[24] += t_ - ks0; sm->acc[26] += 1; }
@@ -713,11 +813,12 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     if (rt > rd) {
                         // up to 4 x 64 records per pass
                         const int k = min(4 * 64, rt - rd);
-                        int uu[4];
+                        int uu[4], ev[4];
                         uint32_t xx[4];
 #pragma unroll
                         for (int q = 0; q < 4; q++) {
                             uu[q] = -1;
+                            ev[q] = -1;
                             xx[q] = KD_NONE;
                             if (q * 64 + lane < k) {
                                 const int slot = (rd + q * 64 + lane) & (RR - 1);
@@ -730,7 +831,9 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                                 const uint32_t x = (uint32_t)rv, y = (uint32_t)(rv >> 32);
                                 *sp = 0xFFFFFFFF00000000ull;
                                 const int u = (int)(y & 0xFFFFu);
-                                if (y != 0xFFFFFFFFu && ld16(dist, u) == (y >> 16)) {  // from u's latest expansion
+                                if (y != 0xFFFFFFFFu && (y & KD_EVTAG) == KD_EVTAG) {  // tie event (seeded rows)
+                                    ev[q] = u; xx[q] = x;
+                                } else if (y != 0xFFFFFFFFu && ld16(dist, u) == (y >> 16)) {  // from u's latest expansion
                                     const unsigned long long bit = 1ull << (u & 63);
                                     if (x != KD_NONE) { uu[q] = u; xx[q] = x; atomicAnd(&fix[u >> 6], ~bit); }
                                     else atomicOr(&fix[u >> 6], bit);
@@ -740,6 +843,15 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
 #pragma unroll
                         for (int q = 0; q < 4; q++)  // records are parent | ridx << 16
                             if (uu[q] >= 0) wpr[uu[q]] = xx[q];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {  // tie events -> the slice's event list
+                            const unsigned long long em = __ballot(ev[q] >= 0);
+                            if (em) {
+                                const int at = wnev + __popcll(em & (upto >> 1));
+                                if (ev[q] >= 0 && at < g.evcap) evl[at] = make_uint2(xx[q], (uint32_t)ev[q]);
+                                wnev += __popcll(em);
+                            }
+                        }
                         rd += k;
                         __builtin_amdgcn_wave_barrier();
                         if (lane == 0) __hip_atomic_store(&sm->rdone, rd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -747,8 +859,10 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         continue;
                     }
                     if (__hip_atomic_load(&sm->nexit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == ncomp &&
-                        __hip_atomic_load(&sm->rtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == rd)
+                        __hip_atomic_load(&sm->rtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == rd) {
+                        if (lane == 0) sm->nev = wnev;
                         break;
+                    }
                     if (++spins > (1 << 22)) { if (lane == 0) raise_err(err, SHD_ROUTE_EDEVICE); break; }
                     __builtin_amdgcn_s_sleep(1);
                 }
@@ -759,6 +873,68 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         }
         wait_stores();  // the writer's records land before phase B rewrites fixed-up vertices
         lds_barrier();
+        if (seeded) {
+            // ---- A': parents of the vertices that kept D0 ------------------------------
+            const int nev = sm->nev;
+            if (nev > g.evcap) {  // (uniform) the slice lost events: this row again, unseeded
+                seed = -1;
+                lds_barrier();
+                goto kd_restart;
+            }
+            auto d0 = [&](int v) __attribute__((always_inline)) {
+                return min(0xFFFFu, wsu + (unsigned)sdrow[v]);
+            };
+            // their parent is u's, except u itself, whose parent is s (tight: D0(u) = w(s,u))
+#pragma unroll 4
+            for (int v = tid; v < n; v += B) {
+                const unsigned dv = ld16(dist, v), sd = sdrow[v];
+                const uint32_t pr = sprow[v];
+                if (dv == min(0xFFFFu, wsu + sd)) wpr[v] = v == su ? ((uint32_t)s | (rsu << 16)) : pr;
+            }
+            wait_stores();
+            lds_barrier();
+            // ...or a tight improved in-neighbour that wins the tie rule (largest w, then
+            // smallest parent): keys (255 - w) << 24 | parent << 8 | ridx, min over u's
+            // parent and every valid event, through u32 keys in the slice (relv is free)
+            uint32_t* key = reinterpret_cast<uint32_t*>(relv);
+            // event e -> v (-1 if invalid: v improved on D0, or the arc is not tight) + key
+            auto event = [&](int e, int& v, uint32_t& ke) __attribute__((always_inline)) {
+                const uint2 r = evl[e];
+                v = (int)r.y;
+                const int p = (int)(r.x & 0xFFFFu);
+                const unsigned w = r.x >> 24, dv = ld16(dist, v);
+                if (dv != d0(v) || ld16(dist, p) + w != dv) { v = -1; return; }
+                ke = ((0xFFu - w) << 24) | ((uint32_t)p << 8) | ((r.x >> 16) & 0xFFu);
+            };
+            for (int e = tid; e < nev; e += B) {
+                int v; uint32_t ke = 0;
+                event(e, v, ke);
+                if (v >= 0) {  // u's parent (from the copy above) as the starting key
+                    const uint32_t b = wpr[v];
+                    const unsigned pb = b & 0xFFFFu, wb = ld16(dist, v) - ld16(dist, (int)pb);
+                    key[v] = ((0xFFu - wb) << 24) | (pb << 8) | ((b >> 16) & 0xFFu);
+                }
+            }
+            wait_stores();
+            lds_barrier();
+            for (int e = tid; e < nev; e += B) {
+                int v; uint32_t ke = 0;
+                event(e, v, ke);
+                if (v >= 0) atomicMin(&key[v], ke);
+            }
+            wait_stores();
+            lds_barrier();
+            for (int e = tid; e < nev; e += B) {
+                int v; uint32_t ke = 0;
+                event(e, v, ke);
+                if (v >= 0) {
+                    const uint32_t k = __hip_atomic_load(&key[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    wpr[v] = ((k >> 8) & 0xFFFFu) | ((k & 0xFFu) << 16);
+                }
+            }
+            wait_stores();
+            lds_barrier();
+        }
         KD_STAMP(1);
         KD_MARK();
 
@@ -883,9 +1059,20 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             else { Lv = (double)dist[t]; lmin = fmin(lmin, Lv); }
             if (lrow) __builtin_nontemporal_store(Lv, lrow + j);
         }
+        if (store >= 0) {  // this row seeds later ones: keep its distances (u16, incl. the pad)
+            uint32_t* d32 = reinterpret_cast<uint32_t*>(g.drow_out + (size_t)store * g.rstride);
+            for (int k = tid; k < (n + 2) / 2; k += B) d32[k] = reinterpret_cast<const uint32_t*>(dist)[k];
+        }
         wait_stores();  // wpr of phase B visible to the whole workgroup
         if (tid == 0) { sm->deep = 0; sm->rmin = kInfBits; }
         __syncthreads();
+        if (store >= 0 && tid == 0) {
+            // the kept row (distances + parent records) is complete: every wave's stores
+            // drained before the barrier above; release at agent scope, then the flag
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&g.done[store], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         KD_ACC(18);
         // dist is dead: its LDS becomes the parent array
         uint16_t* parv = dist;

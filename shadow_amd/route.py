@@ -52,11 +52,22 @@ class _Info(C.Structure):
     ]
 
 
+class _PlanInfo(C.Structure):
+    _fields_ = [
+        ("rows", C.c_int32), ("seeded", C.c_int32), ("launches", C.c_int32), ("levels", C.c_int32),
+        ("roots", C.c_int32),
+        ("helpers", C.c_int32), ("stored_rows", C.c_int32), ("world", C.c_int32), ("rank", C.c_int32),
+        ("store_bytes", C.c_uint64),
+    ]
+
+
 # every symbol include/shd_route.h declares
 EXPORTS = (
     "shd_route_create", "shd_route_destroy", "shd_route_get_info", "shd_route_strerror",
     "shd_route_rows", "shd_route_rows_async", "shd_route_sync", "shd_route_direct",
     "shd_route_self", "shd_route_min_reduce_async", "shd_route_fw_async",
+    "shd_route_plan_create", "shd_route_plan_destroy", "shd_route_plan_get_info", "shd_route_plan_rows",
+    "shd_route_rows_planned_async",
 )
 
 _lib = None
@@ -92,6 +103,15 @@ def load_library():
     L.shd_route_min_reduce_async.argtypes = [P, P, I64, P, P]
     L.shd_route_fw_async.restype = C.c_int
     L.shd_route_fw_async.argtypes = [P, P, P]
+    L.shd_route_plan_create.restype = C.c_int
+    L.shd_route_plan_create.argtypes = [P, P, I32, I32, I32, C.POINTER(P)]
+    L.shd_route_plan_destroy.argtypes = [P]
+    L.shd_route_plan_get_info.restype = C.c_int
+    L.shd_route_plan_get_info.argtypes = [P, C.POINTER(_PlanInfo)]
+    L.shd_route_plan_rows.restype = C.c_int
+    L.shd_route_plan_rows.argtypes = [P, P]
+    L.shd_route_rows_planned_async.restype = C.c_int
+    L.shd_route_rows_planned_async.argtypes = [P, P, P, I32, I64, U32, P, P, P, P]
     _lib = L
     return L
 
@@ -188,6 +208,50 @@ class RouteEngine:
                                                        C.c_void_p(stream) if stream else None)
         _check(rc, "shd_route_min_reduce_async")
 
+    def plan(self, sources, world: int = 1, rank: int = 0) -> "RoutePlan":
+        return RoutePlan(self, sources, world, rank)
+
     def fw_async(self, d_dist, stream=None):
         _check(load_library().shd_route_fw_async(self._h, C.c_void_p(d_dist.data_ptr()),
                                                  C.c_void_p(stream) if stream else None), "shd_route_fw_async")
+
+
+class RoutePlan:
+    """A seeded plan over a source list (shd_route_plan_*): this rank's output rows, the
+    launches that compute them and the device row store.  Keep it for repeated fills."""
+
+    def __init__(self, eng: RouteEngine, sources, world: int = 1, rank: int = 0):
+        L = load_library()
+        self.eng = eng
+        src = np.ascontiguousarray(sources, np.int32)
+        h = C.c_void_p()
+        _check(L.shd_route_plan_create(eng._h, _p(src), len(src), int(world), int(rank), C.byref(h)),
+               "shd_route_plan_create")
+        self._h = h
+        inf = _PlanInfo()
+        _check(L.shd_route_plan_get_info(self._h, C.byref(inf)), "shd_route_plan_get_info")
+        self.info = {k: getattr(inf, k) for k, _ in _PlanInfo._fields_}
+        pos = np.empty(max(1, self.info["rows"]), np.int32)
+        _check(L.shd_route_plan_rows(self._h, _p(pos)), "shd_route_plan_rows")
+        self.positions = pos[: self.info["rows"]]
+        self.sources = src[self.positions]
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            load_library().shd_route_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def rows_async(self, d_tgt, d_lat, d_rel, d_rowmin, stream=None, dispatch=True, ld=None):
+        nt = int(d_tgt.numel())
+        ld = nt if ld is None else int(ld)
+        ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        rc = load_library().shd_route_rows_planned_async(
+            self.eng._h, self._h, ptr(d_tgt), nt, ld, DISPATCH if dispatch else 0, ptr(d_lat), ptr(d_rel),
+            ptr(d_rowmin), C.c_void_p(stream) if stream else None)
+        _check(rc, "shd_route_rows_planned_async")

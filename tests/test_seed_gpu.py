@@ -1,0 +1,122 @@
+"""GPU parity of seeded KD rows (shd_route_plan_* / sssp_delta.hpp seeded mode).
+
+A seeded row starts from w(s,u) + d_u(v) for a neighbour u whose row is already in the
+row store, and settles the parents of the vertices that keep that distance from u's
+parent records plus the tie events of the expansion.  Everything must stay bit-exact
+against the oracle (engine tie rule), including: many launches (deep seed forests),
+workgroups running many rows back to back (small grid), tie-event lists that overflow
+(the row reruns unseeded), directed graphs (plans fall back to plain rows), and the
+full C3/C4 tables against the committed golden row digests.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from shadow_amd.graph import config
+
+from tests.test_kd_gpu import _graph
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture
+def kd(monkeypatch):
+    monkeypatch.setenv("SHD_ROUTE_KERNEL", "kd")
+    monkeypatch.setenv("SHD_ROUTE_KDGRID", "7")
+    monkeypatch.delenv("SHD_ROUTE_SEED", raising=False)
+    monkeypatch.delenv("SHD_ROUTE_EVCAP", raising=False)
+    return monkeypatch
+
+
+@pytest.mark.parametrize("evcap", [None, "0", "2"])
+@pytest.mark.parametrize("name", ["ba400", "ties", "chain", "c2"])
+def test_seeded_rows_bitexact(oracle_mod, kd, name, evcap):
+    from shadow_amd import route
+    if evcap is not None:
+        kd.setenv("SHD_ROUTE_EVCAP", evcap)
+    g = _graph(name)
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 4
+    T = g.targets()
+    S = T if name != "c2" else T[::3]
+    plan = eng.plan(S)
+    assert plan.info["seeded"] == 1 and plan.info["levels"] > 2 and plan.info["stored_rows"] > 0
+    assert np.array_equal(plan.positions, np.arange(len(S)))
+    lat, rel, mn = eng.rows(S, T, dispatch=False)  # host rows take the seeded plan
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(S, T, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(rel, orel)
+    assert np.array_equal(mn, olat.min(axis=1))
+
+
+def test_seeded_equals_unseeded_shuffled_sources(kd):
+    """Sources in arbitrary order with repeats: seeding picks seeds among the listed rows."""
+    from shadow_amd import route
+    g = _graph("ba400")
+    T = g.targets()
+    rng = np.random.default_rng(3)
+    S = np.concatenate([rng.permutation(T), T[:17]]).astype(np.int32)
+    lat, rel, mn = route.RouteEngine(g).rows(S, T, dispatch=False)
+    kd.setenv("SHD_ROUTE_SEED", "0")
+    lat0, rel0, mn0 = route.RouteEngine(g).rows(S, T, dispatch=False)
+    assert np.array_equal(lat, lat0) and np.array_equal(rel, rel0) and np.array_equal(mn, mn0)
+
+
+def test_directed_plan_falls_back(oracle_mod, kd):
+    from shadow_amd import route
+    g = _graph("dir")
+    eng = route.RouteEngine(g)
+    T = g.targets()
+    plan = eng.plan(T)
+    assert plan.info["seeded"] == 0 and plan.info["levels"] == 1
+    lat, rel, _ = eng.rows(T, T, dispatch=False)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(T, T, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat) and np.array_equal(rel, orel)
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, np.float64).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("cfg", ["c3", "c4"])
+def test_full_table_planned_matches_golden(monkeypatch, cfg):
+    """The whole C3 (9.3k x 9.3k) / C4 (50k x 50k, 40 GB) table by one seeded plan in
+    HBM; the golden rows (oracle digests) and the row minima must match, and the planned
+    table's runahead min must equal the golden one."""
+    import torch
+    from shadow_amd import route
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    monkeypatch.delenv("SHD_ROUTE_KDGRID", raising=False)
+    monkeypatch.delenv("SHD_ROUTE_SEED", raising=False)
+    dig = json.load(open(os.path.join(GOLD, "rows_digests.json")))[cfg]
+    g = config(cfg)
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 4
+    T = g.targets()
+    plan = eng.plan(T)
+    assert plan.info["seeded"] == 1
+    dev = torch.device("cuda", 0)
+    d_tgt = torch.from_numpy(T.astype(np.int32)).to(dev)
+    d_lat = torch.empty((len(T), len(T)), dtype=torch.float64, device=dev)
+    d_rel = torch.empty_like(d_lat)
+    d_min = torch.empty(len(T), dtype=torch.float64, device=dev)
+    plan.rows_async(d_tgt, d_lat, d_rel, d_min, dispatch=False)
+    eng.sync()
+    row_of = {int(v): i for i, v in enumerate(T)}
+    idx = torch.tensor([row_of[r["src"]] for r in dig["rows"]], device=dev)
+    lat = d_lat[idx].cpu().numpy()
+    rel = d_rel[idx].cpu().numpy()
+    mn = d_min[idx].cpu().numpy()
+    for k, r in enumerate(dig["rows"]):
+        assert _sha(lat[k]) == r["lat_sha"] and _sha(rel[k]) == r["rel_sha"], (cfg, r["src"])
+        assert mn[k] == r["row_min"]
+    # undirected integer latencies: the latency table is symmetric (spot-check a block)
+    blk = d_lat[:512, :512].cpu().numpy()
+    assert np.array_equal(blk, blk.T)
+    del d_lat, d_rel
+    torch.cuda.empty_cache()

@@ -1,8 +1,10 @@
 // engine.hip -- host side of the routing engine (C-ABI in include/shd_route.h).
 #include "common.hpp"
 
+#include <array>
 #include <map>
 #include <memory>
+#include <queue>
 #include <thread>
 #include "sssp_f64.hpp"
 #include "sssp_k32.hpp"
@@ -1096,60 +1098,136 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     auto P = std::make_unique<shd_route_plan>();
     P->c = c; P->world = world; P->rank = rank; P->ns_all = ns;
     const int n = c->n;
-    // rows of this rank: a contiguous block of the caller's list (world 1: all of it)
-    const int blk = (ns + world - 1) / world, lo = std::min(ns, rank * blk), hi = std::min(ns, lo + blk);
-    for (int p = lo; p < hi; p++) P->row_pos.push_back(p);
-    const int nr = (int)P->row_pos.size();
     const char* env = getenv("SHD_ROUTE_SEED");
     const bool want = (!env || atoi(env) != 0) && c->sel == 4 && c->kd_fused && !c->complete && !c->prefer_direct &&
-                      nr >= 2 && !c->h_row.empty();
-    std::vector<KDJob> jobs;
+                      ns >= 2 && !c->h_row.empty();
+    // closeness rank of every vertex: a row may only be seeded by rows of smaller rank
+    std::vector<int> rk;
     if (want) {
         ensure_close(c);
-        // rank of every vertex by (closeness, id): a row may only be seeded by a row of
-        // smaller rank, so the seed graph is a forest and its depth orders the launches
-        std::vector<int> ord(n), rk(n);
+        std::vector<int> ord(n);
+        rk.resize(n);
         std::iota(ord.begin(), ord.end(), 0);
         std::sort(ord.begin(), ord.end(), [&](int a, int b) {
             return c->close[a] != c->close[b] ? c->close[a] < c->close[b] : a < b;
         });
         for (int q = 0; q < n; q++) rk[ord[q]] = q;
-        std::vector<int> first(n, -1);  // first row of each source vertex
-        for (int r = 0; r < nr; r++) if (first[src[P->row_pos[r]]] < 0) first[src[P->row_pos[r]]] = r;
-        // rows in rank order: a row's seed (smaller rank) is settled before it
-        std::vector<int> rows(nr), lvl(nr, 0), slot(nr, -1), seedrow(nr, -1), su(nr, -1), wr(nr, 0);
-        std::iota(rows.begin(), rows.end(), 0);
-        std::sort(rows.begin(), rows.end(), [&](int a, int b) {
-            const int va = src[P->row_pos[a]], vb = src[P->row_pos[b]];
-            return rk[va] != rk[vb] ? rk[va] < rk[vb] : a < b;
+    }
+    auto by_rank = [&](std::vector<int>& v) {  // positions by (vertex rank, position)
+        std::sort(v.begin(), v.end(), [&](int a, int b) {
+            return rk[src[a]] != rk[src[b]] ? rk[src[a]] < rk[src[b]] : a < b;
         });
-        // options: the `roots` most central rows start unseeded (fills the machine at the
-        // start of the launch), and seed chains are at most `depth` rows long
-        int nroot_min = 0, depth = 1 << 30;
+    };
+    // the best seeds of position p among the positions marked in `avail` (first[v]: the
+    // available position of vertex v): neighbours of smaller rank by w(s,u) + closeness(u)
+    std::vector<std::pair<double, int>> cand;
+    auto best_seeds = [&](int p, const std::vector<int>& first, int k, int* arc_out) {
+        const int s = src[p];
+        cand.clear();
+        for (int a = c->h_row[s]; a < c->h_row[s + 1]; a++) {
+            const int u = c->h_col[a];
+            if (u == s || first[u] < 0 || rk[u] >= rk[s]) continue;
+            cand.push_back({c->h_w[a] + c->close[u], a});
+        }
+        std::sort(cand.begin(), cand.end(), [&](const std::pair<double, int>& x, const std::pair<double, int>& y) {
+            return x.first != y.first ? x.first < y.first : c->h_col[x.second] < c->h_col[y.second];
+        });
+        int m = 0;
+        for (const auto& cd : cand) {
+            if (m == k) break;
+            bool dup = false;  // (a multigraph would list u twice)
+            for (int q = 0; q < m; q++) dup = dup || c->h_col[arc_out[q]] == c->h_col[cd.second];
+            if (!dup) arc_out[m++] = cd.second;
+        }
+        return m;
+    };
+    // ---- which positions this rank computes: output rows + helper rows ----------------
+    std::vector<int> job_pos, job_row;
+    if (!want || world == 1) {
+        // a contiguous block of the caller's list (world 1: all of it)
+        const int blk = (ns + world - 1) / world, lo = std::min(ns, rank * blk), hi = std::min(ns, lo + blk);
+        for (int p = lo; p < hi; p++) { P->row_pos.push_back(p); job_pos.push_back(p); job_row.push_back(p - lo); }
+    } else {
+        // Multi-GPU: partition the seed forest (each row's best seed) so that a rank holds
+        // whole subtrees: every seed a row needs is then on its own rank.  The forest's
+        // top levels (T) are computed on every rank (helper rows where not output there);
+        // the subtrees hanging below T go to ranks by size (largest first, least loaded).
+        std::vector<int> first(n, -1), pos(ns);
+        for (int p = 0; p < ns; p++) if (first[src[p]] < 0) first[src[p]] = p;
+        std::iota(pos.begin(), pos.end(), 0);
+        by_rank(pos);
+        std::vector<int> fpar(ns, -1), flvl(ns, 0), sub(ns, 1);
+        int maxl = 0;
+        for (int p : pos) {
+            int a;
+            if (best_seeds(p, first, 1, &a)) { fpar[p] = first[c->h_col[a]]; flvl[p] = flvl[fpar[p]] + 1; }
+            maxl = std::max(maxl, flvl[p]);
+        }
+        for (int q = ns - 1; q >= 0; q--) if (fpar[pos[q]] >= 0) sub[fpar[pos[q]]] += sub[pos[q]];
+        // cut level: the shallowest whose subtrees all fit a quarter of a rank's share
+        const int cap = std::max(1, ns / (4 * world));
+        int L = 1;
+        for (; L <= maxl; L++) {
+            int mx = 0;
+            for (int p = 0; p < ns; p++) if (flvl[p] == L) mx = std::max(mx, sub[p]);
+            if (mx <= cap) break;
+        }
+        std::vector<int> top, heads;
+        for (int p : pos) {
+            if (flvl[p] < L) top.push_back(p);
+            else if (flvl[p] == L) heads.push_back(p);
+        }
+        std::stable_sort(heads.begin(), heads.end(), [&](int a, int b) { return sub[a] > sub[b]; });
+        std::vector<int> owner(ns, -1);
+        std::vector<long long> load(world, 0);
+        auto least = [&]() { return (int)(std::min_element(load.begin(), load.end()) - load.begin()); };
+        for (int h : heads) { const int r = least(); owner[h] = r; load[r] += sub[h]; }
+        for (int p : top) { const int r = least(); owner[p] = r; load[r] += 1; }
+        for (int p : pos) if (owner[p] < 0 && fpar[p] >= 0) owner[p] = owner[fpar[p]];  // (rank order: parent first)
+        // rows of this rank: its share of T, then its subtrees, in rank order; helpers: T
+        for (int p : pos)
+            if (owner[p] == rank) { job_row.push_back((int)P->row_pos.size()); P->row_pos.push_back(p); job_pos.push_back(p); }
+        for (int p : top)
+            if (owner[p] != rank) { job_pos.push_back(p); job_row.push_back(-1); P->nhelpers++; }
+    }
+    const int nj = (int)job_pos.size(), nr = (int)P->row_pos.size();
+    std::vector<KDJob> jobs;
+    if (want && nj >= 2) {
+        std::vector<int> first(n, -1);  // first job of each source vertex
+        for (int j = 0; j < nj; j++) if (first[src[job_pos[j]]] < 0) first[src[job_pos[j]]] = j;
+        std::vector<int> jpos_of(ns, -1);
+        for (int j = 0; j < nj; j++) if (jpos_of[job_pos[j]] < 0) jpos_of[job_pos[j]] = j;
+        // jobs in rank order: a job's seeds (smaller rank) are settled before it
+        std::vector<int> order(job_pos);
+        by_rank(order);
+        std::vector<int> lvl(nj, 0), slot(nj, -1), nsd(nj, 0);
+        std::vector<std::array<int, KD_SEEDS>> seedjob(nj), su(nj), wr(nj);
+        // options: seeds per row (1..KD_SEEDS), the `roots` most central rows start
+        // unseeded, and seed chains are at most `depth` rows long
+        int kseeds = 2, nroot_min = 0, depth = 1 << 30;
+        if (const char* e = getenv("SHD_ROUTE_SEEDS")) kseeds = std::max(1, std::min(KD_SEEDS, atoi(e)));
         if (const char* e = getenv("SHD_ROUTE_SEED_ROOTS")) nroot_min = std::max(0, atoi(e));
         if (const char* e = getenv("SHD_ROUTE_SEED_DEPTH")) depth = std::max(1, atoi(e));
-        // seed of each row: the neighbour u (a row of this rank, smaller rank, level below
-        // the cap) minimising w(s,u) + closeness(u), i.e. the likely gateway of most
-        // shortest paths from s
+        // seeds of each job: the kseeds neighbours u (jobs of this rank, smaller rank, level
+        // below the cap) with the smallest w(s,u) + closeness(u), i.e. the likely gateways
+        // of most shortest paths from s
+        std::vector<int> fl(n, -1);  // first job of a vertex, once its level is below the cap
         int nlev = 1, q = 0;
-        for (int r : rows) {
-            const int s = src[P->row_pos[r]];
-            double best = INFINITY;
-            if (q++ >= nroot_min)
-                for (int a = c->h_row[s]; a < c->h_row[s + 1]; a++) {
-                    const int u = c->h_col[a];
-                    if (u == s || first[u] < 0 || rk[u] >= rk[s] || lvl[first[u]] + 1 >= depth) continue;
-                    const double sc = c->h_w[a] + c->close[u];
-                    if (sc < best || (sc == best && u < su[r])) {
-                        best = sc; su[r] = u; seedrow[r] = first[u];
-                        wr[r] = (int)c->h_w[a] | ((int)c->h_ridx[a] << 16);
-                    }
-                }
-            if (seedrow[r] >= 0) {
-                lvl[r] = lvl[seedrow[r]] + 1;
-                if (slot[seedrow[r]] < 0) slot[seedrow[r]] = P->nslots++;
-            } else P->nroots++;
-            nlev = std::max(nlev, lvl[r] + 1);
+        for (int p : order) {
+            const int j = jpos_of[p];
+            int arcs[KD_SEEDS];
+            const int m = q++ >= nroot_min ? best_seeds(p, fl, kseeds, arcs) : 0;
+            for (int k = 0; k < m; k++) {
+                const int a = arcs[k], u = c->h_col[a], sj = first[u];
+                seedjob[j][k] = sj; su[j][k] = u;
+                wr[j][k] = (int)c->h_w[a] | ((int)c->h_ridx[a] << 16);
+                lvl[j] = std::max(lvl[j], lvl[sj] + 1);
+                if (slot[sj] < 0) slot[sj] = P->nslots++;
+            }
+            nsd[j] = m;
+            if (!m) P->nroots++;
+            nlev = std::max(nlev, lvl[j] + 1);
+            if (first[src[p]] == j && lvl[j] + 1 < depth) fl[src[p]] = p;
         }
         const long long rs = kd_row_stride(n);
         P->store_bytes = (uint64_t)P->nslots * (uint64_t)rs * 6u;
@@ -1158,15 +1236,49 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                   hipMalloc((void**)&P->d_prow, sizeof(uint32_t) * (size_t)rs * P->nslots) == hipSuccess;
         if (ok) {
             std::vector<int> cnt(nlev + 1, 0);
-            for (int r = 0; r < nr; r++) cnt[lvl[r] + 1]++;
+            for (int j = 0; j < nj; j++) cnt[lvl[j] + 1]++;
             for (int k = 0; k < nlev; k++) cnt[k + 1] += cnt[k];
             P->lvl_off = cnt;
-            jobs.resize(nr);
-            for (int r = 0; r < nr; r++) {  // rows of a level in row order
-                KDJob& J = jobs[cnt[lvl[r]]++];
-                J.row = r; J.s = src[P->row_pos[r]];
-                J.seed = seedrow[r] >= 0 ? slot[seedrow[r]] : -1;
-                J.store = slot[r]; J.u = su[r]; J.wr = wr[r]; J.pad0 = J.pad1 = 0;
+            // queue order: list scheduling of the seed DAG over the launch's workgroups with
+            // estimated row times (a root ~3.4x a seeded row; a kept row's flag at ~0.7 of
+            // it): each workgroup, when free, takes the row whose seeds' flags are estimated
+            // earliest.  A row still follows all of its seeds in the queue (no deadlock),
+            // but rows no longer wait at every level boundary for seeds just started.
+            const int W = std::max(1, c->kd_slots);
+            std::vector<std::vector<int>> dep(nj);
+            std::vector<int> left(nj);
+            for (int j = 0; j < nj; j++) {
+                left[j] = nsd[j];
+                for (int k = 0; k < nsd[j]; k++) dep[seedjob[j][k]].push_back(j);
+            }
+            std::vector<double> ready(nj, 0.0);
+            typedef std::pair<double, int> DI;
+            std::priority_queue<DI, std::vector<DI>, std::greater<DI>> cq, free_at;
+            for (int j = 0; j < nj; j++) if (!nsd[j]) cq.push({0.0, j});
+            for (int w = 0; w < W; w++) free_at.push({0.0, w});
+            std::vector<int> qorder;
+            qorder.reserve(nj);
+            while (!cq.empty()) {
+                const DI f = free_at.top(); free_at.pop();
+                const DI jr = cq.top(); cq.pop();
+                const int j = jr.second;
+                const double t = nsd[j] ? 1.0 : 3.4, start = std::max(f.first, jr.first);
+                free_at.push({start + t, f.second});
+                qorder.push_back(j);
+                for (int d : dep[j]) {
+                    ready[d] = std::max(ready[d], start + 0.7 * t);
+                    if (--left[d] == 0) cq.push({ready[d], d});
+                }
+            }
+            jobs.resize(nj);
+            int qi = 0;
+            for (int j : qorder) {
+                KDJob& J = jobs[qi++];
+                std::memset(&J, 0, sizeof(J));
+                J.row = job_row[j]; J.s = src[job_pos[j]]; J.store = slot[j]; J.nseed = nsd[j];
+                for (int k = 0; k < nsd[j]; k++) {
+                    J.seed[k] = slot[seedjob[j][k]]; J.u[k] = su[j][k]; J.wr[k] = wr[j][k];
+                }
             }
             P->seeded = 1;
         } else {
@@ -1175,7 +1287,6 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             P->nslots = 0; P->nroots = 0; P->store_bytes = 0;
         }
     }
-    int rc = SHD_ROUTE_OK;
     if (P->seeded) {
         if (hipMalloc((void**)&P->d_jobs, sizeof(KDJob) * jobs.size()) != hipSuccess ||
             hipMalloc((void**)&P->d_next, sizeof(int) * (1 + (size_t)P->nslots)) != hipSuccess)
@@ -1183,6 +1294,8 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         if (hipMemcpy(P->d_jobs, jobs.data(), sizeof(KDJob) * jobs.size(), hipMemcpyHostToDevice) != hipSuccess)
             return SHD_ROUTE_EDEVICE;
     } else {
+        // plain rows (the helpers of an unseeded multi-GPU plan are not needed)
+        P->nhelpers = 0;
         std::vector<int32_t> sv(std::max(nr, 1), 0);
         for (int r = 0; r < nr; r++) sv[r] = src[P->row_pos[r]];
         if (hipMalloc((void**)&P->d_src, sizeof(int32_t) * sv.size()) != hipSuccess) return SHD_ROUTE_ENOMEM;
@@ -1191,7 +1304,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         P->nroots = nr;
     }
     *out = P.release();
-    return rc;
+    return SHD_ROUTE_OK;
 }
 
 void shd_route_plan_destroy(shd_route_plan_t* P) {
@@ -1236,7 +1349,7 @@ int shd_route_rows_planned_async(shd_route_t* c, const shd_route_plan_t* P, cons
     k.drow = P->d_drow; k.drow_out = P->d_drow; k.prow = P->d_prow; k.rstride = kd_row_stride(c->n);
     k.jobs = P->d_jobs;
     k.done = P->d_next + 1;
-    return kd_launch(c, k, P->d_next, nullptr, nr, d_tgt, nt, ld, d_lat, d_rel, d_row_min, st);
+    return kd_launch(c, k, P->d_next, nullptr, P->lvl_off.back(), d_tgt, nt, ld, d_lat, d_rel, d_row_min, st);
 }
 
 }  // extern "C"

@@ -75,15 +75,22 @@ constexpr uint32_t KD_SRC_MARK = 0xFFFFFFFEu;  // parent record of the source it
 // also kept D0) plus tight arcs from improved vertices, so the parent is the better
 // (engine tie rule) of p_u(v) and the tight improved in-neighbours, which the
 // expansion reports as tie events (dist[x] + w == dist[v], found by the same reads).
+// Up to KD_SEEDS seeds per row: D0(v) = min_j w(s,u_j) + d_{u_j}(v) is still consistent
+// (a min of consistent labellings), and a vertex keeping D0 takes the best (tie rule) of
+// the parents p_{u_j}(v) of the seeds that attain the min, and of its tie events.  Two
+// seeds leave 3-4% of the vertices to improve on C3/C4 (one seed: 14-20%).
+constexpr int KD_SEEDS = 2;
 struct KDJob {
-    int row;    // output row
-    int s;      // source vertex
-    int seed;   // row-store slot of the seed's row, -1 = unseeded (a root)
-    int store;  // row-store slot this row is kept in for later seeds, -1 = not kept
-    int u;      // seed vertex (a neighbour of s)
-    int wr;     // w(s,u) | ridx(s,u) << 16
-    int pad0, pad1;
+    int row;               // output row
+    int s;                 // source vertex
+    int store;             // row-store slot this row is kept in for later seeds, -1 = not kept
+    int nseed;             // seeds used (0 = unseeded: a root)
+    int seed[KD_SEEDS];    // row-store slots of the seeds' rows
+    int u[KD_SEEDS];       // seed vertices (neighbours of s)
+    int wr[KD_SEEDS];      // w(s,u) | ridx(s,u) << 16
+    int pad[16 - 4 - 3 * KD_SEEDS];
 };
+static_assert(sizeof(KDJob) == 64, "one 64-byte job record");
 constexpr uint32_t KD_EVTAG = 0xFFFF0000u;  // ring record y of a tie event: v | KD_EVTAG
 typedef unsigned short kd_us2 __attribute__((ext_vector_type(2)));
 
@@ -129,7 +136,7 @@ struct DevDelta {
 #define KD_COUNT(slot, x) do { if (lane == 0 && (x)) atomicAdd(&sm->acc[slot], (unsigned long long)(x)); } while (0)
 #define KD_MARK() do { if (tid == 0) kd_t = __builtin_amdgcn_s_memtime(); } while (0)
 #define KD_ACC(slot) do { if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[slot] += t_ - kd_t; kd_t = t_; } } while (0)
-#define KD_FLUSH() do { lds_barrier(); if (g.dbg) for (int q_ = tid; q_ < 32; q_ += B) g.dbg[(size_t)i * 32 + q_] = sm->acc[q_]; lds_barrier(); if (tid < 32) sm->acc[tid] = 0; lds_barrier(); } while (0)
+#define KD_FLUSH() do { lds_barrier(); if (g.dbg && i >= 0) for (int q_ = tid; q_ < 32; q_ += B) g.dbg[(size_t)i * 32 + q_] = sm->acc[q_]; lds_barrier(); if (tid < 32) sm->acc[tid] = 0; lds_barrier(); } while (0)
 #else
 #define KD_ACCP nullptr
 #define KD_STAMP(slot) do { } while (0)
@@ -152,6 +159,8 @@ struct KDSmall {
     int next;           // the workgroup's next source index
     int nev;            // seeded: tie events the writer wave stored
     int evovf;          // seeded: more tie events than the slice holds (rerun unseeded)
+    KDJob job;          // the current job (kept in LDS: read where needed, not held in
+                        // registers across phase A, whose expansion needs all of them)
 #ifdef SHD_STAMPS
     unsigned long long acc[32];
 #endif
@@ -200,11 +209,12 @@ constexpr int KD_RR = 512;  // parent-record ring slots (1024-thread workgroups;
 template <int B>
 constexpr int kd_rr() { return B >= 1024 ? KD_RR : 256; }
 
-// per-workgroup HBM slice: relv f64[n] | wpr u32[n], the parent record of every vertex:
-// parent | ridx << 16 of the parent arc (KD_SRC_MARK for the source) | tie events
+// per-workgroup HBM slice: relv f64[n] | wpr u32[n + 8], the parent record of every vertex:
+// parent | ridx << 16 (| w << 24, packed arcs) of the parent arc (KD_SRC_MARK for the source)
+// | tie events
 // {p | ridx << 16 | w << 24, v} x n (seeded rows).  Seeded rows use relv as u32 keys.
 __host__ __device__ inline size_t kd_ws_stride(int n) {
-    return a16(sizeof(double) * n) + a16(sizeof(uint32_t) * n) + a16(8 * (size_t)n) + 256;
+    return a16(sizeof(double) * n) + a16(sizeof(uint32_t) * (n + 8)) + a16(8 * (size_t)n) + 256;
 }
 __host__ __device__ inline long long kd_row_stride(int n) { return ((long long)n + 2 + 7) & ~7ll; }
 
@@ -287,6 +297,9 @@ __device__ inline void kd_bpermute16(const int own[8], int x, int y, int ob[8], 
 }
 
 __device__ inline unsigned ld16(const uint16_t* d, int v) { return d[v]; }
+// component k (a constant after unrolling) of a uint4 without taking its address (an
+// address-taken register array lands in scratch memory)
+__device__ inline uint32_t kd_comp(const uint4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
 // pop up to four set bits of *b (lowest first) into v[] as vertex ids of word k (-1 = none)
 __device__ inline void pop4(unsigned long long* b, int k, int v[4]) {
@@ -344,6 +357,24 @@ __device__ inline void kd_relax_list(const uint32_t* wimp, int cnt, int lane, un
 
 // planned launches (jobs): every job from the queue, in queue order, so a job a workgroup
 // waits on (its seed) was taken earlier by a running workgroup: no residency assumption
+
+// the current job's seeds, from its LDS copy (wave-uniform: scalar registers)
+#define SEED_VIEW()                                                                                   \
+    const int nseed = __builtin_amdgcn_readfirstlane(sm->job.nseed);                                   \
+    int su[KD_SEEDS], sslot[KD_SEEDS];                                                                 \
+    unsigned wsu[KD_SEEDS], rsu[KD_SEEDS];                                                             \
+    const uint16_t* sdrow[KD_SEEDS];                                                                   \
+    const uint32_t* sprow[KD_SEEDS];                                                                   \
+    _Pragma("unroll") for (int q_ = 0; q_ < KD_SEEDS; q_++) {                                          \
+        const int sl_ = __builtin_amdgcn_readfirstlane(q_ < nseed ? sm->job.seed[q_] : 0);             \
+        const unsigned wr_ = (unsigned)__builtin_amdgcn_readfirstlane(q_ < nseed ? sm->job.wr[q_] : 0); \
+        su[q_] = __builtin_amdgcn_readfirstlane(q_ < nseed ? sm->job.u[q_] : -1);                      \
+        sslot[q_] = sl_; wsu[q_] = wr_ & 0xFFFFu; rsu[q_] = wr_ >> 16;                                 \
+        sdrow[q_] = g.drow + (size_t)sl_ * g.rstride;                                                  \
+        sprow[q_] = g.prow + (size_t)sl_ * g.rstride;                                                  \
+    }                                                                                                  \
+    (void)sslot; (void)rsu; (void)sprow; (void)su
+
 __device__ inline int kd_next_source(int* ctr, int* slot, int tid, bool all_queued = false) {
     if (tid == 0) *slot = (all_queued ? 0 : (int)gridDim.x) + atomicAdd(ctr, 1);
     __syncthreads();
@@ -378,6 +409,9 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
     const unsigned delta = (unsigned)g.delta;
     const int qcap = L.qcap;
     const unsigned wmask = g.packed ? 0xFFu : 0xFFFFu;
+    // parent records: parent | ridx << 16 (| w << 24 with packed arcs: the tie-rule key of
+    // a record is then a byte permutation of it)
+    const unsigned rmask = g.packed ? 0xFFu : 0xFFFFu;
     const __amdgpu_buffer_rsrc_t orsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(g.orec), (short)0, g.nnz * 4, 0x00020000);
     const int rc = g.rc;
@@ -386,7 +420,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
     double* relv = reinterpret_cast<double*>(ws + (size_t)blockIdx.x * ws_stride);
     uint32_t* const wslice = reinterpret_cast<uint32_t*>(ws + (size_t)blockIdx.x * ws_stride + a16(sizeof(double) * n));
     uint2* const evl = reinterpret_cast<uint2*>(ws + (size_t)blockIdx.x * ws_stride + a16(sizeof(double) * n) +
-                                                a16(sizeof(uint32_t) * n));
+                                                a16(sizeof(uint32_t) * (n + 8)));
 #ifdef SHD_STAMPS
     if (tid < 32) sm->acc[tid] = 0;
     __syncthreads();
@@ -399,54 +433,112 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
     const bool queued = g.jobs != nullptr;
     for (int jb = queued ? kd_next_source(g.next, &sm->next, tid, true) : (int)blockIdx.x; jb < ns;
          jb = kd_next_source(g.next, &sm->next, tid, queued)) {
-        int i = jb, s, seed = -1, store = -1, su = -1;
-        unsigned wsu = 0, rsu = 0;
-        if (g.jobs) {
-            const KDJob J = g.jobs[jb];
-            i = J.row; s = J.s; seed = J.seed; store = J.store; su = J.u;
-            wsu = (unsigned)J.wr & 0xFFFFu; rsu = (unsigned)J.wr >> 16;
-        } else s = src[jb];
-        if (s < 0 || s >= n || (seed >= 0 && (su < 0 || su >= n))) {
-            if (tid == 0) raise_err(err, SHD_ROUTE_EINVAL);
-            continue;
+        if (tid < 16) {
+            int x;
+            if (g.jobs) x = reinterpret_cast<const int*>(g.jobs + jb)[tid];
+            else x = tid == 0 ? jb : tid == 1 ? src[jb] : tid == 2 ? -1 : 0;  // row, s, store = -1, nseed = 0
+            reinterpret_cast<int*>(&sm->job)[tid] = x;
         }
-        // the row kept for later seeds is this source's own parent-record array
-        uint32_t* const wpr = store >= 0 ? g.prow + (size_t)store * g.rstride : wslice;
-        const uint16_t* const sdrow = seed >= 0 ? g.drow + (size_t)seed * g.rstride : nullptr;
-        const uint32_t* const sprow = seed >= 0 ? g.prow + (size_t)seed * g.rstride : nullptr;
-        KD_STAMP(0);
+        __syncthreads();
+        const int i = sm->job.row, s = sm->job.s;
+        {
+            bool bad = s < 0 || s >= n || sm->job.nseed < 0 || sm->job.nseed > KD_SEEDS;
+            for (int q = 0; q < KD_SEEDS; q++)
+                if (q < sm->job.nseed) bad = bad || sm->job.u[q] < 0 || sm->job.u[q] >= n || sm->job.seed[q] < 0;
+            if (bad) {
+                if (tid == 0) raise_err(err, SHD_ROUTE_EINVAL);
+                continue;
+            }
+        }
+        // parent records: the row kept for later seeds is this source's own array
+        auto wpr_of = [&]() __attribute__((always_inline)) {
+            const int st = __builtin_amdgcn_readfirstlane(sm->job.store);
+            return st >= 0 ? g.prow + (size_t)st * g.rstride : wslice;
+        };
         const double fs = g.vf[s];
         const double cs = isnan(fs) ? 1.0 : 1.0 * fs;
     kd_restart:
-        const bool seeded = seed >= 0;
+#ifdef SHD_STAMPS
+        unsigned long long kd_t = 0;
+#endif
+        KD_MARK();
+#ifdef SHD_STAMPS
+        wait_stores();  // diagnostic: the previous row's output stores, drained here
+        KD_ACC(9);
+#endif
+        const bool seeded = __builtin_amdgcn_readfirstlane(sm->job.nseed) > 0;
         if (seeded) {
-            // the seed's row is ready: one relaxed poll of its flag, one agent-scope acquire
-            // (this CU's L1 invalidated), then every wave reads it with plain loads
+            uint32_t* const wpr = wpr_of();
+            SEED_VIEW();
+            // the seeds' rows are ready: one relaxed poll of each flag, one agent-scope
+            // acquire (this CU's L1 invalidated), then every wave reads them with plain loads
             if (tid == 0) {
-                int spin = 0;
-                while (__hip_atomic_load(&g.done[seed], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-                       spin < (1 << 22)) {
-                    __builtin_amdgcn_s_sleep(8);
-                    spin++;
+#ifdef SHD_STAMPS
+                const unsigned long long w0 = __builtin_amdgcn_s_memtime();
+#endif
+                for (int q = 0; q < nseed; q++) {
+                    int spin = 0;
+                    while (__hip_atomic_load(&g.done[sslot[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+                           spin < (1 << 22)) {
+                        __builtin_amdgcn_s_sleep(8);
+                        spin++;
+                    }
+                    if (spin >= (1 << 22)) raise_err(err, SHD_ROUTE_EDEVICE);
                 }
-                if (spin >= (1 << 22)) raise_err(err, SHD_ROUTE_EDEVICE);
+#ifdef SHD_STAMPS
+                sm->acc[31] += __builtin_amdgcn_s_memtime() - w0;
+#endif
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            // D0(v) = w(s,u) + d_u(v), saturating at 0xFFFF (= unreached); entries past n too
-            const uint32_t* sd32 = reinterpret_cast<const uint32_t*>(sdrow);
-            const kd_us2 wv = {(unsigned short)wsu, (unsigned short)wsu};
-#pragma unroll 4
-            for (int v = tid; v < (n + 2) / 2; v += B) {
-                uint32_t x = 0xFFFFFFFFu;
-                if (2 * v < n) {
-                    const kd_us2 d2 = __builtin_bit_cast(kd_us2, sd32[v]);
-                    x = __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(d2, wv));
-                    if (2 * v + 1 >= n) x |= 0xFFFF0000u;
+            // one streaming pass, 8 vertices per lane (16-B loads of every seed's distances
+            // and parent records): D0(v) = min_j w(s,u_j) + d_{u_j}(v), saturating at 0xFFFF
+            // (= unreached), into LDS; and the parent record a vertex keeps if it never
+            // improves on D0: the best (tie rule: largest w, then smallest parent) of the
+            // parents of the seeds attaining D0(v), u_j's own vertex having parent s.  Phase
+            // A's records overwrite the vertices that do improve.
+            // 4 vertices per lane: 8-B distance and 16-B parent-record loads of every seed
+            for (int v0 = 4 * tid; v0 <= n; v0 += 4 * B) {
+                const int vl = min(v0, n & ~3);
+                uint2 dq[KD_SEEDS];
+                uint4 pq[KD_SEEDS];
+#pragma unroll
+                for (int q = 0; q < KD_SEEDS; q++) {
+                    if (q < nseed) {
+                        dq[q] = *reinterpret_cast<const uint2*>(sdrow[q] + vl);
+                        pq[q] = *reinterpret_cast<const uint4*>(sprow[q] + vl);
+                    } else {
+                        dq[q] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+                        pq[q] = make_uint4(KD_NONE, KD_NONE, KD_NONE, KD_NONE);
+                    }
                 }
-                reinterpret_cast<uint32_t*>(dist)[v] = x;
+                uint32_t dw[2], rw[4];
+#pragma unroll
+                for (int h = 0; h < 4; h++) {
+                    const int v = v0 + h;
+                    unsigned dbest = 0xFFFFu, kbest = 0xFFFFFFFFu;
+                    uint32_t rbest = KD_NONE;
+#pragma unroll
+                    for (int q = 0; q < KD_SEEDS; q++) {
+                        const uint32_t d2 = (h < 2) ? dq[q].x : dq[q].y;
+                        const unsigned d = (h & 1) ? (d2 >> 16) : (d2 & 0xFFFFu);
+                        const unsigned c = q < nseed ? min(0xFFFFu, wsu[q] + d) : 0xFFFFFu;
+                        const uint32_t p = kd_comp(pq[q], h);
+                        const uint32_t r = v == su[q] ? ((uint32_t)s | (rsu[q] << 16) | (wsu[q] << 24)) : p;
+                        const uint32_t k = __builtin_amdgcn_perm(~r, r, 0x07010002u);  // (255-w) | p | ridx
+                        if (c < dbest || (c == dbest && k < kbest)) { dbest = c; kbest = k; rbest = r; }
+                    }
+                    if (v >= n) dbest = 0xFFFFu;
+                    if (v == s) rbest = KD_SRC_MARK;
+                    if (h & 1) dw[h >> 1] |= dbest << 16;
+                    else dw[h >> 1] = dbest;
+                    rw[h] = rbest;
+                }
+                *reinterpret_cast<uint2*>(dist + v0) = make_uint2(dw[0], dw[1]);
+                *reinterpret_cast<uint4*>(wpr + v0) = make_uint4(rw[0], rw[1], rw[2], rw[3]);
             }
+            wait_stores();  // before phase A's writer overwrites improved vertices
         } else {
             for (int v = tid; v < (n + 2) / 2; v += B) reinterpret_cast<uint32_t*>(dist)[v] = 0xFFFFFFFFu;
         }
@@ -457,9 +549,11 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             sm->gmin[0] = sm->gmin[1] = 0xFFFFFFFFu;
             sm->rtail = sm->rdone = 0;
             sm->nev = 0; sm->evovf = 0;
-            wpr[s] = KD_SRC_MARK;
+            wpr_of()[s] = KD_SRC_MARK;
         }
         lds_barrier();
+        KD_ACC(29);
+        KD_STAMP(0);  // after the seed wait and the distance init
         if (tid == 0) {
             dist[s] = 0;
             pend[s >> 6] = 1ull << (s & 63);
@@ -479,9 +573,6 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         int par = 0;
         const int ncomp = NW - 1;
         int wnev = 0;  // writer wave: tie events stored so far
-#ifdef SHD_STAMPS
-        unsigned long long kd_t = 0;
-#endif
         KD_MARK();
         for (;;) {
             KD_COUNT(5, tid == 0 ? 1 : 0);
@@ -794,7 +885,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     if (g.fused && hasrec) {
                         const uint32_t kk = deg0 > 0 ? wkey[crank] : ~0u;
                         if (kk != ~0u && (0xFFu - (kk >> 24)) >= delta)  // heavy winner: parent | ridx << 16
-                            prec = ((kk >> 8) & 0xFFFFu) | ((kk & 0xFFu) << 16);
+                            prec = ((kk >> 8) & 0xFFFFu) | ((kk & 0xFFu) << 16) | ((0xFFu - (kk >> 24)) << 24);
                     }
                     const unsigned long long rm = __ballot(hasrec);
                     if (rm) push_rec(rm, hasrec, prec, (uint32_t)u | (du0 << 16));
@@ -806,6 +897,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                 if (lane == 0) atomicAdd(&sm->nexit, 1);
             } else {
                 // ---- writer wave: parent records -> wpr (HBM) + fix bits -------------
+                uint32_t* const wpr = wpr_of();
                 int rd = __hip_atomic_load(&sm->rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 int spins = 0;
                 for (;;) {
@@ -875,27 +967,28 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         lds_barrier();
         if (seeded) {
             // ---- A': parents of the vertices that kept D0 ------------------------------
+            KD_MARK();
             const int nev = sm->nev;
             if (nev > g.evcap) {  // (uniform) the slice lost events: this row again, unseeded
-                seed = -1;
+                lds_barrier();
+                if (tid == 0) sm->job.nseed = 0;
                 lds_barrier();
                 goto kd_restart;
             }
+            uint32_t* const wpr = wpr_of();
+            SEED_VIEW();
             auto d0 = [&](int v) __attribute__((always_inline)) {
-                return min(0xFFFFu, wsu + (unsigned)sdrow[v]);
+                unsigned x = 0xFFFFu;
+#pragma unroll
+                for (int q = 0; q < KD_SEEDS; q++)
+                    if (q < nseed) x = min(x, min(0xFFFFu, wsu[q] + (unsigned)sdrow[q][v]));
+                return x;
             };
-            // their parent is u's, except u itself, whose parent is s (tight: D0(u) = w(s,u))
-#pragma unroll 4
-            for (int v = tid; v < n; v += B) {
-                const unsigned dv = ld16(dist, v), sd = sdrow[v];
-                const uint32_t pr = sprow[v];
-                if (dv == min(0xFFFFu, wsu + sd)) wpr[v] = v == su ? ((uint32_t)s | (rsu << 16)) : pr;
-            }
-            wait_stores();
-            lds_barrier();
-            // ...or a tight improved in-neighbour that wins the tie rule (largest w, then
-            // smallest parent): keys (255 - w) << 24 | parent << 8 | ridx, min over u's
-            // parent and every valid event, through u32 keys in the slice (relv is free)
+            KD_ACC(27);
+            // a vertex that kept D0 holds the seed-derived parent from the init pass; a tight
+            // improved in-neighbour reported as a tie event may beat it (tie rule: largest w,
+            // then smallest parent): keys (255 - w) << 24 | parent << 8 | ridx, min over
+            // that parent and every valid event, through u32 keys in the slice (relv is free)
             uint32_t* key = reinterpret_cast<uint32_t*>(relv);
             // event e -> v (-1 if invalid: v improved on D0, or the arc is not tight) + key
             auto event = [&](int e, int& v, uint32_t& ke) __attribute__((always_inline)) {
@@ -929,11 +1022,12 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                 event(e, v, ke);
                 if (v >= 0) {
                     const uint32_t k = __hip_atomic_load(&key[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    wpr[v] = ((k >> 8) & 0xFFFFu) | ((k & 0xFFu) << 16);
+                    wpr[v] = ((k >> 8) & 0xFFFFu) | ((k & 0xFFu) << 16) | ((0xFFu - (k >> 24)) << 24);
                 }
             }
             wait_stores();
             lds_barrier();
+            KD_ACC(28);
         }
         KD_STAMP(1);
         KD_MARK();
@@ -943,6 +1037,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         // the row bounds and KD_TAIL tail arcs are loaded straight-line, long tails are
         // re-queued (qbeg) for one wave per vertex
         const int last_arc = g.nlight > 0 ? g.nlight - 1 : 0;
+        uint32_t* const wpr = wpr_of();  // (phases B and C)
         if (tid == 0) {
             fix[s >> 6] &= ~(1ull << (s & 63));
             sm->qtail[0] = sm->qtail[1] = 0;
@@ -1006,7 +1101,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     for (int e = KD_TAIL - 1; e >= 0; e--)
                         if (a4[q] + e < r4[q] && dt[q][e] + (rc[q][e].x >> 16) == d4[q]) {
                             f = e;
-                            rec = (rc[q][e].x & 0xFFFFu) | (rc[q][e].y << 16);
+                            rec = (rc[q][e].x & 0xFFFFu) | (rc[q][e].y << 16) | (g.packed ? (rc[q][e].x >> 16) << 24 : 0u);
                         }
                     out_a[q] = rec;
                     if (v4[q] >= 0 && f < 0) {
@@ -1033,7 +1128,8 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     const uint2 rc = g.lrec[min(a, last_arc)];
                     const bool tight = a < r1 && ld16(dist, (int)(rc.x & 0xFFFFu)) + (rc.x >> 16) == dv;
                     const unsigned long long tm = __ballot(tight);
-                    if (tm) fr = (uint32_t)__builtin_amdgcn_readlane((int)((rc.x & 0xFFFFu) | (rc.y << 16)), __ffsll((long long)tm) - 1);
+                    if (tm) fr = (uint32_t)__builtin_amdgcn_readlane((int)((rc.x & 0xFFFFu) | (rc.y << 16) | (g.packed ? (rc.x >> 16) << 24 : 0u)),
+                                                                  __ffsll((long long)tm) - 1);
                 }
                 if (lane == 0) {
                     if (fr == KD_NONE) raise_err(err, SHD_ROUTE_EUNREACH);
@@ -1043,11 +1139,29 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         }
         KD_ACC(16);
         KD_ACC(17);
+        const int store = __builtin_amdgcn_readfirstlane(sm->job.store);
+        if (store >= 0) {
+            // this row seeds later ones: its parent records are final (wpr), keep its
+            // distances (u16, incl. the pad); once every wave's stores have drained, the
+            // flag (agent-scope release first) lets the rows it seeds start, before this
+            // row's own output
+            uint16_t* dr = g.drow_out + (size_t)store * g.rstride;
+            for (int v0 = 8 * tid; v0 <= n; v0 += 8 * B)
+                *reinterpret_cast<uint4*>(dr + v0) = *reinterpret_cast<const uint4*>(dist + v0);
+            wait_stores();
+            __syncthreads();
+            if (tid == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&g.done[store], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
         KD_STAMP(2);
-        double* lrow = lat_out ? lat_out + (long long)i * ld : nullptr;
-        double* rrow = rel_out ? rel_out + (long long)i * ld : nullptr;
+        // helper rows (i < 0, multi-GPU plans) only seed others: no output, no phase C
+        double* lrow = lat_out && i >= 0 ? lat_out + (long long)i * ld : nullptr;
+        double* rrow = rel_out && i >= 0 ? rel_out + (long long)i * ld : nullptr;
         double lmin = INFINITY;
-        for (int j = tid; j < nt; j += B) {
+        for (int j = tid; j < (i >= 0 ? nt : 0); j += B) {
             const int t = tgt[j];
             double Lv;
             if (t < 0 || t >= n) { raise_err(err, SHD_ROUTE_EINVAL); Lv = NAN; }
@@ -1059,20 +1173,10 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             else { Lv = (double)dist[t]; lmin = fmin(lmin, Lv); }
             if (lrow) __builtin_nontemporal_store(Lv, lrow + j);
         }
-        if (store >= 0) {  // this row seeds later ones: keep its distances (u16, incl. the pad)
-            uint32_t* d32 = reinterpret_cast<uint32_t*>(g.drow_out + (size_t)store * g.rstride);
-            for (int k = tid; k < (n + 2) / 2; k += B) d32[k] = reinterpret_cast<const uint32_t*>(dist)[k];
-        }
         wait_stores();  // wpr of phase B visible to the whole workgroup
         if (tid == 0) { sm->deep = 0; sm->rmin = kInfBits; }
         __syncthreads();
-        if (store >= 0 && tid == 0) {
-            // the kept row (distances + parent records) is complete: every wave's stores
-            // drained before the barrier above; release at agent scope, then the flag
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(&g.done[store], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+
         KD_ACC(18);
         // dist is dead: its LDS becomes the parent array
         uint16_t* parv = dist;
@@ -1102,7 +1206,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     const bool src_v = v == s, unr = !src_v && dv8[q] == 0xFFFFu;
                     parv[v] = src_v || unr ? (uint16_t)s : (uint16_t)(pr[q] & 0xFFFFu);
                     rixl[v] = src_v ? (uint8_t)KD_ONE : unr ? (uint8_t)KD_NAN
-                                                     : (uint8_t)min(pr[q] >> 16, (uint32_t)(g.nrtab - 1));
+                                                     : (uint8_t)min((pr[q] >> 16) & rmask, (uint32_t)(g.nrtab - 1));
                 }
             }
             __syncthreads();
@@ -1188,7 +1292,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             KD_ACC(13);
             KD_STAMP(3);
         }
-        const bool sweep = !(g.walk && rrow) || sm->deep;
+        const bool sweep = i >= 0 && (!(g.walk && rrow) || sm->deep);
         if (sweep) {
         // parent records: parent | ridx << 16 (writer wave and phase B), KD_SRC_MARK at s
         for (int v0 = tid; v0 < n; v0 += B * 8) {
@@ -1197,7 +1301,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             for (int q = 0; q < 8; q++) pr[q] = wpr[min(v0 + q * B, n - 1)];
             double rr[8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) rr[q] = g.rtab[min((int)(pr[q] >> 16), g.nrtab - 1)];
+            for (int q = 0; q < 8; q++) rr[q] = g.rtab[min((int)((pr[q] >> 16) & rmask), g.nrtab - 1)];
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const int v = v0 + q * B;
@@ -1322,7 +1426,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             }
         }
         }  // sweep
-        if (row_min) {
+        if (row_min && i >= 0) {
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) lmin = fmin(lmin, __shfl_xor(lmin, d, 64));
             if (lane == 0 && lmin < INFINITY) atomicMin(&sm->rmin, as_u(lmin));

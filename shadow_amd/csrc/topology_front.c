@@ -43,6 +43,22 @@ typedef struct {
 #define PC_STRIPES 64
 static inline unsigned pc_stripe(uint64_t key) { return (unsigned)((key * 0xD6E8FEB86659FD93ull) >> 58); }
 
+/* One fill of the Path cache over the attached set of its time.  Published to readers
+ * with a release store and never changed or freed while the topology lives: a late
+ * attach retires it (readers still holding it stay valid) and the next lookup fills a
+ * new one, carrying the packet counters over.  Lookups pay one acquire load. */
+typedef struct pcache {
+    int32_t na;
+    int32_t* A;          /* sorted attached vertices */
+    int32_t* cid;        /* vertex -> index in A, -1 = not attached */
+    double* lr;          /* (lat, rel) pairs: one cache line serves both getters */
+    uint32_t* cnt;       /* packet counters per pair (calloc: pages commit on first touch);
+                          * each 2^32 wrap adds 2^32 to the striped spill map pc */
+    double min_lat;
+    pcmap pc[PC_STRIPES];  /* spill map for counters past 2^32, striped over locks */
+    struct pcache* older;  /* retired fills (freed with the topology) */
+} pcache;
+
 struct shd_topology {
     shd_graphml_t gml;   /* owns the arrays when loaded from a file */
     shd_graph_t g;       /* view used by the engine */
@@ -58,23 +74,15 @@ struct shd_topology {
     uint8_t* attached;
     int32_t nattached;
     /* dense cache over A (sorted attached vertices), upper triangle incl. diagonal */
-    int32_t na;
-    int32_t* A;
-    int32_t* cid;
-    double* lr;          /* (lat, rel) pairs: one cache line serves both getters */
-    uint32_t* cnt;       /* packet counters per pair (calloc: pages commit on first touch);
-                          * each 2^32 wrap adds 2^32 to the striped spill map pc */
-    int filled;
-    double min_lat;
+    pcache* cache;       /* current fill (acquire/release), NULL = fill at the next lookup */
+    pcache* retired;     /* the fills a late attach replaced */
     double fill_seconds;
     pthread_mutex_t lock;
-    /* spill map for counters past 2^32, striped over PC_STRIPES locks */
-    pcmap pc[PC_STRIPES];
     shd_attach_t* at;    /* host attachment index (graphml topologies only) */
 };
 
-#define LAT(t, k) ((t)->lr[2 * (size_t)(k)])
-#define REL(t, k) ((t)->lr[2 * (size_t)(k) + 1])
+#define LAT(c, k) ((c)->lr[2 * (size_t)(k)])
+#define REL(c, k) ((c)->lr[2 * (size_t)(k) + 1])
 
 static inline size_t tri(int32_t na, int32_t i, int32_t j) { /* i <= j */
     return (size_t)i * (size_t)na - ((size_t)i * (size_t)(i - 1)) / 2 + (size_t)(j - i);
@@ -118,9 +126,23 @@ static int adjacent(const shd_topology_t* t, int32_t s, int32_t d) {
     return 0;
 }
 
+#define FILL_MAX_DEV 64  /* fill worker threads (one per device context) */
+
+static uint64_t* pc_slot(pcmap* m, uint64_t key);
+
+static void pcache_free(pcache* c) {
+    while (c) {
+        pcache* o = c->older;
+        free(c->A); free(c->cid); free(c->lr); free(c->cnt);
+        for (int k = 0; k < PC_STRIPES; k++) { pthread_mutex_destroy(&c->pc[k].lock); free(c->pc[k].s); }
+        free(c);
+        c = o;
+    }
+}
+
 static shd_topology_t* finish_new(shd_topology_t* t, const int* devices, int ndev) {
     t->n = t->g.n_vertices;
-    t->ndev = ndev > 0 ? ndev : 1;
+    t->ndev = ndev > 0 ? (ndev < FILL_MAX_DEV ? ndev : FILL_MAX_DEV) : 1;
     t->eng = calloc((size_t)t->ndev, sizeof(shd_route_t*));
     for (int d = 0; d < t->ndev; d++) {
         int dev = (devices && ndev > 0) ? devices[d] : 0;
@@ -135,11 +157,8 @@ static shd_topology_t* finish_new(shd_topology_t* t, const int* devices, int nde
     t->directed = info.directed;
     t->prefer_direct = info.prefer_direct;
     t->attached = calloc((size_t)t->n, 1);
-    t->cid = malloc(sizeof(int32_t) * (size_t)t->n);
-    for (int32_t v = 0; v < t->n; v++) t->cid[v] = -1;
     build_adjacency(t);
     pthread_mutex_init(&t->lock, NULL);
-    for (int k = 0; k < PC_STRIPES; k++) pthread_mutex_init(&t->pc[k].lock, NULL);
     return t;
 }
 
@@ -195,9 +214,9 @@ void shd_topology_free(shd_topology_t* t) {
     }
     shd_attach_destroy(t->at);
     shd_graphml_free(&t->gml);
-    free(t->arow); free(t->acol); free(t->attached); free(t->A); free(t->cid);
-    free(t->lr); free(t->cnt);
-    for (int k = 0; k < PC_STRIPES; k++) { pthread_mutex_destroy(&t->pc[k].lock); free(t->pc[k].s); }
+    free(t->arow); free(t->acol); free(t->attached);
+    pcache_free(t->cache);
+    pcache_free(t->retired);
     free(t);
 }
 
@@ -216,7 +235,15 @@ int shd_topology_attach_vertex(shd_topology_t* t, int32_t v) {
     if (!t->attached[v]) {
         t->attached[v] = 1;
         t->nattached++;
-        t->filled = 0;  /* the next lookup refills over the grown attached set */
+        /* the next lookup refills over the grown attached set (paths do not depend on the
+         * target set, so pairs already cached keep their values; their counters move over).
+         * Readers still holding the old fill keep a valid one: it is retired, not freed */
+        pcache* c = t->cache;
+        if (c) {
+            __atomic_store_n(&t->cache, (pcache*)NULL, __ATOMIC_RELEASE);
+            c->older = t->retired;
+            t->retired = c;
+        }
     }
     pthread_mutex_unlock(&t->lock);
     return SHD_ROUTE_OK;
@@ -240,27 +267,30 @@ int32_t shd_topology_attached_count(const shd_topology_t* t) { return t ? t->nat
 
 typedef struct {
     shd_topology_t* t;
-    int dev;
+    pcache* c;
+    int dev, nd;
     int rc;
 } fill_job;
 
-/* Row chunks are dealt round-robin over the devices; chunk c covers sources
- * A[c*R, (c+1)*R) and targets A[c*R, na) (the upper triangle it stores). */
+/* Row chunks are dealt round-robin over the fill threads (one per device context);
+ * chunk k covers sources A[k*R, (k+1)*R) and targets A[k*R, na) (the upper triangle it
+ * stores). */
 #define FILL_ROWS 256
 
 static void* fill_worker(void* arg) {
     fill_job* job = arg;
     shd_topology_t* t = job->t;
-    const int32_t na = t->na;
+    pcache* c = job->c;
+    const int32_t na = c->na;
     double* lbuf = malloc(sizeof(double) * (size_t)FILL_ROWS * (size_t)na);
     double* rbuf = malloc(sizeof(double) * (size_t)FILL_ROWS * (size_t)na);
     if (!lbuf || !rbuf) { job->rc = SHD_ROUTE_ENOMEM; free(lbuf); free(rbuf); return NULL; }
     const int32_t nchunks = (na + FILL_ROWS - 1) / FILL_ROWS;
-    for (int32_t c = job->dev; c < nchunks && !job->rc; c += t->ndev) {
-        const int32_t i0 = c * FILL_ROWS;
+    for (int32_t k = job->dev; k < nchunks && !job->rc; k += job->nd) {
+        const int32_t i0 = k * FILL_ROWS;
         const int32_t rows = (na - i0) < FILL_ROWS ? (na - i0) : FILL_ROWS;
         const int32_t nt = na - i0;
-        int rc = shd_route_rows(t->eng[job->dev], t->A + i0, rows, t->A + i0, nt, SHD_ROUTE_DISPATCH,
+        int rc = shd_route_rows(t->eng[job->dev], c->A + i0, rows, c->A + i0, nt, SHD_ROUTE_DISPATCH,
                                 lbuf, rbuf, NULL);
         /* ENOEDGE: a self pair without a self-loop; the rows are complete and that entry
          * is NaN, i.e. not stored by the batch, as the reference skips the failed target
@@ -273,7 +303,7 @@ static void* fill_worker(void* arg) {
             /* row i stores targets j >= i: offsets (j - i0) in the returned row */
             const double* lr_ = lbuf + (size_t)r * nt + r;
             const double* rr_ = rbuf + (size_t)r * nt + r;
-            double* o = t->lr + 2 * base;
+            double* o = c->lr + 2 * base;
             for (int32_t q = 0; q < na - i; q++) { o[2 * q] = lr_[q]; o[2 * q + 1] = rr_[q]; }
         }
     }
@@ -287,72 +317,96 @@ static double now_s(void) {
     return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
+/* counters of the pairs the last retired fill held, moved to fill c (after a late
+ * attach every old pair is still a pair: the attached set only grows) */
+static void carry_counters(const pcache* o, pcache* c) {
+    for (int32_t i = 0; i < o->na; i++)
+        for (int32_t j = i; j < o->na; j++) {
+            const size_t ko = tri(o->na, i, j);
+            uint64_t v = __atomic_load_n(&o->cnt[ko], __ATOMIC_RELAXED);
+            const pcmap* m = &o->pc[pc_stripe((uint64_t)ko + 1)];
+            if (m->cap) {
+                size_t h = (((uint64_t)ko + 1) * 0x9E3779B97F4A7C15ull) & (m->cap - 1);
+                while (m->s[h].key && m->s[h].key != (uint64_t)ko + 1) h = (h + 1) & (m->cap - 1);
+                if (m->s[h].key) v += m->s[h].val;
+            }
+            if (!v) continue;
+            int32_t a = c->cid[o->A[i]], b = c->cid[o->A[j]];
+            if (a > b) { int32_t x = a; a = b; b = x; }
+            const size_t k = tri(c->na, a, b);
+            c->cnt[k] = (uint32_t)v;
+            if (v >> 32) {
+                pcmap* mm = &c->pc[pc_stripe((uint64_t)k + 1)];
+                *pc_slot(mm, (uint64_t)k + 1) = v & ~(uint64_t)UINT32_MAX;
+            }
+        }
+}
+
 static int fill_locked(shd_topology_t* t) {
-    if (t->filled) return SHD_ROUTE_OK;
+    if (t->cache) return SHD_ROUTE_OK;
     const double t0 = now_s();
-    free(t->A); free(t->lr); free(t->cnt);
-    t->A = NULL; t->lr = NULL; t->cnt = NULL;
-    /* a refill renumbers the pairs: counters restart (Shadow attaches every host before
-     * the first packet, so this only happens in tests) */
-    for (int k = 0; k < PC_STRIPES; k++) {
-        pthread_mutex_lock(&t->pc[k].lock);
-        free(t->pc[k].s); t->pc[k].s = NULL; t->pc[k].cap = t->pc[k].len = 0;
-        pthread_mutex_unlock(&t->pc[k].lock);
-    }
-    t->na = 0;
-    t->A = malloc(sizeof(int32_t) * ((size_t)t->nattached + 1));
+    pcache* c = calloc(1, sizeof(pcache));
+    if (!c) return SHD_ROUTE_ENOMEM;
+    for (int k = 0; k < PC_STRIPES; k++) pthread_mutex_init(&c->pc[k].lock, NULL);
+    c->A = malloc(sizeof(int32_t) * ((size_t)t->nattached + 1));
+    c->cid = malloc(sizeof(int32_t) * (size_t)t->n);
+    if (!c->A || !c->cid) { pcache_free(c); return SHD_ROUTE_ENOMEM; }
     for (int32_t v = 0; v < t->n; v++) {
-        t->cid[v] = -1;
-        if (t->attached[v]) { t->cid[v] = t->na; t->A[t->na++] = v; }
+        c->cid[v] = -1;
+        if (t->attached[v]) { c->cid[v] = c->na; c->A[c->na++] = v; }
     }
-    const size_t ntri = (size_t)t->na * ((size_t)t->na + 1) / 2;
-    t->lr = malloc(2 * sizeof(double) * (ntri ? ntri : 1));
-    t->cnt = calloc(ntri ? ntri : 1, sizeof(uint32_t));
-    if (!t->lr || !t->cnt) return SHD_ROUTE_ENOMEM;
+    const size_t ntri = (size_t)c->na * ((size_t)c->na + 1) / 2;
+    c->lr = malloc(2 * sizeof(double) * (ntri ? ntri : 1));
+    c->cnt = calloc(ntri ? ntri : 1, sizeof(uint32_t));
+    if (!c->lr || !c->cnt) { pcache_free(c); return SHD_ROUTE_ENOMEM; }
+    for (size_t k = 0; k < 2 * ntri; k++) c->lr[k] = NAN;  /* a chunk that fails stays unstored */
     int rc = SHD_ROUTE_OK;
-    if (t->na) {
-        pthread_t th[64];
-        fill_job jobs[64];
-        const int nd = t->ndev < 64 ? t->ndev : 64;
+    if (c->na) {
+        pthread_t th[FILL_MAX_DEV];
+        fill_job jobs[FILL_MAX_DEV];
+        int started[FILL_MAX_DEV];
+        const int nd = t->ndev;  /* <= FILL_MAX_DEV (finish_new) */
         for (int d = 0; d < nd; d++) {
-            jobs[d].t = t; jobs[d].dev = d; jobs[d].rc = 0;
-            pthread_create(&th[d], NULL, fill_worker, &jobs[d]);
+            jobs[d].t = t; jobs[d].c = c; jobs[d].dev = d; jobs[d].nd = nd; jobs[d].rc = 0;
+            started[d] = pthread_create(&th[d], NULL, fill_worker, &jobs[d]) == 0;
         }
         for (int d = 0; d < nd; d++) {
-            pthread_join(th[d], NULL);
+            if (started[d]) pthread_join(th[d], NULL);
+            else fill_worker(&jobs[d]);  /* no thread: this device's chunks inline */
             if (jobs[d].rc && !rc) rc = jobs[d].rc;
         }
     }
-    if (rc) return rc;
+    if (rc) { pcache_free(c); return rc; }
     /* (s,s) pairs the batch could not store (no self-loop at s): the reference's next
      * (s,s) lookup misses and computes _topology_computeShortestPathToSelf
      * (topology.c:1674-1676, 1545-1653), i.e. 2*w_min and r_min^2 over s's out-edges */
     {
         int32_t nself = 0;
-        int32_t* sv = malloc(sizeof(int32_t) * ((size_t)t->na + 1));
-        for (int32_t i = 0; i < t->na; i++)
-            if (isnan(LAT(t, tri(t->na, i, i)))) sv[nself++] = t->A[i];
+        int32_t* sv = malloc(sizeof(int32_t) * ((size_t)c->na + 1));
+        for (int32_t i = 0; i < c->na; i++)
+            if (isnan(LAT(c, tri(c->na, i, i)))) sv[nself++] = c->A[i];
         if (nself) {
             double* sl = malloc(sizeof(double) * (size_t)nself);
             double* sr = malloc(sizeof(double) * (size_t)nself);
             rc = shd_route_self(t->eng[0], sv, nself, sl, sr);
             if (rc == SHD_ROUTE_ENOEDGE) rc = SHD_ROUTE_OK;  /* no out-edge: stays unstored */
             for (int32_t q = 0; q < nself && !rc; q++) {
-                const size_t k = tri(t->na, t->cid[sv[q]], t->cid[sv[q]]);
-                LAT(t, k) = sl[q];
-                REL(t, k) = sr[q];
+                const size_t k = tri(c->na, c->cid[sv[q]], c->cid[sv[q]]);
+                LAT(c, k) = sl[q];
+                REL(c, k) = sr[q];
             }
             free(sl); free(sr);
         }
         free(sv);
-        if (rc) return rc;
+        if (rc) { pcache_free(c); return rc; }
     }
     double mn = 0;
     for (size_t k = 0; k < ntri; k++)  /* topology.c:1375: minLat == 0 means unset */
-        if (!isnan(LAT(t, k)) && (mn == 0 || LAT(t, k) < mn)) mn = LAT(t, k);
-    t->min_lat = mn;
+        if (!isnan(LAT(c, k)) && (mn == 0 || LAT(c, k) < mn)) mn = LAT(c, k);
+    c->min_lat = mn;
+    if (t->retired) carry_counters(t->retired, c);
     t->fill_seconds += now_s() - t0;
-    __atomic_store_n(&t->filled, 1, __ATOMIC_RELEASE);
+    __atomic_store_n(&t->cache, c, __ATOMIC_RELEASE);
     return SHD_ROUTE_OK;
 }
 
@@ -365,29 +419,39 @@ int shd_topology_fill(shd_topology_t* t, double* elapsed_s) {
     return rc;
 }
 
-/* _topology_getPathEntry (topology.c:1969-2051) -> index into the triangle, or -1 */
-static int64_t entry(shd_topology_t* t, int32_t s, int32_t d) {
+/* the published fill, filling it first if needed (NULL on failure) */
+static pcache* cache_of(shd_topology_t* t) {
+    pcache* c = __atomic_load_n(&t->cache, __ATOMIC_ACQUIRE);
+    if (c) return c;
+    pthread_mutex_lock(&t->lock);
+    const int rc = fill_locked(t);
+    c = t->cache;
+    pthread_mutex_unlock(&t->lock);
+    return rc ? NULL : c;
+}
+
+/* _topology_getPathEntry (topology.c:1969-2051) -> index into the triangle of *cp, or -1 */
+static int64_t entry(shd_topology_t* t, int32_t s, int32_t d, pcache** cp) {
     if (!t || s < 0 || d < 0 || s >= t->n || d >= t->n) return -1;
-    if (!__atomic_load_n(&t->filled, __ATOMIC_ACQUIRE)) {
-        pthread_mutex_lock(&t->lock);
-        int rc = fill_locked(t);
-        pthread_mutex_unlock(&t->lock);
-        if (rc) return -1;
-    }
-    const int32_t i = t->cid[s], j = t->cid[d];
+    pcache* c = cache_of(t);
+    if (!c) return -1;
+    const int32_t i = c->cid[s], j = c->cid[d];
     if (i < 0 || j < 0) return -1;  /* address not connected to the topology */
-    const int64_t k = (int64_t)(i <= j ? tri(t->na, i, j) : tri(t->na, j, i));
-    return isnan(LAT(t, k)) ? -1 : k;  /* never stored (topology.c:2040-2046) */
+    const int64_t k = (int64_t)(i <= j ? tri(c->na, i, j) : tri(c->na, j, i));
+    *cp = c;
+    return isnan(LAT(c, k)) ? -1 : k;  /* never stored (topology.c:2040-2046) */
 }
 
 double shd_topology_get_latency(shd_topology_t* t, int32_t s, int32_t d) {
-    int64_t k = entry(t, s, d);
-    return k < 0 ? -1.0 : LAT(t, k);
+    pcache* c;
+    int64_t k = entry(t, s, d, &c);
+    return k < 0 ? -1.0 : LAT(c, k);
 }
 
 double shd_topology_get_reliability(shd_topology_t* t, int32_t s, int32_t d) {
-    int64_t k = entry(t, s, d);
-    return k < 0 ? -1.0 : REL(t, k);
+    pcache* c;
+    int64_t k = entry(t, s, d, &c);
+    return k < 0 ? -1.0 : REL(c, k);
 }
 
 int shd_topology_is_routable(shd_topology_t* t, int32_t s, int32_t d) {
@@ -395,7 +459,8 @@ int shd_topology_is_routable(shd_topology_t* t, int32_t s, int32_t d) {
 }
 
 int shd_topology_is_direct_path(shd_topology_t* t, int32_t s, int32_t d) {
-    if (entry(t, s, d) < 0) return -1;
+    pcache* c;
+    if (entry(t, s, d, &c) < 0) return -1;
     const int32_t a = s < d ? s : d, b = s < d ? d : s;  /* stored orientation: min -> max */
     return t->complete || (t->prefer_direct && adjacent(t, a, b));
 }
@@ -420,10 +485,10 @@ static uint64_t* pc_slot(pcmap* m, uint64_t key) {
 }
 
 /* read without inserting */
-static uint64_t pc_get(shd_topology_t* t, uint64_t key) {
+static uint64_t pc_get(pcache* c, uint64_t key) {
     const unsigned st = pc_stripe(key);
     uint64_t v = 0;
-    pcmap* m = &t->pc[st];
+    pcmap* m = &c->pc[st];
     pthread_mutex_lock(&m->lock);
     if (m->cap) {
         size_t j = (key * 0x9E3779B97F4A7C15ull) & (m->cap - 1);
@@ -435,28 +500,30 @@ static uint64_t pc_get(shd_topology_t* t, uint64_t key) {
 }
 
 void shd_topology_increment_path_packet_counter(shd_topology_t* t, int32_t s, int32_t d) {
-    int64_t k = entry(t, s, d);
+    pcache* c;
+    int64_t k = entry(t, s, d, &c);
     if (k < 0) return;
     /* path_incrementPacketCount (path.c:57-60) without its data race: one relaxed
      * atomic add on the pair's own counter, no lock */
-    if (__atomic_fetch_add(&t->cnt[k], 1u, __ATOMIC_RELAXED) != UINT32_MAX) return;
+    if (__atomic_fetch_add(&c->cnt[k], 1u, __ATOMIC_RELAXED) != UINT32_MAX) return;
     const uint64_t key = (uint64_t)k + 1;
     const unsigned st = pc_stripe(key);
-    pthread_mutex_lock(&t->pc[st].lock);
-    *pc_slot(&t->pc[st], key) += 1ull << 32;
-    pthread_mutex_unlock(&t->pc[st].lock);
+    pthread_mutex_lock(&c->pc[st].lock);
+    *pc_slot(&c->pc[st], key) += 1ull << 32;
+    pthread_mutex_unlock(&c->pc[st].lock);
 }
 
 uint64_t shd_topology_get_path_packet_count(shd_topology_t* t, int32_t s, int32_t d) {
-    int64_t k = entry(t, s, d);
+    pcache* c;
+    int64_t k = entry(t, s, d, &c);
     if (k < 0) return 0;
-    return pc_get(t, (uint64_t)k + 1) + __atomic_load_n(&t->cnt[k], __ATOMIC_RELAXED);
+    return pc_get(c, (uint64_t)k + 1) + __atomic_load_n(&c->cnt[k], __ATOMIC_RELAXED);
 }
 
 double shd_topology_min_path_latency(shd_topology_t* t) {
     if (!t) return -1;
-    if (shd_topology_fill(t, NULL) != SHD_ROUTE_OK) return -1;
-    return t->min_lat;
+    pcache* c = cache_of(t);
+    return c ? c->min_lat : -1;
 }
 
 uint64_t shd_topology_runahead_ns(shd_topology_t* t) {
@@ -467,22 +534,22 @@ uint64_t shd_topology_runahead_ns(shd_topology_t* t) {
 
 int shd_topology_dump_paths(shd_topology_t* t, FILE* out) {
     if (!t || !out) return SHD_ROUTE_EINVAL;
-    int rc = shd_topology_fill(t, NULL);
-    if (rc) return rc;
-    for (int32_t i = 0; i < t->na; i++)
-        for (int32_t j = i; j < t->na; j++) {
-            const size_t k = tri(t->na, i, j);
-            const int32_t a = t->A[i], b = t->A[j];
+    pcache* c = cache_of(t);
+    if (!c) return SHD_ROUTE_EDEVICE;
+    for (int32_t i = 0; i < c->na; i++)
+        for (int32_t j = i; j < c->na; j++) {
+            const size_t k = tri(c->na, i, j);
+            const int32_t a = c->A[i], b = c->A[j];
             const char* ia = t->gml.vertex_ids ? t->gml.vertex_ids[a] : NULL;
             const char* ib = t->gml.vertex_ids ? t->gml.vertex_ids[b] : NULL;
             char na_[32], nb_[32];
             if (!ia) { snprintf(na_, sizeof na_, "%d", a); ia = na_; }
             if (!ib) { snprintf(nb_, sizeof nb_, "%d", b); ib = nb_; }
-            const uint64_t pc = pc_get(t, (uint64_t)k + 1) + __atomic_load_n(&t->cnt[k], __ATOMIC_RELAXED);
+            const uint64_t pc = pc_get(c, (uint64_t)k + 1) + __atomic_load_n(&c->cnt[k], __ATOMIC_RELAXED);
             /* path_toString (path.c:62-74) inside _topology_logAllCachedPathsHelper2 */
             fprintf(out, "Found path %s%s%s in cache: SourceIndex=%d DestinationIndex=%d Latency=%f "
                          "Reliability=%f PacketCount=%llu isDirect=%s\n",
-                    ia, t->directed ? "->" : "<->", ib, a, b, LAT(t, k), REL(t, k), (unsigned long long)pc,
+                    ia, t->directed ? "->" : "<->", ib, a, b, LAT(c, k), REL(c, k), (unsigned long long)pc,
                     (t->complete || (t->prefer_direct && adjacent(t, a, b))) ? "True" : "False");
         }
     return SHD_ROUTE_OK;

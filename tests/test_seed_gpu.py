@@ -30,15 +30,20 @@ def kd(monkeypatch):
     monkeypatch.setenv("SHD_ROUTE_KDGRID", "7")
     monkeypatch.delenv("SHD_ROUTE_SEED", raising=False)
     monkeypatch.delenv("SHD_ROUTE_EVCAP", raising=False)
+    monkeypatch.delenv("SHD_ROUTE_SEEDS", raising=False)
     return monkeypatch
 
 
-@pytest.mark.parametrize("evcap", [None, "0", "2"])
+@pytest.mark.parametrize("seeds,evcap", [(None, None), ("1", None), ("3", None), (None, "0"), ("3", "2")])
 @pytest.mark.parametrize("name", ["ba400", "ties", "chain", "c2"])
-def test_seeded_rows_bitexact(oracle_mod, kd, name, evcap):
+def test_seeded_rows_bitexact(oracle_mod, kd, name, seeds, evcap):
+    """seeds: rows started from 1..3 neighbour rows (default 2); evcap 0 / 2: every row
+    with more tie events than that reruns unseeded."""
     from shadow_amd import route
     if evcap is not None:
         kd.setenv("SHD_ROUTE_EVCAP", evcap)
+    if seeds is not None:
+        kd.setenv("SHD_ROUTE_SEEDS", seeds)
     g = _graph(name)
     eng = route.RouteEngine(g)
     assert eng.info["kernel"] == 4

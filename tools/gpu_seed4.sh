@@ -1,0 +1,6 @@
+#!/bin/bash
+set -o pipefail
+export PYTHONUNBUFFERED=1
+mkdir -p gpurun_out
+TESTS="tests/test_seed_gpu.py tests/test_topology_gpu.py" SWEEP="c4:SHD_ROUTE_SEEDS=1 c4:SHD_ROUTE_SEEDS=2 c3:SHD_ROUTE_SEEDS=1" tools/gpu_seed_sweep.sh || exit 1
+timeout -k 10 200 python -u tools/stamps.py --config c4 --plan > gpurun_out/stamps_c4_plan4.txt 2>&1 && grep -v amdgpu.ids gpurun_out/stamps_c4_plan4.txt | head -30

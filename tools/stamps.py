@@ -19,6 +19,7 @@ from shadow_amd.graph import config  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c2")
 ap.add_argument("--sources", type=int, default=0)
+ap.add_argument("--plan", action="store_true", help="seeded plan over the sources (rows in source order)")
 a = ap.parse_args()
 g = config(a.config)
 eng = route.RouteEngine(g)
@@ -35,10 +36,16 @@ nwg = (len(S) + 7) // 8
 dbg = torch.zeros((len(S) + nwg) * 32, dtype=torch.int64, device=dev)
 L.shd_route_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
 L.shd_route_debug_buffer(eng._h, C.c_void_p(dbg.data_ptr()))
+plan = eng.plan(S) if a.plan else None
 for rep in range(3):
     dbg.zero_()
-    eng.rows_async(d_src, d_tgt, lat, rel, mn)
+    if plan is not None:
+        plan.rows_async(d_tgt, lat, rel, mn)
+    else:
+        eng.rows_async(d_src, d_tgt, lat, rel, mn)
     eng.sync()
+if plan is not None:
+    print("plan", plan.info)
 d_all = dbg.cpu().numpy().astype(np.int64).reshape(-1, 32 if eng.info["kernel"] == 4 else 8)
 d = d_all[: len(S)]
 if eng.info["kernel"] == 2:
@@ -81,6 +88,8 @@ if eng.info["kernel"] == 4:
     ng = max(d[:, 25].mean(), 1)
     print(f"  wave0 per group: owners {d[:, 30].mean() / ng:.0f}  owners+loads {d[:, 27].mean() / ng:.0f}  process {d[:, 28].mean() / ng:.0f} (relax {d[:, 29].mean() / ng:.0f}) cyc")
     print(f"  queue overflow/source: pushes to pending {d[:, 14].mean():.0f}  gathered past capacity {d[:, 15].mean():.0f}")
+    print(f"  drain of the previous row's stores {d[:, 9].mean():.0f}")
+    print(f"  seeded init {d[:, 29].mean():.0f} (seed wait {d[:, 31].mean():.0f})  A' copy {d[:, 27].mean():.0f}  A' events {d[:, 28].mean():.0f} cyc/source")
     for k, nm in [(11, "minreduce"), (8, "gather"), (9, "prep"), (10, "expand"), (16, "B.short"), (17, "B.long"),
                   (18, "lat row+drain"), (19, "par copy"), (13, "C.compute")]:
         print(f"  A.{nm:10s} mean {d[:, k].mean():10.0f} cyc  ({d[:, k].mean() / max(d[:, 5].mean(), 1):.0f}/sweep)")

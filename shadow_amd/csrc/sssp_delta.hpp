@@ -31,7 +31,7 @@
 //    no light arc can beat it and no heavy arc can appear later.  Vertices whose winner
 //    is light or absent (45% on C4: shortest-path trees favour short arcs) are marked
 //    for a pull fix-up over the light tail of their (-w, u, eid)-sorted in-row (phase
-//    B, ~6% of the arcs).  Directed graphs fix up every vertex over its whole in-row.
+//    B, ~12% of the arcs).  Directed graphs fix up every vertex over its whole in-row.
 //
 // B  fix-ups (four vertices and four tail arcs each in flight per thread; long tails one
 //    wave per vertex), lat row out (dist is exact: integer latencies, bound < 0xFFFF).
@@ -49,7 +49,7 @@
 //  * arc records carry everything a parent needs: out-arcs {v | w << 16, ridx} where
 //    ridx indexes the table of distinct reliabilities (101 entries on C4), so the winning
 //    parent (vertex, ridx) comes out of the expansion itself, no gather;
-//  * fix-ups read a compact light in-CSR (6% of the arcs, L2-resident);
+//  * fix-ups read a compact light in-CSR (12% of the arcs, L2-resident);
 //  * loads are straight-line (clamped addresses, no branches around them) and stores are
 //    deferred: a slice records each winner in LDS, the next sweep flushes the records
 //    (wpr, one u32 per vertex) before its only global loads.

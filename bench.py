@@ -13,9 +13,10 @@ select the smaller configs, --config c5 the dense complete graph (K3 direct fill
 with the K4 Floyd-Warshall timed beside it).
 
 Multi-GPU (one process per GPU, launched by torch.distributed.run):
-  --scaling strong (default) one topology, attached sources in contiguous blocks per
-                   rank; the runahead min is combined with an RCCL all-reduce(MIN) each
-                   step.  The all-gather of the latency AND reliability row shards into
+  --scaling strong (default) one topology, attached sources sharded over the ranks
+                   by the seeded plan (whole subtrees of the seed forest per rank, its top
+                   levels computed on every rank as helper rows); the runahead min is
+                   combined with an RCCL all-reduce(MIN) each step.  The all-gather of the latency AND reliability row shards into
                    the full table on every GPU is timed separately (it is needed only
                    where a device-resident full matrix is; Shadow's host cache is filled
                    per rank by D2H of its own shard); --allgather puts it in every step.
@@ -155,6 +156,8 @@ def main():
     ap.add_argument("--sources", type=int, default=0, help="limit sources (0 = all)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "f64", "k32", "kb", "kd"], help="force an SSSP kernel")
     ap.add_argument("--no-seed", action="store_true", help="plain KD rows (no seeded plan)")
+    ap.add_argument("--emulate", default="", help="W:R = one GPU runs rank R's plan of a W-GPU strong split "
+                    "(diagnostic: that rank's compute time; no collectives)")
     args = ap.parse_args()
     if args.kernel != "auto":
         os.environ["SHD_ROUTE_KERNEL"] = args.kernel
@@ -192,7 +195,11 @@ def main():
     # the rows of this rank (strong: a contiguous block of the source list) under one
     # seeded plan: rows whose source has an already-computed neighbour start from it
     t_plan = time.perf_counter()
-    plan = eng.plan(all_sources, 1 if weak else world, 0 if weak else rank)
+    if args.emulate and world == 1:
+        ew, er = (int(x) for x in args.emulate.split(":"))
+        plan = eng.plan(all_sources, ew, er)
+    else:
+        plan = eng.plan(all_sources, 1 if weak else world, 0 if weak else rank)
     t_plan = time.perf_counter() - t_plan
     my_sources = plan.sources
     ns, nt = len(my_sources), len(targets)
@@ -202,9 +209,15 @@ def main():
     gather = world > 1 and not weak
     proto = torch.empty(0, dtype=torch.float64, device=dev)
     if gather:
-        # shards are views into the full tables: rows land in place, the gather is in place
-        f_lat, d_lat = full_table(len(all_sources), nt, world, rank, proto)
-        f_rel, d_rel = full_table(len(all_sources), nt, world, rank, proto)
+        # shards are views into the full tables: rows land in place, the gather is in place.
+        # A rank's block holds its plan rows (the seed forest's subtrees it owns), padded
+        # to the largest block; the gathered table's row order is every rank's
+        # plan.positions in turn
+        blk_t = torch.tensor([ns], dtype=torch.int64, device=dev)
+        dist.all_reduce(blk_t, op=dist.ReduceOp.MAX)
+        blk = int(blk_t.item())
+        f_lat, d_lat = full_table(len(all_sources), nt, world, rank, proto, blk)
+        f_rel, d_rel = full_table(len(all_sources), nt, world, rank, proto, blk)
         d_lat, d_rel = d_lat[: max(ns, 1)], d_rel[: max(ns, 1)]
     else:
         d_lat = torch.empty((max(ns, 1), nt), dtype=torch.float64, device=dev)
@@ -261,7 +274,7 @@ def main():
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
-    total_src = ns * world if weak else len(all_sources)
+    total_src = ns * world if weak else (ns if args.emulate else len(all_sources))
 
     # correctness spot check against the oracle, outside the timed region
     verified = None
@@ -305,7 +318,8 @@ def main():
             "sources_total": total_src, "sources_per_gpu": ns, "targets": nt,
             "table_bytes": 16 * total_src * nt,
             "parallelism": (f"replicas x{world} (independent topologies)" if weak
-                            else f"sources sharded in contiguous blocks /{world}"),
+                            else (f"sources sharded /{world}: seed-forest subtrees per rank, "
+                                  f"top levels replicated as helper rows" if world > 1 else "one GPU")),
         },
         "gteps": total_src * g.m_nonloop * args.steps / dt / 1e9,
         "pairs_per_s": total_src * nt * args.steps / dt,

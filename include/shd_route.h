@@ -6,7 +6,11 @@
  * its public routing API unchanged (topology.h:17-28); its topology.c front end
  * calls this module instead of igraph for every number that ends up in a Path
  * (path.c:13-21: latency, reliability).  Plain C types only; no HIP/torch types
- * in any signature.  One context per GPU; contexts are not re-entrant.
+ * in any signature.  One context per GPU; contexts are not re-entrant, and a context
+ * (with its plans) runs one rows launch at a time: the launches of shd_route_rows_async
+ * and shd_route_rows_planned_async share the context's work-queue counter and
+ * per-workgroup scratch, so two of them must not be in flight together (enqueue them
+ * on one stream, or synchronise in between).
  *
  * Reference interface each entry point replaces (file:line in the reference):
  *   shd_route_create   <- _topology_loadGraph/_topology_checkGraph/_topology_extractEdgeWeights

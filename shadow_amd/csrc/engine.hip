@@ -1166,19 +1166,16 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             maxl = std::max(maxl, flvl[p]);
         }
         for (int q = ns - 1; q >= 0; q--) if (fpar[pos[q]] >= 0) sub[fpar[pos[q]]] += sub[pos[q]];
-        // cut level: the shallowest whose subtrees all fit a quarter of a rank's share
+        // T = the rows whose subtree holds more than a quarter of a rank's share (the
+        // forest's skeleton near its roots); every other row hangs in a subtree of at most
+        // that size whose head's parent is in T (or which is a whole small tree)
         const int cap = std::max(1, ns / (4 * world));
-        int L = 1;
-        for (; L <= maxl; L++) {
-            int mx = 0;
-            for (int p = 0; p < ns; p++) if (flvl[p] == L) mx = std::max(mx, sub[p]);
-            if (mx <= cap) break;
-        }
         std::vector<int> top, heads;
         for (int p : pos) {
-            if (flvl[p] < L) top.push_back(p);
-            else if (flvl[p] == L) heads.push_back(p);
+            if (sub[p] > cap) top.push_back(p);
+            else if (fpar[p] < 0 || sub[fpar[p]] > cap) heads.push_back(p);
         }
+        (void)maxl;
         std::stable_sort(heads.begin(), heads.end(), [&](int a, int b) { return sub[a] > sub[b]; });
         std::vector<int> owner(ns, -1);
         std::vector<long long> load(world, 0);
@@ -1205,11 +1202,13 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         std::vector<int> lvl(nj, 0), slot(nj, -1), nsd(nj, 0);
         std::vector<std::array<int, KD_SEEDS>> seedjob(nj), su(nj), wr(nj);
         // options: seeds per row (1..KD_SEEDS), the `roots` most central rows start
-        // unseeded, and seed chains are at most `depth` rows long
+        // unseeded (default: one per workgroup slot, so the launch starts full and the
+        // seed chains below them are short: C4 1 GPU 52.9 -> 51.0 ms, an 8-way rank
+        // 12.8 -> 10.0 ms, C3 4.0 -> 3.4 ms), and seed chains are at most `depth` rows long
         // default depth cap: about half the rows each workgroup slot runs in turn, so that
         // seed chains are shorter than a slot's queue (C4: 195 rows per slot, no cap in
         // effect; C3: 9 per slot, cap 4: the critical path, not the work, bounds C3)
-        int kseeds = 2, nroot_min = 0, depth = std::max(3, nj / std::max(1, 2 * c->kd_slots));
+        int kseeds = 2, nroot_min = c->kd_slots, depth = std::max(3, nj / std::max(1, 2 * c->kd_slots));
         if (const char* e = getenv("SHD_ROUTE_SEEDS")) kseeds = std::max(1, std::min(KD_SEEDS, atoi(e)));
         if (const char* e = getenv("SHD_ROUTE_SEED_ROOTS")) nroot_min = std::max(0, atoi(e));
         if (const char* e = getenv("SHD_ROUTE_SEED_DEPTH")) depth = std::max(1, atoi(e));

@@ -44,12 +44,14 @@ def allgather_rows(local_rows, n_total: int, dist, group=None):
     return out[:n_total]
 
 
-def full_table(n_total: int, nt: int, world: int, rank: int, like):
-    """A [ceil(n_total/world) * world, nt] table whose rank block is this rank's shard:
-    rows are computed straight into `shard` and gathered in place (allgather_inplace),
-    so the C4 table (20 GB per f64 array) never needs a second copy."""
+def full_table(n_total: int, nt: int, world: int, rank: int, like, blk: int = 0):
+    """A [blk * world, nt] table (blk defaults to ceil(n_total/world)) whose rank block is
+    this rank's shard: rows are computed straight into `shard` and gathered in place
+    (allgather_inplace), so the C4 table (20 GB per f64 array) never needs a second copy.
+    With seeded plans the blocks hold each rank's plan rows (shd_route_plan_rows), padded
+    to the largest block."""
     import torch
-    blk = block_rows(n_total, world)
+    blk = blk or block_rows(n_total, world)
     full = torch.empty((blk * world, nt), dtype=like.dtype, device=like.device)
     return full, full[rank * blk:(rank + 1) * blk]
 

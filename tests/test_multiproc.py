@@ -1,5 +1,5 @@
 """CPU, world_size 2 over gloo: source sharding, runahead all-reduce MIN and the row
-all-gather reproduce the single-process table (rows computed by the oracle here; on
+all-gather (latency and reliability, also in the bench's in-place form) reproduce the single-process table (rows computed by the oracle here; on
 the GPU box the same plumbing carries the HIP rows over RCCL)."""
 import os
 import socket
@@ -35,8 +35,16 @@ def _worker(rank, world, port, q):
     local_min = torch.tensor([lat.min() if len(lat) else np.inf], dtype=torch.float64)
     runahead_min(local_min, dist)
     full = allgather_rows(torch.from_numpy(lat), len(T), dist)
+    # the bench's in-place form: rows written into this rank's block of the full tables
+    from shadow_amd.shard import allgather_inplace, full_table
+    f_lat, s_lat = full_table(len(T), len(T), world, rank, torch.empty(0, dtype=torch.float64))
+    f_rel, s_rel = full_table(len(T), len(T), world, rank, torch.empty(0, dtype=torch.float64))
+    s_lat[:hi - lo] = torch.from_numpy(lat)
+    s_rel[:hi - lo] = torch.from_numpy(rel)
+    allgather_inplace(f_lat, dist)
+    allgather_inplace(f_rel, dist)
     if rank == 0:
-        q.put((full.numpy(), float(local_min.item())))
+        q.put((full.numpy(), float(local_min.item()), f_lat[:len(T)].numpy(), f_rel[:len(T)].numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -49,15 +57,16 @@ def test_sharded_rows_allgather_and_min(world, oracle_mod):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    full, mn = q.get(timeout=120)
+    full, mn, glat, grel = q.get(timeout=120)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     g = internet_like(90, 2, seed=21)
     T = g.targets()
     og = oracle_mod.OracleGraph(g)
-    ref, _, _, _ = og.source_rows(T, T, oracle_mod.TIE_MINKEY)
+    ref, rref, _, _ = og.source_rows(T, T, oracle_mod.TIE_MINKEY)
     assert np.array_equal(full, ref)
+    assert np.array_equal(glat, ref) and np.array_equal(grel, rref)
     assert mn == ref.min()
 
 

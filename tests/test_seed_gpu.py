@@ -125,3 +125,67 @@ def test_full_table_planned_matches_golden(monkeypatch, cfg):
     assert np.array_equal(blk, blk.T)
     del d_lat, d_rel
     torch.cuda.empty_cache()
+
+
+def _plan_rows(eng, plan, T):
+    import torch
+    dev = torch.device("cuda", 0)
+    d_tgt = torch.from_numpy(np.ascontiguousarray(T, np.int32)).to(dev)
+    nr = max(1, plan.info["rows"])
+    d_lat = torch.empty((nr, len(T)), dtype=torch.float64, device=dev)
+    d_rel = torch.empty_like(d_lat)
+    d_min = torch.empty(nr, dtype=torch.float64, device=dev)
+    plan.rows_async(d_tgt, d_lat, d_rel, d_min, dispatch=False)
+    eng.sync()
+    k = plan.info["rows"]
+    return d_lat[:k].cpu().numpy(), d_rel[:k].cpu().numpy(), d_min[:k].cpu().numpy()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("name", ["ba400", "c2"])
+def test_partitioned_plans_cover_and_match(kd, name, world):
+    """Multi-GPU plans (one per rank, all run here on device 0): the ranks' rows cover the
+    source list exactly once, every rank's seeds are its own rows or its helper rows
+    (top of the seed forest), and each row equals the single-GPU table's row."""
+    from shadow_amd import route
+    g = _graph(name)
+    eng = route.RouteEngine(g)
+    T = g.targets()
+    ref_lat, ref_rel, ref_mn = eng.rows(T, T, dispatch=False)
+    seen = []
+    for r in range(world):
+        plan = eng.plan(T, world, r)
+        assert plan.info["seeded"] == 1 and plan.info["world"] == world and plan.info["rank"] == r
+        assert plan.info["helpers"] > 0
+        lat, rel, mn = _plan_rows(eng, plan, T)
+        pos = plan.positions
+        assert np.array_equal(lat, ref_lat[pos]) and np.array_equal(rel, ref_rel[pos]) and np.array_equal(mn, ref_mn[pos])
+        seen.extend(pos.tolist())
+    assert sorted(seen) == list(range(len(T)))
+
+
+def test_c4_eight_rank_plans_balanced_and_golden(monkeypatch):
+    """C4 split over 8 ranks: blocks within 10% of 6,250 rows, few helper rows, and the
+    golden sampled rows come out of whichever rank owns them bit-exact."""
+    from shadow_amd import route
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    monkeypatch.delenv("SHD_ROUTE_KDGRID", raising=False)
+    dig = json.load(open(os.path.join(GOLD, "rows_digests.json")))["c4"]
+    g = config("c4")
+    eng = route.RouteEngine(g)
+    T = g.targets()
+    want = {r["src"]: r for r in dig["rows"]}
+    found = 0
+    for r in range(8):
+        plan = eng.plan(T, 8, r)
+        assert abs(plan.info["rows"] - 6250) <= 625, plan.info
+        assert plan.info["helpers"] <= 2500, plan.info
+        mine = [k for k, s in enumerate(plan.sources) if int(s) in want]
+        if not mine:
+            continue
+        lat, rel, mn = _plan_rows(eng, plan, T)
+        for k in mine:
+            w = want[int(plan.sources[k])]
+            assert _sha(lat[k]) == w["lat_sha"] and _sha(rel[k]) == w["rel_sha"] and mn[k] == w["row_min"]
+            found += 1
+    assert found == len(want)

@@ -175,6 +175,23 @@ int shd_route_rows_planned_async(shd_route_t* ctx, const shd_route_plan_t* plan,
                                  int32_t nt, int64_t ld, uint32_t flags, double* d_lat, double* d_rel,
                                  double* d_row_min, void* stream);
 
+/* K4: all-pairs shortest latencies by blocked min-plus
+ * Floyd-Warshall over all vertices, u16 on the device (kept in the context).  Integer
+ * latencies with every shortest path below 65535 ms, n <= 12000, simple graphs; else
+ * SHD_ROUTE_EUNSUPPORTED.  No reference equivalent: Shadow 1.14 never takes shortest
+ * paths on a complete graph (topology.c:1321-1323, 2019-2021); this is the dense
+ * alternative to per-source SSSP. */
+int shd_route_fw_table_async(shd_route_t* ctx, void* stream);
+
+/* SOURCE(s,.) rows (as shd_route_rows_async without dispatch: topology.c:1407-1523)
+ * from the resident K4 table: lat from the table, the parent of each vertex by the
+ * engine tie rule among its tight in-arcs, rel the source-first product down that
+ * tree.  Same entries as shd_route_rows_async bit for bit (integer latencies).  Device
+ * pointers; call shd_route_fw_table_async first (same stream or synchronised). */
+int shd_route_fw_rows_async(shd_route_t* ctx, const int32_t* d_src, int32_t ns, const int32_t* d_tgt,
+                            int32_t nt, int64_t ld, double* d_lat, double* d_rel, double* d_row_min,
+                            void* stream);
+
 /* Dense all-pairs shortest latencies by blocked min-plus Floyd-Warshall over all
  * vertices: d_dist is n x n (device, row-major).  Bit-exact against Dijkstra only
  * for integer-valued latencies (fl sums of subpaths are not left folds otherwise). */

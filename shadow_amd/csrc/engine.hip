@@ -13,6 +13,7 @@
 #include "sssp_k16.hpp"
 #include "sssp_delta.hpp"
 #include "direct_fw.hpp"
+#include "fw.hpp"
 
 using namespace shd;
 
@@ -76,6 +77,12 @@ struct shd_route {
     std::vector<uint16_t> h_ridx;
     std::vector<double> close;
     int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD
+    // K4 (fw.hpp): u16 all-pairs table + dense u16 weights, Np x Np (Np = n rounded to 64)
+    uint16_t* d_fwD = nullptr;
+    uint16_t* d_fwW = nullptr;
+    uint32_t* d_fwkey = nullptr;
+    size_t fwkey_cap = 0;
+    int fw_np = 0, fw_ready = 0;
     uint64_t device_bytes = 0;
     // host copies needed for lazy dense build
     std::vector<int32_t> e_src, e_dst;
@@ -738,6 +745,7 @@ void shd_route_destroy(shd_route_t* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->d_keys) (void)hipFree(c->d_keys);
+    if (c->d_fwkey) (void)hipFree(c->d_fwkey);
     for (void* p : c->allocs) (void)hipFree(p);
     delete c;
 }
@@ -1390,6 +1398,98 @@ int planned_host_rows(shd_route* c, const int32_t* src, int32_t ns, const int32_
     return soft;
 }
 }  // namespace
+
+// =============================================================================
+// K4: blocked min-plus Floyd-Warshall (fw.hpp)
+// =============================================================================
+namespace {
+constexpr int kFwMaxN = 12000;  // fw_rows keeps rel f64 + order i32 per vertex in LDS
+
+__global__ void fw_w16_kernel(const double* __restrict__ W, int n, int np, uint16_t* __restrict__ Wd) {
+    const long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (k >= (long long)np * np) return;
+    const int i = (int)(k / np), j = (int)(k % np);
+    uint16_t d = 0xFFFFu;  // self-loops never lie on a shortest path (w > 0)
+    if (i != j && i < n && j < n) {
+        const double w = W[(long long)i * n + j];
+        if (!isnan(w)) d = (uint16_t)w;
+    }
+    Wd[k] = d;
+}
+
+int fw_prepare(shd_route* c) {
+    if (c->d_fwD) return SHD_ROUTE_OK;
+    if (!c->integer_w || c->multigraph || c->n > kFwMaxN || c->k32_bound <= 0 || c->k32_bound >= 0xFFFF)
+        return SHD_ROUTE_EUNSUPPORTED;
+    int rc = ensure_dense(c);
+    if (rc) return rc;
+    const int np = (c->n + FW_T - 1) / FW_T * FW_T;
+    const size_t cells = (size_t)np * np;
+    if (hipMalloc((void**)&c->d_fwD, 2 * cells) != hipSuccess) return SHD_ROUTE_ENOMEM;
+    c->allocs.push_back(c->d_fwD);
+    if (hipMalloc((void**)&c->d_fwW, 2 * cells) != hipSuccess) return SHD_ROUTE_ENOMEM;
+    c->allocs.push_back(c->d_fwW);
+    c->fw_np = np;
+    const size_t lds = a16(sizeof(double) * c->n) + a16(sizeof(int) * c->n) + a16(sizeof(int) * (c->k32_bound + 2));
+    if (lds > kLdsBudget) return SHD_ROUTE_EUNSUPPORTED;
+    rc = hip_check(hipFuncSetAttribute((const void*)fw_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (rc) return rc;
+    const unsigned blocks = (unsigned)((cells + 255) / 256);
+    hipLaunchKernelGGL(fw_w16_kernel, dim3(blocks), dim3(256), 0, nullptr, c->d_W, c->n, np, c->d_fwW);
+    return hip_check(hipGetLastError());
+}
+}  // namespace
+
+extern "C" {
+
+int shd_route_fw_table_async(shd_route_t* c, void* stream) {
+    if (!c) return SHD_ROUTE_EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    int rc = fw_prepare(c);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const int np = c->fw_np, nb = np / FW_T;
+    const unsigned blocks = (unsigned)(((size_t)np * np + 255) / 256);
+    hipLaunchKernelGGL(fw_init_kernel, dim3(blocks), dim3(256), 0, st, c->d_W, c->n, np, c->d_fwD);
+    for (int kb = 0; kb < nb; kb++) {
+        hipLaunchKernelGGL(fw_diag_kernel, dim3(1), dim3(256), 0, st, c->d_fwD, np, kb);
+        if (nb > 1) {
+            hipLaunchKernelGGL(fw_panel_kernel, dim3(nb - 1, 2), dim3(256), 0, st, c->d_fwD, np, kb);
+            hipLaunchKernelGGL(fw_rest_kernel, dim3(nb - 1, nb - 1), dim3(256), 0, st, c->d_fwD, np, kb);
+        }
+    }
+    c->fw_ready = 1;
+    return hip_check(hipGetLastError());
+}
+
+int shd_route_fw_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const int32_t* d_tgt, int32_t nt,
+                            int64_t ld, double* d_lat, double* d_rel, double* d_row_min, void* stream) {
+    if (!c || ns < 0 || nt < 0 || (ns && !d_src) || (nt && !d_tgt) || ld < nt) return SHD_ROUTE_EINVAL;
+    if (!c->fw_ready) return SHD_ROUTE_EINVAL;  // shd_route_fw_table_async first
+    if (ns == 0) return SHD_ROUTE_OK;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    hipStream_t st = (hipStream_t)stream;
+    const int np = c->fw_np;
+    const size_t need = (size_t)ns * np;
+    if (need > c->fwkey_cap) {
+        if (c->d_fwkey) (void)hipFree(c->d_fwkey);
+        c->d_fwkey = nullptr;
+        c->fwkey_cap = 0;
+        if (hipMalloc((void**)&c->d_fwkey, need * sizeof(uint32_t)) != hipSuccess) return SHD_ROUTE_ENOMEM;
+        c->fwkey_cap = need;
+    }
+    hipLaunchKernelGGL(fw_parent_kernel, dim3(np / FW_T, (ns + FW_T - 1) / FW_T), dim3(256), 0, st, c->d_fwD,
+                       c->d_fwW, np, d_src, ns, c->d_fwkey);
+    FWRowsArgs a;
+    a.n = c->n; a.np = np; a.bound = c->k32_bound; a.D = c->d_fwD; a.key = c->d_fwkey; a.R = c->d_R;
+    a.vf = c->d_vf; a.self_w = c->d_self_w; a.self_r = c->d_self_r;
+    const size_t lds = a16(sizeof(double) * c->n) + a16(sizeof(int) * c->n) + a16(sizeof(int) * (c->k32_bound + 2));
+    hipLaunchKernelGGL(fw_rows_kernel, dim3(std::min(ns, 2048)), dim3(1024), lds, st, a, d_src, ns, d_tgt, nt,
+                       (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
+    return hip_check(hipGetLastError());
+}
+
+}  // extern "C"
 
 #ifdef SHD_STAMPS
 // Diagnostic builds only (not part of include/shd_route.h): per-source phase stamps.

@@ -1,0 +1,330 @@
+#pragma once
+// K4: blocked min-plus Floyd-Warshall for dense all-pairs tables,
+// and the SOURCE-row latency / reliability of the path it implies.
+//
+// No reference equivalent in Shadow 1.14: a complete graph never takes shortest paths
+// there (topology.c:1321-1323, 2019-2021: direct mode, K3).  K4 is the dense
+// alternative to per-source SSSP; its rows follow the same SOURCE(s,.) semantics as
+// shd_route_rows (topology.c:1407-1523, 1655-1875): lat is the left-fold path sum,
+// rel the source-first product along the engine tie rule's shortest-path tree.
+//
+// Integer latencies only (FW adds two subpath sums, so it is not a left fold: exact only
+// when every sum is an exact integer).  Distances are u16 (bound < 0xFFFF), two per
+// 32-bit lane, so a relaxation of two pairs is one v_pk_add_u16 (clamped: 0xFFFF stays
+// "no path") + one v_pk_min_u16.  VALU-bound by design: min-plus is not a multiply-add
+// contraction, so MFMA does not apply.
+//
+//  fw_init     D[i][j] = w(i,j) (0 on the diagonal, 0xFFFF = no edge), padded to 64
+//  fw_diag     the pivot tile: 64 dependent steps in LDS (one workgroup)
+//  fw_panel    row / column panel tiles: D* (x) P and P (x) D* with the closed pivot
+//              tile D* -- one tropical product each, no dependent steps
+//  fw_rest     every other tile: C = min(C, colpanel (x) rowpanel)
+//  The tropical product of two 64x64 u16 tiles: 256 threads, 4 rows x 4 columns each,
+//  A stored transposed in LDS so a thread's 4 rows at step k are one 8-byte read.
+//
+//  fw_parent   per (source s, vertex v): the tie-rule parent among the tight in-arcs
+//              (D[s][u] + w(u,v) == D[s][v]): largest w, then smallest u -- the key
+//              (0xFFFF - w) << 16 | u, minimised over u in 64-wide LDS chunks
+//  fw_rows     per source: reliability top-down in distance order (parents have smaller
+//              distance: w >= 1), rel[v] = rel[p] * r(p,v), f_t last; lat / rel rows out
+#include "common.hpp"
+
+namespace shd {
+
+constexpr int FW_T = 64;  // tile edge
+
+typedef unsigned short fw_us2 __attribute__((ext_vector_type(2)));
+
+__device__ inline uint32_t fw_pkadd(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(__builtin_bit_cast(fw_us2, a),
+                                                                      __builtin_bit_cast(fw_us2, b)));
+}
+__device__ inline uint32_t fw_pkmin(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(fw_us2, a),
+                                                                  __builtin_bit_cast(fw_us2, b)));
+}
+
+// D (Np x Np u16) from the dense W (n x n f64, NaN = no edge)
+__global__ void fw_init_kernel(const double* __restrict__ W, int n, int np, uint16_t* __restrict__ D) {
+    const long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (k >= (long long)np * np) return;
+    const int i = (int)(k / np), j = (int)(k % np);
+    uint16_t d = 0xFFFFu;
+    if (i == j) d = 0;
+    else if (i < n && j < n) {
+        const double w = W[(long long)i * n + j];
+        if (!isnan(w)) d = (uint16_t)w;
+    }
+    D[k] = d;
+}
+
+// one 64x64 tile product C = min(C, A (x) B); At is A transposed ([k][i]), B is [k][j];
+// the thread's C block (rows 4r.., cols 4c..) in acc[4][2] (packed column pairs)
+__device__ inline void fw_tile_product(const uint16_t* At, const uint16_t* Bt, uint32_t acc[4][2], int r, int c) {
+#pragma unroll 8
+    for (int k = 0; k < FW_T; k++) {
+        const uint2 a = *reinterpret_cast<const uint2*>(At + k * FW_T + 4 * r);
+        const uint2 b = *reinterpret_cast<const uint2*>(Bt + k * FW_T + 4 * c);
+        const uint32_t a2[4] = {(a.x & 0xFFFFu) * 0x10001u, (a.x >> 16) * 0x10001u, (a.y & 0xFFFFu) * 0x10001u,
+                                (a.y >> 16) * 0x10001u};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            acc[i][0] = fw_pkmin(acc[i][0], fw_pkadd(a2[i], b.x));
+            acc[i][1] = fw_pkmin(acc[i][1], fw_pkadd(a2[i], b.y));
+        }
+    }
+}
+
+// tile (ti, tj) of D <-> registers of the thread's 4x4 block
+__device__ inline void fw_load_block(const uint16_t* D, int np, int ti, int tj, int r, int c, uint32_t acc[4][2]) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint2 v = *reinterpret_cast<const uint2*>(D + (long long)(ti * FW_T + 4 * r + i) * np + tj * FW_T + 4 * c);
+        acc[i][0] = v.x; acc[i][1] = v.y;
+    }
+}
+__device__ inline void fw_store_block(uint16_t* D, int np, int ti, int tj, int r, int c, const uint32_t acc[4][2]) {
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        *reinterpret_cast<uint2*>(D + (long long)(ti * FW_T + 4 * r + i) * np + tj * FW_T + 4 * c) =
+            make_uint2(acc[i][0], acc[i][1]);
+}
+// a global tile into LDS, [row][col] (transpose = false) or [col][row]
+__device__ inline void fw_stage(const uint16_t* D, int np, int ti, int tj, uint16_t* L, bool transpose) {
+    for (int q = threadIdx.x; q < FW_T * FW_T / 4; q += 256) {
+        const int row = q / (FW_T / 4), c4 = (q % (FW_T / 4)) * 4;
+        const uint2 v = *reinterpret_cast<const uint2*>(D + (long long)(ti * FW_T + row) * np + tj * FW_T + c4);
+        if (!transpose) *reinterpret_cast<uint2*>(L + row * FW_T + c4) = v;
+        else {
+            L[(c4 + 0) * FW_T + row] = (uint16_t)(v.x & 0xFFFFu);
+            L[(c4 + 1) * FW_T + row] = (uint16_t)(v.x >> 16);
+            L[(c4 + 2) * FW_T + row] = (uint16_t)(v.y & 0xFFFFu);
+            L[(c4 + 3) * FW_T + row] = (uint16_t)(v.y >> 16);
+        }
+    }
+}
+
+// pivot tile kb: 64 dependent steps (D[i][j] = min(D[i][j], D[i][k] + D[k][j]))
+__global__ __launch_bounds__(256) void fw_diag_kernel(uint16_t* __restrict__ D, int np, int kb) {
+    __shared__ __attribute__((aligned(16))) uint16_t T[FW_T * FW_T];
+    const int r = threadIdx.x / 16, c = threadIdx.x % 16;
+    fw_stage(D, np, kb, kb, T, false);
+    __syncthreads();
+    for (int k = 0; k < FW_T; k++) {
+        uint32_t col[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) col[i] = (uint32_t)T[(4 * r + i) * FW_T + k] * 0x10001u;
+        const uint2 rowk = *reinterpret_cast<const uint2*>(T + k * FW_T + 4 * c);
+        uint32_t v[4][2];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint2 x = *reinterpret_cast<const uint2*>(T + (4 * r + i) * FW_T + 4 * c);
+            v[i][0] = fw_pkmin(x.x, fw_pkadd(col[i], rowk.x));
+            v[i][1] = fw_pkmin(x.y, fw_pkadd(col[i], rowk.y));
+        }
+        __syncthreads();  // every read of step k done before its writes
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            *reinterpret_cast<uint2*>(T + (4 * r + i) * FW_T + 4 * c) = make_uint2(v[i][0], v[i][1]);
+        __syncthreads();
+    }
+    for (int q = threadIdx.x; q < FW_T * FW_T / 4; q += 256) {
+        const int row = q / (FW_T / 4), c4 = (q % (FW_T / 4)) * 4;
+        *reinterpret_cast<uint2*>(D + (long long)(kb * FW_T + row) * np + kb * FW_T + c4) =
+            *reinterpret_cast<const uint2*>(T + row * FW_T + c4);
+    }
+}
+
+// panels of pivot kb: blockIdx.y = 0 row panel (kb, b), 1 column panel (b, kb), b != kb
+__global__ __launch_bounds__(256) void fw_panel_kernel(uint16_t* __restrict__ D, int np, int kb) {
+    __shared__ __attribute__((aligned(16))) uint16_t At[FW_T * FW_T];
+    __shared__ __attribute__((aligned(16))) uint16_t Bt[FW_T * FW_T];
+    const int nb = np / FW_T;
+    int b = blockIdx.x;
+    if (b >= kb) b++;
+    if (b >= nb) return;
+    const int r = threadIdx.x / 16, c = threadIdx.x % 16;
+    const bool rowp = blockIdx.y == 0;
+    const int ti = rowp ? kb : b, tj = rowp ? b : kb;
+    // row panel: C = D* (x) C (A = pivot, B = the panel); column panel: C = C (x) D*
+    fw_stage(D, np, rowp ? kb : ti, rowp ? kb : tj, At, true);
+    fw_stage(D, np, rowp ? ti : kb, rowp ? tj : kb, Bt, false);
+    __syncthreads();
+    uint32_t acc[4][2];
+    fw_load_block(D, np, ti, tj, r, c, acc);
+    fw_tile_product(At, Bt, acc, r, c);
+    fw_store_block(D, np, ti, tj, r, c, acc);
+}
+
+// every tile (i, j), i, j != kb: C = min(C, D[i][kb] (x) D[kb][j])
+__global__ __launch_bounds__(256) void fw_rest_kernel(uint16_t* __restrict__ D, int np, int kb) {
+    __shared__ __attribute__((aligned(16))) uint16_t At[FW_T * FW_T];
+    __shared__ __attribute__((aligned(16))) uint16_t Bt[FW_T * FW_T];
+    const int nb = np / FW_T;
+    int ti = blockIdx.y, tj = blockIdx.x;
+    if (ti >= kb) ti++;
+    if (tj >= kb) tj++;
+    if (ti >= nb || tj >= nb) return;
+    const int r = threadIdx.x / 16, c = threadIdx.x % 16;
+    fw_stage(D, np, ti, kb, At, true);
+    fw_stage(D, np, kb, tj, Bt, false);
+    __syncthreads();
+    uint32_t acc[4][2];
+    fw_load_block(D, np, ti, tj, r, c, acc);
+    fw_tile_product(At, Bt, acc, r, c);
+    fw_store_block(D, np, ti, tj, r, c, acc);
+}
+
+// parents: key[s][v] = min over u != v with D[s][u] + w(u,v) == D[s][v] of
+// (0xFFFF - w) << 16 | u (largest w, then smallest u: the engine tie rule).  Tiles of 64
+// sources x 64 targets; u in 64-wide chunks through LDS (D[s][u] transposed, w(u,v)).
+// Wd is the dense weight matrix as u16 (0xFFFF = no edge), Np x Np.
+__global__ __launch_bounds__(256) void fw_parent_kernel(const uint16_t* __restrict__ D, const uint16_t* __restrict__ Wd,
+                                                        int np, const int* __restrict__ src, int ns,
+                                                        uint32_t* __restrict__ key) {
+    __shared__ __attribute__((aligned(16))) uint16_t At[FW_T * FW_T];  // [u][s]
+    __shared__ __attribute__((aligned(16))) uint16_t Bt[FW_T * FW_T];  // [u][v]
+    const int r = threadIdx.x / 16, c = threadIdx.x % 16;
+    const int s0 = blockIdx.y * FW_T, v0 = blockIdx.x * FW_T;
+    // target distances of the thread's 4 sources x 4 targets
+    unsigned tgt[4][4], best[4][4];
+    int srow[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int si = s0 + 4 * r + i;
+        srow[i] = si < ns ? src[si] : 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            tgt[i][j] = D[(long long)srow[i] * np + v0 + 4 * c + j];
+            best[i][j] = 0xFFFFFFFFu;
+        }
+    }
+    for (int u0 = 0; u0 < np; u0 += FW_T) {
+        __syncthreads();
+        for (int q = threadIdx.x; q < FW_T * FW_T; q += 256) {
+            const int si = q / FW_T, uu = q % FW_T;  // At[u][s] = D[src[s0+si]][u0+uu]
+            const int sv = s0 + si < ns ? src[s0 + si] : 0;
+            At[uu * FW_T + si] = D[(long long)sv * np + u0 + uu];
+            const int ub = q / FW_T, vb = q % FW_T;  // Bt[u][v] = W[u0+ub][v0+vb]
+            Bt[ub * FW_T + vb] = Wd[(long long)(u0 + ub) * np + v0 + vb];
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int k = 0; k < FW_T; k++) {
+            const uint2 a = *reinterpret_cast<const uint2*>(At + k * FW_T + 4 * r);
+            const uint2 b = *reinterpret_cast<const uint2*>(Bt + k * FW_T + 4 * c);
+            const unsigned ds[4] = {a.x & 0xFFFFu, a.x >> 16, a.y & 0xFFFFu, a.y >> 16};
+            const unsigned wv[4] = {b.x & 0xFFFFu, b.x >> 16, b.y & 0xFFFFu, b.y >> 16};
+            const unsigned u = (unsigned)(u0 + k);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const unsigned kk = ((0xFFFFu - wv[j]) << 16) | u;
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if (wv[j] != 0xFFFFu && ds[i] + wv[j] == tgt[i][j]) best[i][j] = min(best[i][j], kk);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int si = s0 + 4 * r + i;
+        if (si >= ns) continue;
+#pragma unroll
+        for (int j = 0; j < 4; j++) key[(long long)si * np + v0 + 4 * c + j] = best[i][j];
+    }
+}
+
+// rows: per source (one workgroup), rel down the parent tree in distance order (LDS
+// buckets by distance), then the lat / rel rows for the targets; the self entry is the
+// batch self-loop (lat = w_ss, rel = (1*f_s)*r_ss) as in every SOURCE row
+struct FWRowsArgs {
+    int n, np, bound;
+    const uint16_t* D;
+    const uint32_t* key;     // [ns][np]
+    const double* R;         // dense 1 - loss, n x n (NaN = no edge)
+    const double* vf;
+    const double* self_w;
+    const double* self_r;
+};
+__global__ __launch_bounds__(1024) void fw_rows_kernel(FWRowsArgs a, const int* __restrict__ src, int ns,
+                                                       const int* __restrict__ tgt, int nt, long long ld,
+                                                       double* __restrict__ lat_out, double* __restrict__ rel_out,
+                                                       double* __restrict__ row_min, int* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // rel f64[n] | order int[n] | bucket starts int[bound + 2]
+    double* rel = reinterpret_cast<double*>(smem);
+    int* order = reinterpret_cast<int*>(smem + a16(sizeof(double) * a.n));
+    int* bstart = reinterpret_cast<int*>(smem + a16(sizeof(double) * a.n) + a16(sizeof(int) * a.n));
+    __shared__ unsigned long long rmin;
+    const int nbk = a.bound + 2;
+    for (int i = blockIdx.x; i < ns; i += gridDim.x) {
+        const int s = src[i];
+        if (s < 0 || s >= a.n) { if (threadIdx.x == 0) raise_err(err, SHD_ROUTE_EINVAL); continue; }
+        const uint16_t* Ds = a.D + (long long)s * a.np;
+        const uint32_t* Ks = a.key + (long long)i * a.np;
+        for (int b = threadIdx.x; b < nbk; b += blockDim.x) bstart[b] = 0;
+        if (threadIdx.x == 0) rmin = kInfBits;
+        __syncthreads();
+        // counting sort of the vertices by distance
+        for (int v = threadIdx.x; v < a.n; v += blockDim.x) {
+            const unsigned d = Ds[v];
+            if (d <= (unsigned)a.bound) atomicAdd(&bstart[d + 1], 1);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int b = 1; b < nbk; b++) bstart[b] += bstart[b - 1];
+        __syncthreads();
+        for (int v = threadIdx.x; v < a.n; v += blockDim.x) {
+            const unsigned d = Ds[v];
+            if (d <= (unsigned)a.bound) order[atomicAdd(&bstart[d], 1)] = v;
+        }
+        __syncthreads();
+        // bstart[d] now holds the end of bucket d; buckets in increasing distance
+        const double fs = a.vf[s];
+        const double cs = isnan(fs) ? 1.0 : 1.0 * fs;
+        if (threadIdx.x == 0) rel[s] = cs;
+        __syncthreads();
+        for (int d = 1; d <= a.bound; d++) {
+            const int b0 = bstart[d - 1], b1 = bstart[d];
+            if (b0 == b1) continue;
+            for (int q = b0 + (int)threadIdx.x; q < b1; q += blockDim.x) {
+                const int v = order[q];
+                const uint32_t k = Ks[v];
+                if (k == 0xFFFFFFFFu) { raise_err(err, SHD_ROUTE_EUNREACH); rel[v] = NAN; continue; }
+                const int p = (int)(k & 0xFFFFu);
+                rel[v] = rel[p] * a.R[(long long)p * a.n + v];
+            }
+            __syncthreads();
+        }
+        double lmin = INFINITY;
+        double* lrow = lat_out ? lat_out + (long long)i * ld : nullptr;
+        double* rrow = rel_out ? rel_out + (long long)i * ld : nullptr;
+        for (int j = threadIdx.x; j < nt; j += blockDim.x) {
+            const int t = tgt[j];
+            double L = NAN, Rv = NAN;
+            if (t < 0 || t >= a.n) raise_err(err, SHD_ROUTE_EINVAL);
+            else if (t == s) {
+                if (isnan(a.self_w[s])) raise_err(err, SHD_ROUTE_ENOEDGE);
+                else { L = 0.0 + a.self_w[s]; Rv = cs * a.self_r[s]; }
+            } else if (Ds[t] == 0xFFFFu) raise_err(err, SHD_ROUTE_EUNREACH);
+            else {
+                L = (double)Ds[t];
+                const double ft = a.vf[t];
+                Rv = isnan(ft) ? rel[t] : rel[t] * ft;
+            }
+            if (!isnan(L)) lmin = fmin(lmin, L);
+            if (lrow) __builtin_nontemporal_store(L, lrow + j);
+            if (rrow) __builtin_nontemporal_store(Rv, rrow + j);
+        }
+        if (row_min) {
+#pragma unroll
+            for (int dd = 32; dd >= 1; dd >>= 1) lmin = fmin(lmin, __shfl_xor(lmin, dd, 64));
+            if ((threadIdx.x & 63) == 0 && lmin < INFINITY) atomicMin(&rmin, as_u(lmin));
+            __syncthreads();
+            if (threadIdx.x == 0) row_min[i] = as_d(rmin);
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace shd

@@ -67,7 +67,7 @@ EXPORTS = (
     "shd_route_rows", "shd_route_rows_async", "shd_route_sync", "shd_route_direct",
     "shd_route_self", "shd_route_min_reduce_async", "shd_route_fw_async",
     "shd_route_plan_create", "shd_route_plan_destroy", "shd_route_plan_get_info", "shd_route_plan_rows",
-    "shd_route_rows_planned_async",
+    "shd_route_rows_planned_async", "shd_route_fw_table_async", "shd_route_fw_rows_async",
 )
 
 _lib = None
@@ -103,6 +103,10 @@ def load_library():
     L.shd_route_min_reduce_async.argtypes = [P, P, I64, P, P]
     L.shd_route_fw_async.restype = C.c_int
     L.shd_route_fw_async.argtypes = [P, P, P]
+    L.shd_route_fw_table_async.restype = C.c_int
+    L.shd_route_fw_table_async.argtypes = [P, P]
+    L.shd_route_fw_rows_async.restype = C.c_int
+    L.shd_route_fw_rows_async.argtypes = [P, P, I32, P, I32, I64, P, P, P, P]
     L.shd_route_plan_create.restype = C.c_int
     L.shd_route_plan_create.argtypes = [P, P, I32, I32, I32, C.POINTER(P)]
     L.shd_route_plan_destroy.argtypes = [P]
@@ -207,6 +211,19 @@ class RouteEngine:
                                                        C.c_void_p(d_out.data_ptr()),
                                                        C.c_void_p(stream) if stream else None)
         _check(rc, "shd_route_min_reduce_async")
+
+    def fw_table_async(self, stream=None):
+        """K4: the all-pairs u16 table by blocked min-plus Floyd-Warshall (kept on the device)."""
+        _check(load_library().shd_route_fw_table_async(self._h, C.c_void_p(stream) if stream else None),
+               "shd_route_fw_table_async")
+
+    def fw_rows_async(self, d_src, d_tgt, d_lat, d_rel, d_rowmin, stream=None, ld=None):
+        ns, nt = int(d_src.numel()), int(d_tgt.numel())
+        ld = nt if ld is None else int(ld)
+        ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        _check(load_library().shd_route_fw_rows_async(self._h, ptr(d_src), ns, ptr(d_tgt), nt, ld, ptr(d_lat),
+                                                      ptr(d_rel), ptr(d_rowmin), C.c_void_p(stream) if stream else None),
+               "shd_route_fw_rows_async")
 
     def plan(self, sources, world: int = 1, rank: int = 0) -> "RoutePlan":
         return RoutePlan(self, sources, world, rank)

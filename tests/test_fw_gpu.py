@@ -1,0 +1,94 @@
+"""GPU: K4 blocked min-plus Floyd-Warshall (fw.hpp) and its SOURCE rows, and the f64
+in-place variant, against the oracle.
+
+K4 has no reference equivalent (complete graphs take the direct path in Shadow 1.14,
+topology.c:1321-1323); its rows are held to the SOURCE(s,.) semantics of every other
+rows kernel: latency bit-exact (integer latencies: FW sums are exact), reliability
+bit-exact against the oracle's engine tie rule (vertex factors 1.0 here).
+"""
+import numpy as np
+import pytest
+
+from shadow_amd.graph import complete_graph, config, internet_like
+
+pytestmark = pytest.mark.gpu
+
+
+def _fw_rows(eng, S, T):
+    import torch
+    dev = torch.device("cuda", 0)
+    d_src = torch.from_numpy(np.ascontiguousarray(S, np.int32)).to(dev)
+    d_tgt = torch.from_numpy(np.ascontiguousarray(T, np.int32)).to(dev)
+    lat = torch.empty((len(S), len(T)), dtype=torch.float64, device=dev)
+    rel = torch.empty_like(lat)
+    mn = torch.empty(len(S), dtype=torch.float64, device=dev)
+    eng.fw_table_async()
+    eng.fw_rows_async(d_src, d_tgt, lat, rel, mn)
+    eng.sync()
+    return lat.cpu().numpy(), rel.cpu().numpy(), mn.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", ["k200", "ba300", "ties", "k130_odd"])
+def test_fw_rows_bitexact(oracle_mod, name):
+    from shadow_amd import route
+    from tests.golden import make_golden as mg
+    g = {"k200": lambda: complete_graph(200, seed=5), "ba300": lambda: internet_like(300, 3, seed=17),
+         "ties": lambda: mg._ties(300, 33), "k130_odd": lambda: complete_graph(130, seed=6)}[name]()
+    eng = route.RouteEngine(g)
+    T = np.arange(g.n, dtype=np.int32)
+    S = T[::3]
+    lat, rel, mn = _fw_rows(eng, S, T)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(S, T, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(rel, orel)
+    assert np.array_equal(mn, olat.min(axis=1))
+
+
+def test_fw_table_vs_oracle_floyd_warshall(oracle_mod):
+    """The K4 table (every pair, self distance 0) against the oracle's plain FW, and the
+    f64 in-place shd_route_fw_async against the same."""
+    import torch
+    from shadow_amd import route
+    g = complete_graph(256, seed=12)
+    d = np.full((g.n, g.n), np.inf)
+    np.fill_diagonal(d, 0.0)
+    for a, b, w in zip(g.src, g.dst, g.latency):
+        if a != b:
+            d[a, b] = min(d[a, b], w); d[b, a] = min(d[b, a], w)
+    ref = oracle_mod.floyd_warshall(d)
+    eng = route.RouteEngine(g)
+    T = np.arange(g.n, dtype=np.int32)
+    lat, _, _ = _fw_rows(eng, T, T)
+    off = ~np.eye(g.n, dtype=bool)
+    assert np.array_equal(lat[off], ref[off])
+    dd = torch.from_numpy(d.copy()).cuda()
+    eng.fw_async(dd)
+    eng.sync()
+    assert np.array_equal(dd.cpu().numpy(), ref)
+
+
+def test_c5_fw_rows_sampled(oracle_mod):
+    """C5 (complete K4000 + self-loops): the K4 table and rows of sampled sources against
+    the oracle's Dijkstra rows (SOURCE semantics) and against the KD rows."""
+    from shadow_amd import route
+    g = config("c5")
+    eng = route.RouteEngine(g)
+    assert eng.info["is_complete"] == 1
+    T = np.arange(g.n, dtype=np.int32)
+    S = np.array([0, 1, 777, 2048, 3999], np.int32)
+    lat, rel, mn = _fw_rows(eng, S, T)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(S, T, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(rel, orel)
+    klat, krel, _ = eng.rows(S, T, dispatch=False)
+    assert np.array_equal(lat, klat) and np.array_equal(rel, krel)
+
+
+def test_fw_unsupported_fractional():
+    from shadow_amd import route
+    g = internet_like(120, 2, seed=3)
+    g.latency = g.latency + 0.5
+    eng = route.RouteEngine(g)
+    with pytest.raises(route.RouteError) as e:
+        eng.fw_table_async()
+    assert e.value.code == route.EUNSUPPORTED

@@ -13,8 +13,11 @@ Fixtures are DATA: inputs and expected outputs.
   small_tables.npz        oracle eager tables (igraph tie rule) for small synthetic
                           graphs in every routing mode, latency cross-checked against
                           networkx at generation time
-  c2_rows.json            per-row SHA-256 of the C2 latency/reliability rows (engine tie
-                          rule) and the row minima; c3/c4 sampled rows likewise
+  rows_digests.json       per-row SHA-256 of the C2 latency/reliability rows (engine tie
+                          rule) and the row minima; c3/c4 sampled rows likewise; every
+                          row pinned by networkx at generation time (nx_pin.py: latency
+                          on every pair, rel along networkx's path on unique pairs), the
+                          counts in stats
 """
 from __future__ import annotations
 
@@ -211,21 +214,27 @@ def small_tables():
 
 
 def row_digests():
+    from tests.golden.nx_pin import nx_graph, pin_row
     out = {}
     for cfg, picks in (("c2", None), ("c3", 48), ("c4", 12)):
         g = config(cfg)
         og = O.OracleGraph(g)
+        G = nx_graph(g)
         T = g.targets()
         if picks is None:
             S = T
         else:
             S = T[np.linspace(0, len(T) - 1, num=picks).astype(int)]
         rows = []
-        stats = dict(pairs=0, unique=0, rel_diff_on_ties=0)
+        stats = dict(pairs=0, unique=0, rel_diff_on_ties=0, nx_latency_pairs_equal=0, nx_unique_rel_pairs_equal=0)
         for s in S:
             lat, rel, uq, hops = og.source_row(int(s), T, O.TIE_MINKEY)
             ilat, irel, iuq, _ = og.source_row(int(s), T, O.TIE_IGRAPH)
             assert np.array_equal(lat, ilat)
+            # independent pin: networkx latency (every t != s) and rel along its path on
+            # unique-shortest-path pairs; any mismatch stops the generator
+            nl, nr = pin_row(G, g, int(s), T, lat, rel, uq)
+            stats["nx_latency_pairs_equal"] += nl; stats["nx_unique_rel_pairs_equal"] += nr
             stats["pairs"] += len(T); stats["unique"] += int(uq.sum())
             stats["rel_diff_on_ties"] += int((rel != irel).sum())
             rows.append(dict(src=int(s), lat_sha=sha(lat), rel_sha=sha(rel), row_min=float(lat.min()),
@@ -238,8 +247,9 @@ def row_digests():
 
 if __name__ == "__main__":
     O.build()
-    json.dump(ref_kats(), open(os.path.join(HERE, "ref_kat.json"), "w"), indent=1)
-    json.dump(bundled(), open(os.path.join(HERE, "bundled_expected.json"), "w"), indent=1)
-    small_tables()
+    if "--rows-only" not in sys.argv:
+        json.dump(ref_kats(), open(os.path.join(HERE, "ref_kat.json"), "w"), indent=1)
+        json.dump(bundled(), open(os.path.join(HERE, "bundled_expected.json"), "w"), indent=1)
+        small_tables()
     if "--no-rows" not in sys.argv:
         row_digests()

@@ -39,6 +39,23 @@ def test_roundtrip_xz_bundled(topo, tmp_path):
     assert h.ids == g.ids
 
 
+def test_reference_bundled_file_bytes(topo):
+    """The reference's own resource/topology.graphml.xml.xz (committed as a fixture, byte
+    for byte) through the C loader: the arrays igraph_read_graph_graphml would hold
+    (document order, the file's own keys, ids and attribute types) equal the fixture
+    made from it, and validation as topology.c:565-1185 passes."""
+    g = _bundled()
+    h = topo.load_graphml(os.path.join(HERE, "golden", "topology.graphml.xml.xz"))
+    assert h.n == 183 and h.m == 16836 and not h.directed
+    assert np.array_equal(h.src, g.src) and np.array_equal(h.dst, g.dst)
+    assert np.array_equal(h.latency, g.latency) and np.array_equal(h.packetloss, g.packetloss)
+    assert np.array_equal(np.isnan(h.vertex_packetloss), np.isnan(g.vertex_packetloss))
+    assert np.array_equal(np.nan_to_num(h.vertex_packetloss, nan=-1), np.nan_to_num(g.vertex_packetloss, nan=-1))
+    assert h.ids == g.ids
+    # non-integer latencies (e.g. 2293.85): the generic f64 kernel path if ever forced
+    assert np.any(h.latency != np.floor(h.latency))
+
+
 def test_reference_style_config_topology(topo, tmp_path):
     # the embedded graph of src/test/tcp/tcp-blocking-lossy.test.shadow.config.xml (no vertex packetloss key)
     txt = """<graphml xmlns="http://graphml.graphdrawing.org/xmlns">

@@ -177,3 +177,29 @@ def test_cpu_baselines_consistent(oracle_mod):
     ref = float(np.sum(lat) + np.sum(rel))
     assert math.isclose(cs1, ref, rel_tol=1e-12) and math.isclose(cs2, ref, rel_tol=1e-12)
     assert used >= 1
+
+
+def test_c2_rows_pinned_by_networkx(oracle_mod):
+    """A slice of the C2 golden rows re-derived here: the oracle's rows match the committed
+    digests, networkx's latencies bit for bit, and Shadow's product along networkx's path
+    on every unique-shortest-path pair (tests/golden/nx_pin.py; make_golden.py pins every
+    C2 row and the sampled C3/C4 rows this way and records the counts)."""
+    import hashlib
+    import json
+    import os
+    from shadow_amd.graph import config
+    from tests.golden.nx_pin import nx_graph, pin_row
+    g = config("c2")
+    og = oracle_mod.OracleGraph(g)
+    G = nx_graph(g)
+    T = g.targets()
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "rows_digests.json")))["c2"]
+    by_src = {r["src"]: r for r in gold["rows"]}
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a, np.float64).tobytes()).hexdigest()
+    assert gold["stats"]["nx_latency_pairs_equal"] == 2000 * 1999
+    for s in T[::100]:
+        lat, rel, uq, _ = og.source_row(int(s), T, oracle_mod.TIE_MINKEY)
+        r = by_src[int(s)]
+        assert sha(lat) == r["lat_sha"] and sha(rel) == r["rel_sha"]
+        n_lat, n_rel = pin_row(G, g, int(s), T, lat, rel, uq)
+        assert n_lat == len(T) - 1 and n_rel == int(uq.sum()) - 1

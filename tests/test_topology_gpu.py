@@ -57,6 +57,50 @@ def test_example_config_graphml_kat(topo, tmp_path):
     assert t.runahead_ns() == 50_000_000
 
 
+def test_reference_bundled_file(topo):
+    """topology_new on the reference's own resource/topology.graphml.xml.xz (committed
+    byte for byte): complete -> every pair direct (topology.c:1877-1927); the whole
+    lookup table equals the committed digests, runahead 5 ms."""
+    import hashlib
+    exp = json.load(open(os.path.join(GOLD, "bundled_expected.json")))
+    t = topo.Topology.new(os.path.join(GOLD, "topology.graphml.xml.xz"))
+    n = t.vertex_count()
+    assert n == 183 and t.find_vertex("poi-112") == 0
+    t.attach_all(range(n))
+    lat, rel = t.table(range(n))
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a, np.float64).tobytes()).hexdigest()
+    assert sha(lat) == exp["lat_sha"] and sha(rel) == exp["rel_sha"]
+    assert t.min_path_latency() == exp["min_latency"] == 5.0 and t.runahead_ns() == 5_000_000
+
+
+def test_late_attach_with_concurrent_lookups(topo):
+    """Lookups running while another thread attaches vertices (a late attach retires the
+    filled cache; readers holding it stay valid), and packet counters carried over."""
+    import threading
+    g = internet_like(60, 2, seed=10)
+    t = topo.Topology.from_graph(g)
+    t.attach_all(range(0, 60, 2))
+    ref = {(a, b): t.get_latency(a, b) for a in range(0, 60, 6) for b in range(0, 60, 4)}
+    for _ in range(5):
+        t.increment_path_packet_counter(0, 4)
+    stop = threading.Event()
+    bad = []
+    def reader():
+        while not stop.is_set():
+            for (a, b), L in ref.items():
+                if t.get_latency(a, b) != L:
+                    bad.append((a, b))
+    th = [threading.Thread(target=reader) for _ in range(4)]
+    [x.start() for x in th]
+    for v in range(1, 60, 2):
+        t.attach(v)
+        t.get_latency(0, v)  # refills over the grown set
+    stop.set(); [x.join() for x in th]
+    assert not bad
+    assert t.packet_count(0, 4) == 5 and t.packet_count(4, 0) == 5
+    assert t.attached_count() == 60 and t.get_latency(1, 3) > 0
+
+
 def test_bundled_topology_xz(topo, tmp_path):
     z = np.load(os.path.join(GOLD, "bundled_topology.npz"))
     g = Graph(n=int(z["n"]), src=z["src"], dst=z["dst"], latency=z["latency"], packetloss=z["packetloss"],

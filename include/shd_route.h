@@ -175,6 +175,25 @@ int shd_route_rows_planned_async(shd_route_t* ctx, const shd_route_plan_t* plan,
                                  int32_t nt, int64_t ld, uint32_t flags, double* d_lat, double* d_rel,
                                  double* d_row_min, void* stream);
 
+/* ---- the eager fill of a dense Path cache ------------------------------------------
+ * The front end's cache (shd_topology.h) replaces topology.c's hash of Paths
+ * (topology.c:1284-1386) with an upper triangle over the attached vertices A (sorted):
+ * pair {A[i], A[j]}, i <= j, holds the Path of row i (first writer wins over both
+ * directions under ascending sources, topology.c:1307-1336) as interleaved (lat, rel)
+ * doubles at lr_out + 2 * (i * na - i * (i - 1) / 2 + (j - i)).  This fills the rows this
+ * rank owns (world/rank: the plan's partition; world 1: all) with one seeded plan: rows
+ * on the device, packed into the triangle layout and copied out in 512 MiB chunks on a
+ * second stream while the next chunk packs.  lr_out is host memory, pinned for full
+ * PCIe rate when it comes from shd_route_host_alloc.  *min_out = the smallest latency
+ * written (topology.c:1374-1385), *seconds_out = the wall time (nullable).  Flags as
+ * shd_route_rows (SHD_ROUTE_DISPATCH for the topology.c:2019 dispatch).  The rank's rows
+ * are held whole in HBM (2 x 8 x rows x na bytes + 2 GiB; C4 on one GPU: 41 GB): a
+ * larger request is SHD_ROUTE_ENOMEM (shard it over more devices). */
+int shd_route_fill_triangle(shd_route_t* ctx, const int32_t* A, int32_t na, int32_t world, int32_t rank,
+                            uint32_t flags, double* lr_out, double* min_out, double* seconds_out);
+void* shd_route_host_alloc(size_t bytes);  /* pinned host memory (NULL on failure) */
+void shd_route_host_free(void* p);
+
 /* K4: all-pairs shortest latencies by blocked min-plus
  * Floyd-Warshall over all vertices, u16 on the device (kept in the context).  Integer
  * latencies with every shortest path below 65535 ms, n <= 12000, simple graphs; else

@@ -11,7 +11,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 SOURCES = [os.path.join(HERE, "csrc", "engine.hip")]
-HEADERS = [os.path.join(HERE, "csrc", f) for f in ("common.hpp", "sssp_f64.hpp", "sssp_k32.hpp", "sssp_batch.hpp", "path_attr.hpp", "sssp_k16.hpp", "sssp_delta.hpp", "direct_fw.hpp")]
+HEADERS = [os.path.join(HERE, "csrc", f) for f in ("common.hpp", "sssp_f64.hpp", "sssp_k32.hpp", "sssp_batch.hpp", "path_attr.hpp", "sssp_k16.hpp", "sssp_delta.hpp", "direct_fw.hpp", "fw.hpp")]
 OUT = os.path.join(HERE, "libshd_route.so")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
          "-Wall", "-Wno-unused-result"]
@@ -43,9 +43,10 @@ def needs_build() -> bool:
 
 
 def build_diag(verbose: bool = False) -> str:
-    """Diagnostic build with per-phase s_memtime stamps (tools/stamps.py); never shipped."""
+    """Diagnostic build with per-phase s_memtime stamps (tools/stamps.py) and the retired K16
+    kernel (SHD_ROUTE_KERNEL=k16); never shipped."""
     out = os.path.join(HERE, "libshd_route_diag.so")
-    cmd = [HIPCC, *FLAGS, "-DSHD_STAMPS", "-o", out, *SOURCES]
+    cmd = [HIPCC, *FLAGS, "-DSHD_STAMPS", "-DSHD_DIAG", "-o", out, *SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
@@ -58,7 +59,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-    front_deps = FRONT_SOURCES + [os.path.join(ROOT, "include", "shd_topology.h"), OUT]
+    front_deps = FRONT_SOURCES + [os.path.join(ROOT, "include", f) for f in ("shd_topology.h", "shd_route.h")] + [OUT]
     if force or not os.path.exists(FRONT_OUT) or any(os.path.getmtime(p) > os.path.getmtime(FRONT_OUT)
                                                      for p in front_deps):
         build_front(verbose)

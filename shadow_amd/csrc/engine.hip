@@ -2,6 +2,7 @@
 #include "common.hpp"
 
 #include <array>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <queue>
@@ -10,7 +11,9 @@
 #include "sssp_k32.hpp"
 #include "sssp_batch.hpp"
 #include "path_attr.hpp"
-#include "sssp_k16.hpp"
+#ifdef SHD_DIAG
+#include "sssp_k16.hpp"  // K16: superseded by KD, kept for the diagnostic build only
+#endif
 #include "sssp_delta.hpp"
 #include "direct_fw.hpp"
 #include "fw.hpp"
@@ -310,6 +313,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
         rc = upload(c, &c->d_kb_arc, packed);
         if (rc) return rc;
     }
+#ifdef SHD_DIAG
     // K16: u16 distances in LDS, one 1024-thread workgroup per source
     const bool want_k16 = force && !strcmp(force, "k16");
     {
@@ -329,6 +333,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
         if (rc) return rc;
         c->k16 = 1;
     }
+#endif
     // KD delta-stepping: bucket width ~ the 12th percentile of arc latencies (>= 1), so
     // ~12% of arcs are light; light in-arcs are the tail of each (-w)-sorted in-row
     const bool want_kd = !force || !strcmp(force, "kd") || !strcmp(force, "auto");
@@ -764,7 +769,7 @@ int shd_route_get_info(const shd_route_t* c, shd_route_info_t* info) {
     info->lds_resident = (c->lds || c->sel) ? 1 : 0;
     info->kernel = c->sel;
     info->dist_bound = c->k32_bound;
-    info->block = c->sel == 2 ? KB_BLOCK : c->sel == 3 ? K16_BLOCK : c->sel == 4 ? c->kd_block
+    info->block = c->sel == 2 ? KB_BLOCK : c->sel == 3 ? 1024 : c->sel == 4 ? c->kd_block
                 : c->sel == 1 ? c->k32_block : kBlock;
     info->reserved = c->sel == 4 ? c->kd_delta : c->sel == 2 ? c->kb_fused : 0;
     info->device_bytes = c->device_bytes;
@@ -834,6 +839,7 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         if (hipMemsetAsync(c->d_kd_next, 0, sizeof(int), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
         return kd_launch(c, k, c->d_kd_next, d_src, ns, d_tgt, nt, ld, d_lat, d_rel, d_row_min, st);
     }
+#ifdef SHD_DIAG
     if (c->sel == 3 && !(dispatch && c->prefer_direct)) {
         DevK16 k;
         k.n = c->n; k.bound = c->k32_bound; k.row = c->d_row; k.oarc = c->d_k16_oarc; k.row_in = c->d_k32_row_in;
@@ -843,6 +849,7 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
                            (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_k16_ws, c->k16_stride);
         return hip_check(hipGetLastError());
     }
+#endif
     if (c->sel == 1 && !(dispatch && c->prefer_direct)) {
         DevK32 k;
         k.n = c->n; k.bound = c->k32_bound; k.row = c->d_row; k.arc = c->d_arc; k.row_in = c->d_k32_row_in;
@@ -1487,6 +1494,139 @@ int shd_route_fw_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, co
     hipLaunchKernelGGL(fw_rows_kernel, dim3(std::min(ns, 2048)), dim3(1024), lds, st, a, d_src, ns, d_tgt, nt,
                        (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
     return hip_check(hipGetLastError());
+}
+
+}  // extern "C"
+
+// =============================================================================
+// Eager fill of the front end's dense upper-triangle Path cache
+// =============================================================================
+namespace {
+// pack rows [r0, r1) of the planned table into the triangle layout: row r (source A[i],
+// i = pos[r]) keeps targets j >= i, as interleaved (lat, rel) pairs; one workgroup per
+// row; row minima over the kept entries (NaN skipped) into *mn (u64 bits)
+__global__ __launch_bounds__(256) void tri_pack_kernel(const double* __restrict__ lat, const double* __restrict__ rel,
+                                                       long long ld, const int* __restrict__ pos,
+                                                       const long long* __restrict__ off, int r0, int r1, int na,
+                                                       double* __restrict__ out, unsigned long long* __restrict__ mn) {
+    for (int r = r0 + blockIdx.x; r < r1; r += gridDim.x) {
+        const int i = pos[r];
+        const double* lr = lat + (long long)r * ld;
+        const double* rr = rel + (long long)r * ld;
+        double* o = out + 2 * (off[r] - off[r0]);
+        double m = INFINITY;
+        for (int j = i + threadIdx.x; j < na; j += 256) {
+            const double L = lr[j];
+            o[2 * (j - i)] = L;
+            o[2 * (j - i) + 1] = rr[j];
+            if (!isnan(L)) m = fmin(m, L);
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) m = fmin(m, __shfl_xor(m, d, 64));
+        if ((threadIdx.x & 63) == 0 && m < INFINITY) atomicMin(mn, as_u(m));
+    }
+}
+}  // namespace
+
+extern "C" {
+
+void* shd_route_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return nullptr;
+    return p;
+}
+
+void shd_route_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int shd_route_fill_triangle(shd_route_t* c, const int32_t* A, int32_t na, int32_t world, int32_t rank, uint32_t flags,
+                            double* lr_out, double* min_out, double* seconds_out) {
+    if (!c || na < 0 || (na && (!A || !lr_out)) || world < 1 || rank < 0 || rank >= world) return SHD_ROUTE_EINVAL;
+    if (min_out) *min_out = INFINITY;
+    if (na == 0) return SHD_ROUTE_OK;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    auto t0 = std::chrono::steady_clock::now();
+    shd_route_plan_t* P = nullptr;
+    int rc = shd_route_plan_create(c, A, na, world, rank, &P);
+    if (rc) return rc;
+    std::unique_ptr<shd_route_plan, void (*)(shd_route_plan*)> guard(P, shd_route_plan_destroy);
+    const int nr = (int)P->row_pos.size();
+    if (nr == 0) return SHD_ROUTE_OK;
+    // triangle offsets of this rank's rows (host: pair index of (i, i)), their sizes
+    std::vector<long long> off(nr + 1);
+    auto tri0 = [&](long long i) { return i * (long long)na - i * (i - 1) / 2; };
+    for (int r = 0; r < nr; r++) off[r] = tri0(P->row_pos[r]);
+    off[nr] = off[nr - 1] + (na - P->row_pos[nr - 1]);
+    std::vector<long long> roff(nr + 1, 0);  // packed offsets (pairs) in plan row order
+    for (int r = 0; r < nr; r++) roff[r + 1] = roff[r] + (na - P->row_pos[r]);
+    const size_t table = sizeof(double) * (size_t)nr * (size_t)na;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    const size_t stage_pairs = (size_t)32 << 20;  // 512 MiB of (lat, rel) per staging buffer
+    if (2 * table + 4 * stage_pairs * 8 + ((size_t)1 << 30) > fr) return SHD_ROUTE_ENOMEM;
+    DevBuf dtgt, dlat, drel, dpos, doff, dstage[2], dmn;
+    if ((rc = dtgt.alloc(sizeof(int32_t) * na)) || (rc = dlat.alloc(table)) || (rc = drel.alloc(table)) ||
+        (rc = dpos.alloc(sizeof(int) * nr)) || (rc = doff.alloc(sizeof(long long) * (nr + 1))) ||
+        (rc = dstage[0].alloc(16 * stage_pairs)) || (rc = dstage[1].alloc(16 * stage_pairs)) ||
+        (rc = dmn.alloc(sizeof(unsigned long long))))
+        return rc;
+    hipStream_t cs = nullptr, xs = nullptr;
+    if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&xs, hipStreamNonBlocking) != hipSuccess)
+        return SHD_ROUTE_EDEVICE;
+    std::vector<int> posv(P->row_pos.begin(), P->row_pos.end());
+    bool ok = hipMemcpy(dtgt.p, A, sizeof(int32_t) * na, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(dpos.p, posv.data(), sizeof(int) * nr, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(doff.p, roff.data(), sizeof(long long) * (nr + 1), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemsetAsync(dmn.p, 0xFF, sizeof(unsigned long long), cs) == hipSuccess;
+    if (ok) rc = shd_route_rows_planned_async(c, P, (const int32_t*)dtgt.p, na, na, flags, (double*)dlat.p,
+                                              (double*)drel.p, nullptr, cs);
+    else rc = SHD_ROUTE_EDEVICE;
+    // pack chunks of rows on the compute stream, copy them out on the copy stream; with
+    // rows in triangle order (one rank) a chunk is one contiguous range of the cache
+    hipEvent_t packed[2], copied[2];
+    for (int b = 0; b < 2; b++) { (void)hipEventCreateWithFlags(&packed[b], hipEventDisableTiming); (void)hipEventCreateWithFlags(&copied[b], hipEventDisableTiming); }
+    int buf = 0;
+    bool first[2] = {true, true};
+    for (int r0 = 0; r0 < nr && !rc; buf ^= 1) {
+        int r1 = r0;
+        while (r1 < nr && roff[r1 + 1] - roff[r0] <= (long long)stage_pairs) r1++;
+        if (r1 == r0) r1 = r0 + 1;  // (a row longer than a stage buffer cannot happen: na < 2^25)
+        if (!first[buf] && hipStreamWaitEvent(cs, copied[buf], 0) != hipSuccess) { rc = SHD_ROUTE_EDEVICE; break; }
+        first[buf] = false;
+        hipLaunchKernelGGL(tri_pack_kernel, dim3(std::min(r1 - r0, 4096)), dim3(256), 0, cs, (const double*)dlat.p,
+                           (const double*)drel.p, (long long)na, (const int*)dpos.p, (const long long*)doff.p, r0, r1,
+                           na, (double*)dstage[buf].p, (unsigned long long*)dmn.p);
+        if (hipGetLastError() != hipSuccess || hipEventRecord(packed[buf], cs) != hipSuccess ||
+            hipStreamWaitEvent(xs, packed[buf], 0) != hipSuccess) { rc = SHD_ROUTE_EDEVICE; break; }
+        // copy: consecutive rows with consecutive triangle offsets go out in one piece
+        for (int a = r0; a < r1;) {
+            int b = a + 1;
+            while (b < r1 && off[b] == off[b - 1] + (na - P->row_pos[b - 1])) b++;
+            const size_t pairs = (size_t)(roff[b] - roff[a]);
+            if (hipMemcpyAsync(lr_out + 2 * off[a], (double*)dstage[buf].p + 2 * (roff[a] - roff[r0]), 16 * pairs,
+                               hipMemcpyDeviceToHost, xs) != hipSuccess) { rc = SHD_ROUTE_EDEVICE; break; }
+            a = b;
+        }
+        if (hipEventRecord(copied[buf], xs) != hipSuccess) rc = SHD_ROUTE_EDEVICE;
+        r0 = r1;
+    }
+    if (hipStreamSynchronize(cs) != hipSuccess || hipStreamSynchronize(xs) != hipSuccess) rc = rc ? rc : SHD_ROUTE_EDEVICE;
+    for (int b = 0; b < 2; b++) { (void)hipEventDestroy(packed[b]); (void)hipEventDestroy(copied[b]); }
+    (void)hipStreamDestroy(cs); (void)hipStreamDestroy(xs);
+    if (rc) return rc;
+    const int soft = take_err(c);
+    if (soft && soft != SHD_ROUTE_ENOEDGE && soft != SHD_ROUTE_EUNREACH) return soft;
+    unsigned long long mb = 0;
+    if (hipMemcpy(&mb, dmn.p, sizeof(mb), hipMemcpyDeviceToHost) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    if (min_out) {
+        double m;
+        std::memcpy(&m, &mb, sizeof(m));
+        *min_out = mb == ~0ull ? INFINITY : m;
+    }
+    if (seconds_out) *seconds_out = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return soft;
 }
 
 }  // extern "C"

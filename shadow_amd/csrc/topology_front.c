@@ -133,7 +133,7 @@ static uint64_t* pc_slot(pcmap* m, uint64_t key);
 static void pcache_free(pcache* c) {
     while (c) {
         pcache* o = c->older;
-        free(c->A); free(c->cid); free(c->lr); free(c->cnt);
+        free(c->A); free(c->cid); shd_route_host_free(c->lr); free(c->cnt);
         for (int k = 0; k < PC_STRIPES; k++) { pthread_mutex_destroy(&c->pc[k].lock); free(c->pc[k].s); }
         free(c);
         c = o;
@@ -270,44 +270,24 @@ typedef struct {
     pcache* c;
     int dev, nd;
     int rc;
+    double min_lat;
 } fill_job;
 
-/* Row chunks are dealt round-robin over the fill threads (one per device context);
- * chunk k covers sources A[k*R, (k+1)*R) and targets A[k*R, na) (the upper triangle it
- * stores). */
-#define FILL_ROWS 256
-
+/* One thread per device context: the rows its plan share owns (shd_route_fill_triangle:
+ * one seeded plan, rows packed into this triangle and copied out on the device), so the
+ * eager fill is one call per device instead of a batch per chunk of sources. */
 static void* fill_worker(void* arg) {
     fill_job* job = arg;
-    shd_topology_t* t = job->t;
     pcache* c = job->c;
-    const int32_t na = c->na;
-    double* lbuf = malloc(sizeof(double) * (size_t)FILL_ROWS * (size_t)na);
-    double* rbuf = malloc(sizeof(double) * (size_t)FILL_ROWS * (size_t)na);
-    if (!lbuf || !rbuf) { job->rc = SHD_ROUTE_ENOMEM; free(lbuf); free(rbuf); return NULL; }
-    const int32_t nchunks = (na + FILL_ROWS - 1) / FILL_ROWS;
-    for (int32_t k = job->dev; k < nchunks && !job->rc; k += job->nd) {
-        const int32_t i0 = k * FILL_ROWS;
-        const int32_t rows = (na - i0) < FILL_ROWS ? (na - i0) : FILL_ROWS;
-        const int32_t nt = na - i0;
-        int rc = shd_route_rows(t->eng[job->dev], c->A + i0, rows, c->A + i0, nt, SHD_ROUTE_DISPATCH,
-                                lbuf, rbuf, NULL);
-        /* ENOEDGE: a self pair without a self-loop; the rows are complete and that entry
-         * is NaN, i.e. not stored by the batch, as the reference skips the failed target
-         * (topology.c:1488-1495, 1812-1870); fill_locked resolves it below.  EUNREACH
-         * (not after the strong-connectivity check at load) leaves the pair unstored */
-        if (rc && rc != SHD_ROUTE_ENOEDGE && rc != SHD_ROUTE_EUNREACH) { job->rc = rc; break; }
-        for (int32_t r = 0; r < rows; r++) {
-            const int32_t i = i0 + r;
-            const size_t base = tri(na, i, i);
-            /* row i stores targets j >= i: offsets (j - i0) in the returned row */
-            const double* lr_ = lbuf + (size_t)r * nt + r;
-            const double* rr_ = rbuf + (size_t)r * nt + r;
-            double* o = c->lr + 2 * base;
-            for (int32_t q = 0; q < na - i; q++) { o[2 * q] = lr_[q]; o[2 * q + 1] = rr_[q]; }
-        }
-    }
-    free(lbuf); free(rbuf);
+    double mn = INFINITY;
+    int rc = shd_route_fill_triangle(job->t->eng[job->dev], c->A, c->na, job->nd, job->dev, SHD_ROUTE_DISPATCH, c->lr,
+                                     &mn, NULL);
+    /* ENOEDGE: a self pair without a self-loop; that entry stays NaN, i.e. not stored by
+     * the batch, as the reference skips the failed target (topology.c:1488-1495,
+     * 1812-1870); fill_locked resolves it below.  EUNREACH (not after the
+     * strong-connectivity check at load) leaves the pair unstored */
+    if (rc && rc != SHD_ROUTE_ENOEDGE && rc != SHD_ROUTE_EUNREACH) job->rc = rc;
+    job->min_lat = mn;
     return NULL;
 }
 
@@ -356,11 +336,12 @@ static int fill_locked(shd_topology_t* t) {
         if (t->attached[v]) { c->cid[v] = c->na; c->A[c->na++] = v; }
     }
     const size_t ntri = (size_t)c->na * ((size_t)c->na + 1) / 2;
-    c->lr = malloc(2 * sizeof(double) * (ntri ? ntri : 1));
+    /* pinned: the device copies its rows straight into the triangle at full PCIe rate */
+    c->lr = shd_route_host_alloc(2 * sizeof(double) * (ntri ? ntri : 1));
     c->cnt = calloc(ntri ? ntri : 1, sizeof(uint32_t));
     if (!c->lr || !c->cnt) { pcache_free(c); return SHD_ROUTE_ENOMEM; }
-    for (size_t k = 0; k < 2 * ntri; k++) c->lr[k] = NAN;  /* a chunk that fails stays unstored */
     int rc = SHD_ROUTE_OK;
+    double mn_fill = INFINITY;
     if (c->na) {
         pthread_t th[FILL_MAX_DEV];
         fill_job jobs[FILL_MAX_DEV];
@@ -368,12 +349,14 @@ static int fill_locked(shd_topology_t* t) {
         const int nd = t->ndev;  /* <= FILL_MAX_DEV (finish_new) */
         for (int d = 0; d < nd; d++) {
             jobs[d].t = t; jobs[d].c = c; jobs[d].dev = d; jobs[d].nd = nd; jobs[d].rc = 0;
+            jobs[d].min_lat = INFINITY;
             started[d] = pthread_create(&th[d], NULL, fill_worker, &jobs[d]) == 0;
         }
         for (int d = 0; d < nd; d++) {
             if (started[d]) pthread_join(th[d], NULL);
-            else fill_worker(&jobs[d]);  /* no thread: this device's chunks inline */
+            else fill_worker(&jobs[d]);  /* no thread: this device's rows inline */
             if (jobs[d].rc && !rc) rc = jobs[d].rc;
+            if (jobs[d].min_lat < mn_fill) mn_fill = jobs[d].min_lat;
         }
     }
     if (rc) { pcache_free(c); return rc; }
@@ -394,16 +377,16 @@ static int fill_locked(shd_topology_t* t) {
                 const size_t k = tri(c->na, c->cid[sv[q]], c->cid[sv[q]]);
                 LAT(c, k) = sl[q];
                 REL(c, k) = sr[q];
+                if (!isnan(sl[q]) && sl[q] < mn_fill) mn_fill = sl[q];
             }
             free(sl); free(sr);
         }
         free(sv);
         if (rc) { pcache_free(c); return rc; }
     }
-    double mn = 0;
-    for (size_t k = 0; k < ntri; k++)  /* topology.c:1375: minLat == 0 means unset */
-        if (!isnan(LAT(c, k)) && (mn == 0 || LAT(c, k) < mn)) mn = LAT(c, k);
-    c->min_lat = mn;
+    /* minimumPathLatency over every stored Path (topology.c:1374-1385; 0 = unset): the
+     * fill's per-device minima over the pairs it wrote, and the self pairs above */
+    c->min_lat = mn_fill < INFINITY ? mn_fill : 0;
     if (t->retired) carry_counters(t->retired, c);
     t->fill_seconds += now_s() - t0;
     __atomic_store_n(&t->cache, c, __ATOMIC_RELEASE);

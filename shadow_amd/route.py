@@ -68,6 +68,7 @@ EXPORTS = (
     "shd_route_self", "shd_route_min_reduce_async", "shd_route_fw_async",
     "shd_route_plan_create", "shd_route_plan_destroy", "shd_route_plan_get_info", "shd_route_plan_rows",
     "shd_route_rows_planned_async", "shd_route_fw_table_async", "shd_route_fw_rows_async",
+    "shd_route_fill_triangle", "shd_route_host_alloc", "shd_route_host_free",
 )
 
 _lib = None
@@ -103,6 +104,11 @@ def load_library():
     L.shd_route_min_reduce_async.argtypes = [P, P, I64, P, P]
     L.shd_route_fw_async.restype = C.c_int
     L.shd_route_fw_async.argtypes = [P, P, P]
+    L.shd_route_fill_triangle.restype = C.c_int
+    L.shd_route_fill_triangle.argtypes = [P, P, I32, I32, I32, U32, P, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.shd_route_host_alloc.restype = P
+    L.shd_route_host_alloc.argtypes = [C.c_size_t]
+    L.shd_route_host_free.argtypes = [P]
     L.shd_route_fw_table_async.restype = C.c_int
     L.shd_route_fw_table_async.argtypes = [P, P]
     L.shd_route_fw_rows_async.restype = C.c_int
@@ -225,6 +231,19 @@ class RouteEngine:
                                                       ptr(d_rel), ptr(d_rowmin), C.c_void_p(stream) if stream else None),
                "shd_route_fw_rows_async")
 
+    def fill_triangle(self, attached, out, world: int = 1, rank: int = 0, dispatch: bool = True):
+        """shd_route_fill_triangle: this rank's rows of the front end's upper-triangle cache
+        over the sorted `attached` vertices into `out` (a PinnedBuffer or any object with
+        .ptr; 16 * na * (na + 1) / 2 bytes).  Returns (min latency written, seconds)."""
+        A = np.ascontiguousarray(attached, np.int32)
+        mn, sec = C.c_double(), C.c_double()
+        rc = load_library().shd_route_fill_triangle(self._h, _p(A), len(A), int(world), int(rank),
+                                                   DISPATCH if dispatch else 0, C.c_void_p(out.ptr),
+                                                   C.byref(mn), C.byref(sec))
+        if rc not in (OK, ENOEDGE, EUNREACH):
+            raise RouteError(rc, "shd_route_fill_triangle")
+        return mn.value, sec.value
+
     def plan(self, sources, world: int = 1, rank: int = 0) -> "RoutePlan":
         return RoutePlan(self, sources, world, rank)
 
@@ -272,3 +291,28 @@ class RoutePlan:
             self.eng._h, self._h, ptr(d_tgt), nt, ld, DISPATCH if dispatch else 0, ptr(d_lat), ptr(d_rel),
             ptr(d_rowmin), C.c_void_p(stream) if stream else None)
         _check(rc, "shd_route_rows_planned_async")
+
+
+class PinnedBuffer:
+    """Pinned host memory (shd_route_host_alloc) viewed as float64."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        self.ptr = load_library().shd_route_host_alloc(self.nbytes)
+        if not self.ptr:
+            raise RouteError(ENOMEM, "shd_route_host_alloc")
+
+    def array(self):
+        buf = (C.c_double * (self.nbytes // 8)).from_address(self.ptr)
+        return np.frombuffer(buf, dtype=np.float64)
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            load_library().shd_route_host_free(C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -173,6 +173,47 @@ def test_multi_context_fill_equals_single(topo):
     assert t1.min_path_latency() == t2.min_path_latency()
 
 
+@pytest.mark.parametrize("devices", [(0,), (0, 0)])
+def test_fill_c3_matches_golden_rows(topo, devices):
+    """The eager fill at C3 (9,337 attached vertices, a 43.6M-pair triangle in pinned host
+    memory) through shd_route_fill_triangle: one seeded plan per context (two contexts:
+    the plan's forest partition, rows out of triangle order).  The golden-sampled rows
+    read back through the getters: latency equal to the golden digests (the table is
+    symmetric); reliability, on the pairs the row's own source wrote (targets at or after
+    it in attach order, first writer wins: topology.c:1307-1336), equal to the engine
+    rows, which must themselves hash to the golden digests."""
+    import hashlib
+    from shadow_amd import route
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a, np.float64).tobytes()).hexdigest()
+    dig = json.load(open(os.path.join(GOLD, "rows_digests.json")))["c3"]
+    g = config("c3")
+    T = g.targets()
+    t = topo.Topology.from_graph(g, devices=devices)
+    t.attach_all(T)
+    sec = t.fill()
+    assert sec > 0
+    rows = dig["rows"][::4]
+    S = np.array([r["src"] for r in rows], np.int32)
+    eng = route.RouteEngine(g)
+    lat, rel, mn = eng.rows(S, T)
+    pos = {int(v): i for i, v in enumerate(sorted(int(x) for x in T))}
+    for k, r in enumerate(rows):
+        assert sha(lat[k]) == r["lat_sha"] and sha(rel[k]) == r["rel_sha"]
+        s = r["src"]
+        fl = np.array([t.get_latency(s, int(d)) for d in T])
+        assert sha(fl) == r["lat_sha"], s
+        own = np.array([pos[int(d)] >= pos[s] for d in T])
+        fr = np.array([t.get_reliability(s, int(d)) for d in T])
+        assert np.array_equal(fr[own], rel[k][own]), s
+    # minimumPathLatency (topology.c:1374-1385): a lightest arc between two attached
+    # vertices is their shortest path, so the minimum is that arc or a self pair
+    att = np.zeros(g.n, bool)
+    att[T] = True
+    both = att[g.src] & att[g.dst] & (g.src != g.dst)
+    selfs = [t.get_latency(int(v), int(v)) for v in T]
+    assert t.min_path_latency() == min(float(g.latency[both].min()), min(selfs))
+
+
 def test_dump_paths(topo, tmp_path):
     import ctypes
     g = internet_like(12, 2, seed=2)

@@ -1,0 +1,117 @@
+"""End-to-end eager fill through the C front end (shd_topology_fill: every attached pair's
+Path, topology.c:1284-1386 + 1407-1523 for all sources) at C3 / C4 on the GPU box.
+
+Reports, per config: attach time, fill wall time (plan + rows on the device + pack +
+D2H into the pinned triangle), the triangle's bytes and the rate they land in host
+memory at, and the process's peak host RSS.  The reference's equivalent is one igraph
+Dijkstra per source on one CPU core.
+
+  python tools/fill_bench.py --configs c3,c4 [--devices 0] [--out profiles/r02_fill.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import resource
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def rss_gb():
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6  # kB -> GB
+
+
+def breakdown(g, T, dev):
+    """The same fill straight through the engine (shd_route_fill_triangle), split into:
+    pinning the triangle, planning, the rows on the device into HBM, and the whole fill
+    (plan + rows + pack + D2H) twice: the first into freshly pinned pages, then warm."""
+    import numpy as np
+    import torch
+    from shadow_amd import route
+    eng = route.RouteEngine(g, device=dev)
+    A = np.sort(T).astype(np.int32)
+    na = len(A)
+    t0 = time.perf_counter()
+    buf = route.PinnedBuffer(16 * (na * (na + 1) // 2))
+    pin_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    plan = eng.plan(A)
+    plan_s = time.perf_counter() - t0
+    d = torch.device("cuda", dev)
+    d_tgt = torch.from_numpy(A).to(d)
+    lat = torch.empty((na, na), dtype=torch.float64, device=d)
+    rel = torch.empty_like(lat)
+    plan.rows_async(d_tgt, lat, rel, None)
+    eng.sync()
+    t0 = time.perf_counter()
+    plan.rows_async(d_tgt, lat, rel, None)
+    eng.sync()
+    rows_s = time.perf_counter() - t0
+    del lat, rel
+    plan.close()
+    torch.cuda.empty_cache()
+    _, cold = eng.fill_triangle(A, buf)
+    _, warm = eng.fill_triangle(A, buf)
+    arr = buf.array()
+    probe = float(arr[2 * (na - 1)])  # pair (A[0], A[na-1])
+    buf.close()
+    eng.close()
+    return {"pin_s": round(pin_s, 4), "plan_s": round(plan_s, 4), "rows_hbm_s": round(rows_s, 4),
+            "fill_cold_s": round(cold, 4), "fill_warm_s": round(warm, 4),
+            "d2h_GBps_warm": round(16 * (na * (na + 1) // 2) / max(1e-9, warm - plan_s - rows_s) / 1e9, 2),
+            "probe_latency": probe}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c3,c4")
+    ap.add_argument("--devices", default="0", help="comma list of device ids (one context each)")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.init()  # torch's HIP runtime first (tests/conftest.py)
+    from shadow_amd import topology
+    from shadow_amd.graph import config
+    topology.load_library()
+    devs = tuple(int(x) for x in a.devices.split(","))
+    out = []
+    for cfg in a.configs.split(","):
+        g = config(cfg)
+        T = g.targets()
+        t0 = time.perf_counter()
+        t = topology.Topology.from_graph(g, devices=devs)
+        t_new = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        t.attach_all(T)
+        t_att = time.perf_counter() - t0
+        rss0 = rss_gb()
+        t0 = time.perf_counter()
+        sec = t.fill()
+        wall = time.perf_counter() - t0
+        na = len(T)
+        pairs = na * (na + 1) // 2
+        tri_bytes = 16 * pairs
+        lat = t.get_latency(int(T[0]), int(T[-1]))
+        rec = {"config": cfg, "n": g.n, "attached": na, "contexts": len(devs), "new_s": round(t_new, 3),
+               "attach_s": round(t_att, 3), "fill_s": round(sec, 4), "fill_wall_s": round(wall, 4),
+               "triangle_pairs": pairs, "triangle_bytes": tri_bytes,
+               "host_write_GBps": round(tri_bytes / sec / 1e9, 2), "pairs_per_s": round(pairs / sec),
+               "peak_rss_gb_before_fill": round(rss0, 2), "peak_rss_gb": round(rss_gb(), 2),
+               "min_path_latency": t.min_path_latency(), "probe_latency": lat}
+        t.close()
+        del t
+        if len(devs) == 1:
+            rec["engine"] = breakdown(g, T, devs[0])
+        print(json.dumps(rec), flush=True)
+        out.append(rec)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -26,6 +26,7 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["SHD_ROUTE_KERNEL"] = "kd"
+    os.environ["SHD_ROUTE_KDGRID"] = "7"  # few workgroup slots: few forced roots, deep seed chains
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from shadow_amd import route
     from shadow_amd.graph import internet_like

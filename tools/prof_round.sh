@@ -13,9 +13,10 @@ ks() {  # name bench-args...
     -- python3 bench.py --no-cpu-baseline --verify 0 "$@" > gpurun_out/prof_$tag/$name.json 2> gpurun_out/prof_$tag/$name.err \
     || { echo "kernel trace $name failed"; tail -5 gpurun_out/prof_$tag/$name.err; exit 1; }
 }
-ks c2 --steps 20 --warmup 5
-ks c3 --config c3 --steps 5 --warmup 2
-ks c4 --config c4 --steps 3 --warmup 1 --sources 4096
+ks c2 --config c2 --steps 20 --warmup 5
+ks c3 --config c3 --steps 10 --warmup 2
+ks c4 --config c4 --steps 5 --warmup 1
+ks c5 --config c5 --steps 5 --warmup 1
 pmc() {  # cfg counter bench-args...
   local cfg=$1 ctr=$2; shift 2
   timeout -s KILL 120 rocprofv3 --pmc $ctr -d gpurun_out/prof_$tag/pmc_$cfg/$ctr -o run --output-format csv \
@@ -24,11 +25,11 @@ pmc() {  # cfg counter bench-args...
   cp gpurun_out/prof_$tag/pmc_$cfg/$ctr/run_counter_collection.csv gpurun_out/prof_$tag/pmc_$cfg/$(echo $ctr | tr A-Z a-z | sed 's/_size//')_counter_collection.csv
 }
 [ "${PROF_PMC:-1}" = 0 ] && { echo prof done; exit 0; }
-pmc c2 FETCH_SIZE --steps 5 --warmup 2
-pmc c2 WRITE_SIZE --steps 5 --warmup 2
+pmc c2 FETCH_SIZE --config c2 --steps 5 --warmup 2
+pmc c2 WRITE_SIZE --config c2 --steps 5 --warmup 2
 [ "${PROF_PMC}" = c2 ] && { echo prof done; exit 0; }
-pmc c4 FETCH_SIZE --config c4 --steps 2 --warmup 1 --sources 4096
-pmc c4 WRITE_SIZE --config c4 --steps 2 --warmup 1 --sources 4096
+pmc c4 FETCH_SIZE --config c4 --steps 2 --warmup 1
+pmc c4 WRITE_SIZE --config c4 --steps 2 --warmup 1
 pmc c3 FETCH_SIZE --config c3 --steps 2 --warmup 1
 pmc c3 WRITE_SIZE --config c3 --steps 2 --warmup 1
 echo prof done

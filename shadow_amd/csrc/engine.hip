@@ -71,6 +71,7 @@ struct shd_route {
     uint32_t* d_kd_lrec = nullptr;  // light in-arc records (2 x u32 per arc)
     double* d_kd_rtab = nullptr;    // distinct reliabilities
     int kd_nlight = 0, kd_nrtab = 1, kd_walk = 0, kd_packed = 0, kd_fused = 0;
+    int has_vf = 0;  // some vertex has a packet-loss factor (else f_v is absent everywhere)
     char* d_kd_ws = nullptr;
     int* d_kd_next = nullptr;  // KD source queue counter
     // host copies for seeded planning (shd_route_plan_*): out-CSR, rtab index per arc and
@@ -354,7 +355,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
         int blk = n > 16384 ? 1024 : 256;
         if (const char* e = getenv("SHD_ROUTE_KDBLOCK")) {
             const int b = atoi(e);
-            if (b == 256 || b == 512 || b == 768 || b == 1024) blk = b;
+            if (b == 256 || b == 1024) blk = b;  // (512/768: the phase-A ring sizing assumes 256 or 1024)
         }
         const size_t base = kd_dispatch(blk, [&](auto B) { return kd_lds_bytes<decltype(B)::value>(n, 0); });
         if (base + 2 * 512 <= kLdsBudget) {
@@ -569,7 +570,10 @@ DevDelta kd_args(const shd_route* c) {
     k.row = c->d_row; k.orec = c->d_kd_orec; k.oridx = c->d_kd_oridx;
     k.nnz = c->nnz; k.lrow = c->d_kd_lstart; k.lrec = reinterpret_cast<const uint2*>(c->d_kd_lrec); k.nlight = c->kd_nlight;
     k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab; k.walk = c->kd_walk; k.packed = c->kd_packed;
-    k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;
+    k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg; k.has_vf = c->has_vf; k.dflags = 0;
+#ifdef SHD_STAMPS
+    if (const char* e = getenv("SHD_ROUTE_DFLAGS")) k.dflags = atoi(e);
+#endif
     k.jobs = nullptr; k.drow = nullptr; k.drow_out = nullptr; k.prow = nullptr; k.rstride = 0; k.evcap = c->n;
     k.done = nullptr;
     // tests shrink the tie-event list to force the unseeded rerun of overflowing rows
@@ -703,7 +707,7 @@ int shd_route_create(shd_route_t** out, const shd_graph_t* g, int device) {
     std::vector<double> vf(n, NAN);
     if (g->vertex_packetloss)
         for (int v = 0; v < n; v++)
-            if (!std::isnan(g->vertex_packetloss[v])) vf[v] = (1.0f - g->vertex_packetloss[v]);
+            if (!std::isnan(g->vertex_packetloss[v])) { vf[v] = (1.0f - g->vertex_packetloss[v]); c->has_vf = 1; }
 
     int rc = SHD_ROUTE_OK;
     if (!rc) rc = upload(c, &c->d_row, row);
@@ -1221,9 +1225,9 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // seed chains below them are short: C4 1 GPU 52.9 -> 51.0 ms, an 8-way rank
         // 12.8 -> 10.0 ms, C3 4.0 -> 3.4 ms), and seed chains are at most `depth` rows long
         // default depth cap: about half the rows each workgroup slot runs in turn, so that
-        // seed chains are shorter than a slot's queue (C4: 195 rows per slot, no cap in
-        // effect; C3: 9 per slot, cap 4: the critical path, not the work, bounds C3)
-        int kseeds = 2, nroot_min = c->kd_slots, depth = std::max(3, nj / std::max(1, 2 * c->kd_slots));
+        // seed chains are shorter than a slot's queue, and at least 8 (C4: 195 rows per
+        // slot, no cap in effect; C3: 9 per slot, cap 8: 3.5 -> 3.1 ms against cap 4)
+        int kseeds = 2, nroot_min = c->kd_slots, depth = std::max(8, nj / std::max(1, 2 * c->kd_slots));
         if (const char* e = getenv("SHD_ROUTE_SEEDS")) kseeds = std::max(1, std::min(KD_SEEDS, atoi(e)));
         if (const char* e = getenv("SHD_ROUTE_SEED_ROOTS")) nroot_min = std::max(0, atoi(e));
         if (const char* e = getenv("SHD_ROUTE_SEED_DEPTH")) depth = std::max(1, atoi(e));

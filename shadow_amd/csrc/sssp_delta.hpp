@@ -79,6 +79,10 @@ constexpr uint32_t KD_SRC_MARK = 0xFFFFFFFEu;  // parent record of the source it
 // (a min of consistent labellings), and a vertex keeping D0 takes the best (tie rule) of
 // the parents p_{u_j}(v) of the seeds that attain the min, and of its tie events.  Two
 // seeds leave 3-4% of the vertices to improve on C3/C4 (one seed: 14-20%).
+// global (address space 1) pointers for non-inlined helpers: flat accesses would count in
+// lgkmcnt too, so every LDS wait would also wait for the output stores
+#define KD_GLOBAL __attribute__((address_space(1)))
+
 constexpr int KD_SEEDS = 2;
 struct KDJob {
     int row;               // output row
@@ -123,6 +127,8 @@ struct DevDelta {
     const double* __restrict__ vf;
     const double* __restrict__ self_w;
     const double* __restrict__ self_r;
+    int has_vf;                         // some vertex factor present (else vf is all NaN: not read)
+    int dflags;                         // diagnostic builds: 1 = skip the output-row stores
     unsigned long long* dbg;            // SHD_STAMPS builds: 32 words per source
 };
 
@@ -132,6 +138,8 @@ struct DevDelta {
 // accumulated in LDS (sm->acc) and written out once per source: a global read-modify-
 // write inside the timed regions would drain the wave's vmcnt and distort them
 #define KD_ACCP (sm->acc)
+#define KD_OUT (!(dflags & 1))
+#define KD_DFLAGS g.dflags
 #define KD_STAMP(slot) do { if (tid == 0) sm->acc[slot] = __builtin_amdgcn_s_memtime(); } while (0)
 #define KD_COUNT(slot, x) do { if (lane == 0 && (x)) atomicAdd(&sm->acc[slot], (unsigned long long)(x)); } while (0)
 #define KD_MARK() do { if (tid == 0) kd_t = __builtin_amdgcn_s_memtime(); } while (0)
@@ -139,6 +147,8 @@ struct DevDelta {
 #define KD_FLUSH() do { lds_barrier(); if (g.dbg && i >= 0) for (int q_ = tid; q_ < 32; q_ += B) g.dbg[(size_t)i * 32 + q_] = sm->acc[q_]; lds_barrier(); if (tid < 32) sm->acc[tid] = 0; lds_barrier(); } while (0)
 #else
 #define KD_ACCP nullptr
+#define KD_OUT true
+#define KD_DFLAGS 0
 #define KD_STAMP(slot) do { } while (0)
 #define KD_COUNT(slot, x) do { } while (0)
 #define KD_MARK() do { } while (0)
@@ -159,6 +169,7 @@ struct KDSmall {
     int next;           // the workgroup's next source index
     int nev;            // seeded: tie events the writer wave stored
     int evovf;          // seeded: more tie events than the slice holds (rerun unseeded)
+    int tsorted;        // the target list is strictly increasing: positions from tmask/tpre
     KDJob job;          // the current job (kept in LDS: read where needed, not held in
                         // registers across phase A, whose expansion needs all of them)
 #ifdef SHD_STAMPS
@@ -171,12 +182,17 @@ struct KDSmall {
 // phase A, and the phase B/C vertex lists (u16 x qcap + i32 x qcap) afterwards.
 template <int B>
 struct KDLayout {
-    size_t wmark, wkey, wimp, dist, pend, fix, wmin, work, ring, rrec, qv, qbeg, rix, rtabl, total;
+    size_t tmask, tpre, wmark, wkey, wimp, dist, pend, fix, wmin, work, ring, rrec, qv, qbeg, rix, rtabl, total;
     int qcap;
     __host__ __device__ static KDLayout make(int n, int rc, int rr) {
         KDLayout L;
         const size_t nw = (size_t)(n + 63) / 64;
         size_t o = a16(sizeof(KDSmall));
+        // target set of the launch (kept for every source): a bit per vertex and the
+        // exclusive popcount prefix per word, so an output position is rank(v) with no
+        // global load (output loops never wait behind their own stores: one vmcnt)
+        L.tmask = o; o += a16(8 * nw);
+        L.tpre = o;  o += a16(4 * nw);
         L.dist = o;  o += a16(sizeof(uint16_t) * (size_t)(n + 1));
         // everything after dist is re-initialised per source or written before it is read:
         // the path walk of phase C reuses it for the parent-arc reliability indices (u8 x n)
@@ -383,6 +399,339 @@ __device__ inline int kd_next_source(int* ctr, int* slot, int tid, bool all_queu
     return i;
 }
 
+// Phases C/D of one row (lat row, parent copy, reliability by walks or level sweeps, rel
+// row, row min), called once per row.  Not inlined, on purpose: see the call site.
+template <int B>
+__device__ __attribute__((noinline)) void kd_output(const int n, const int nw, const int nt, const long long ld, const int i,
+                                                    const int s, const double cs, const double sw_s, const double sr_s,
+                                                    const int tsorted, const unsigned rmask, const int rc,
+                                                    const KD_GLOBAL int* __restrict__ tgt, KD_GLOBAL double* __restrict__ lat_out,
+                                                    KD_GLOBAL double* __restrict__ rel_out, KD_GLOBAL double* __restrict__ row_min,
+                                                    int* __restrict__ err, const KD_GLOBAL uint32_t* __restrict__ wpr,
+                                                    KD_GLOBAL double* __restrict__ relv, const int walk,
+                                                    const KD_GLOBAL double* __restrict__ rtab, const int nrtab,
+                                                    const KD_GLOBAL double* __restrict__ vf, const int has_vf, const int dflags) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int RR = kd_rr<B>();
+    const KDLayout<B> L = KDLayout<B>::make(n, rc, RR);
+    KDSmall* sm = reinterpret_cast<KDSmall*>(smem);
+    const int tid = threadIdx.x, lane = tid & 63;
+    uint16_t* dist = reinterpret_cast<uint16_t*>(smem + L.dist);
+    unsigned long long* pend = reinterpret_cast<unsigned long long*>(smem + L.pend);
+    unsigned long long* fix = reinterpret_cast<unsigned long long*>(smem + L.fix);
+    uint16_t* qv = reinterpret_cast<uint16_t*>(smem + L.qv);
+    const unsigned long long* tmask = reinterpret_cast<const unsigned long long*>(smem + L.tmask);
+    const unsigned* tpre = reinterpret_cast<const unsigned*>(smem + L.tpre);
+    const int qcap = L.qcap;
+    auto tpos = [&](int v) __attribute__((always_inline)) {
+        const unsigned long long wd = tmask[v >> 6], bit = 1ull << (v & 63);
+        return (wd & bit) ? (int)tpre[v >> 6] + __popcll(wd & (bit - 1ull)) : -1;
+    };
+    struct { int walk; const KD_GLOBAL double* rtab; int nrtab; const KD_GLOBAL double* vf; int has_vf; } g = {walk, rtab, nrtab, vf, has_vf};
+#ifdef SHD_STAMPS
+    unsigned long long kd_t = __builtin_amdgcn_s_memtime();
+#endif
+    (void)lane; (void)dflags;
+    // helper rows (i < 0, multi-GPU plans) only seed others: no output, no phase C
+    KD_GLOBAL double* lrow = lat_out && i >= 0 ? lat_out + (long long)i * ld : nullptr;
+    KD_GLOBAL double* rrow = rel_out && i >= 0 ? rel_out + (long long)i * ld : nullptr;
+    double lmin = INFINITY;
+    auto lat_of = [&](int t) __attribute__((always_inline)) {
+        double Lv;
+        if (t < 0 || t >= n) { raise_err(err, SHD_ROUTE_EINVAL); Lv = NAN; }
+        else if (t == s) {
+            if (isnan(sw_s)) { raise_err(err, SHD_ROUTE_ENOEDGE); Lv = NAN; }
+            else { Lv = 0.0 + sw_s; lmin = fmin(lmin, Lv); }
+        } else if (dist[t] == 0xFFFFu) { raise_err(err, SHD_ROUTE_EUNREACH); Lv = NAN; }
+        else { Lv = (double)dist[t]; lmin = fmin(lmin, Lv); }
+        return Lv;
+    };
+    if (tsorted) {
+        for (int v = tid; v < (i >= 0 ? n : 0); v += B) {
+            const int j = tpos(v);
+            if (j < 0) continue;
+            const double Lv = lat_of(v);
+            if (lrow && KD_OUT) __builtin_nontemporal_store(Lv, lrow + j);
+        }
+    } else {
+        for (int j = tid; j < (i >= 0 ? nt : 0); j += B) {
+            const double Lv = lat_of(tgt[j]);
+            if (lrow && KD_OUT) __builtin_nontemporal_store(Lv, lrow + j);
+        }
+    }
+    wait_stores();  // wpr of phase B visible to the whole workgroup
+    if (tid == 0) { sm->deep = 0; sm->rmin = kInfBits; }
+    __syncthreads();
+
+    KD_ACC(18);
+    // dist is dead: its LDS becomes the parent array
+    uint16_t* parv = dist;
+    if (g.walk && rrow) {
+        // ---- C': reliability by walking each target's tree path in LDS -------------
+        // parv u16 + rix u8 (index of the parent arc's reliability) + rtab in LDS; each
+        // target walks <= KD_MAXD arcs to the source, then folds the product source-first
+        // (the order the level sweep multiplies in, so the bits agree)
+        // rtl[KD_ONE] = 1.0 is the source's own "arc" (a walk parked at the source keeps
+        // multiplying by an exact 1.0) and rtl[KD_NAN] marks unreachable vertices
+        uint8_t* rixl = reinterpret_cast<uint8_t*>(smem + L.rix);
+        double* rtl = reinterpret_cast<double*>(smem + L.rtabl);
+        for (int k = tid; k < 256; k += B)
+            rtl[k] = k < g.nrtab ? g.rtab[k] : k == KD_ONE ? 1.0 : NAN;
+        for (int v0 = tid; v0 < n; v0 += B * 8) {
+            uint32_t pr[8], dv8[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                pr[q] = wpr[min(v0 + q * B, n - 1)];
+                dv8[q] = dist[min(v0 + q * B, n - 1)];
+            }
+            // (each thread overwrites only the dist entries it read itself)
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int v = v0 + q * B;
+                if (v >= n) continue;
+                const bool src_v = v == s, unr = !src_v && dv8[q] == 0xFFFFu;
+                parv[v] = src_v || unr ? (uint16_t)s : (uint16_t)(pr[q] & 0xFFFFu);
+                rixl[v] = src_v ? (uint8_t)KD_ONE : unr ? (uint8_t)KD_NAN
+                                                 : (uint8_t)min((pr[q] >> 16) & rmask, (uint32_t)(g.nrtab - 1));
+            }
+        }
+        __syncthreads();
+        KD_ACC(19);
+        // sorted targets: one pass over the vertices, positions from the LDS mask (no
+        // global load behind the previous group's stores); else over the target list
+        const int lim = tsorted ? n : nt;
+        for (int j0 = tid; j0 < lim; j0 += KD_WQ * B) {
+            // KD_WQ targets per thread: independent parent chains in flight.  A chain that
+            // reaches the source stays there (parv[s] = s, factor 1.0), so a step is two LDS
+            // reads and a byte insert, and the wave stops when every chain is parked.
+            int t2[KD_WQ], cur[KD_WQ], jq[KD_WQ];
+            uint32_t pk[KD_WQ][KD_MAXD / 4];
+#pragma unroll
+            for (int q = 0; q < KD_WQ; q++) {
+                const int j = j0 + q * B;
+                if (tsorted) {
+                    jq[q] = j < n ? tpos(j) : -1;
+                    t2[q] = jq[q] >= 0 ? j : -1;
+                } else {
+                    jq[q] = j < nt ? j : -1;
+                    t2[q] = j < nt ? tgt[j] : -1;
+                }
+                cur[q] = t2[q] >= 0 && t2[q] < n ? t2[q] : s;
+#pragma unroll
+                for (int k = 0; k < KD_MAXD / 4; k++) pk[q][k] = 0u;
+            }
+            // blocks of 4 arcs (parked chains multiply an exact 1.0, so the padding is
+            // harmless): one packed word per chain and block keeps the loop off the VALU
+            int nb = 0;  // blocks walked, wave-uniform (unrolled: pk stays in registers)
+#pragma unroll
+            for (int b = 0; b < KD_MAXD / 4; b++) {
+                bool any = false;
+#pragma unroll
+                for (int q = 0; q < KD_WQ; q++) any = any || cur[q] != s;
+                if (!__any(any)) break;
+                uint32_t acc[KD_WQ];
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    uint32_t p[KD_WQ], rx[KD_WQ];
+#pragma unroll
+                    for (int q = 0; q < KD_WQ; q++) { p[q] = parv[cur[q]]; rx[q] = rixl[cur[q]]; }
+#pragma unroll
+                    for (int q = 0; q < KD_WQ; q++) {
+                        acc[q] = e == 0 ? rx[q] : (acc[q] | (rx[q] << (8 * e)));
+                        cur[q] = (int)p[q];
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < KD_WQ; q++) pk[q][b] = acc[q];
+                nb = b + 1;
+            }
+            {
+                bool any = false;
+#pragma unroll
+                for (int q = 0; q < KD_WQ; q++) any = any || cur[q] != s;
+                if (any) sm->deep = 1;  // the level sweep below redoes the row
+            }
+            double rr[KD_WQ];
+#pragma unroll
+            for (int q = 0; q < KD_WQ; q++) rr[q] = cs;
+#pragma unroll
+            for (int k4 = KD_MAXD / 4 - 1; k4 >= 0; k4--) {  // source-first: the last arc walked first
+                if (k4 >= nb) continue;  // (uniform)
+                uint32_t wq[KD_WQ];
+#pragma unroll
+                for (int q = 0; q < KD_WQ; q++) wq[q] = pk[q][k4];
+#pragma unroll
+                for (int e = 3; e >= 0; e--) {
+                    double x[KD_WQ];
+#pragma unroll
+                    for (int q = 0; q < KD_WQ; q++) x[q] = rtl[(wq[q] >> (8 * e)) & 0xFFu];
+#pragma unroll
+                    for (int q = 0; q < KD_WQ; q++) rr[q] *= x[q];
+                }
+            }
+            double f2[KD_WQ];
+#pragma unroll
+            for (int q = 0; q < KD_WQ; q++) f2[q] = g.has_vf ? g.vf[(t2[q] >= 0 && t2[q] < n) ? t2[q] : s] : (double)NAN;
+#pragma unroll
+            for (int q = 0; q < KD_WQ; q++) {
+                const int j = jq[q];
+                if (j < 0) continue;
+                const int t = t2[q];
+                double Rv = NAN;
+                if (t >= 0 && t < n) {
+                    if (t == s) Rv = isnan(sw_s) ? NAN : cs * sr_s;
+                    else Rv = isnan(f2[q]) ? rr[q] : rr[q] * f2[q];
+                }
+                if (KD_OUT) __builtin_nontemporal_store(Rv, rrow + j);
+            }
+        }
+        __syncthreads();
+        KD_ACC(13);
+        KD_STAMP(3);
+    }
+    const bool sweep = i >= 0 && (!(g.walk && rrow) || sm->deep);
+    if (sweep) {
+    // parent records: parent | ridx << 16 (writer wave and phase B), KD_SRC_MARK at s
+    for (int v0 = tid; v0 < n; v0 += B * 8) {
+        uint32_t pr[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) pr[q] = wpr[min(v0 + q * B, n - 1)];
+        double rr[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) rr[q] = g.rtab[min((int)((pr[q] >> 16) & rmask), g.nrtab - 1)];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int v = v0 + q * B;
+            if (v >= n) continue;
+            const bool src_v = pr[q] == KD_SRC_MARK;
+            parv[v] = src_v ? (uint16_t)v : (uint16_t)(pr[q] & 0xFFFFu);
+            relv[v] = src_v ? cs : -rr[q];
+        }
+    }
+    for (int k = tid; k < nw; k += B) {
+        unsigned long long mk = (k == nw - 1 && (n & 63)) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
+        if (k == (s >> 6)) mk &= ~(1ull << (s & 63));
+        pend[k] = mk;
+        fix[k] = 0ull;
+    }
+    wait_stores();
+    __syncthreads();
+    KD_ACC(19);
+
+    if (tid == 0) sm->qtail[0] = sm->qtail[1] = 0;
+    lds_barrier();
+    // ---- C: reliability down the tree ------------------------------------------
+    // per level: pending vertices whose parent is done are compacted into qv, then one
+    // thread per listed vertex loads relv[parent] and its own -r and stores the product
+    for (int c = 0;; c ^= 1) {
+        KD_COUNT(12, tid == 0 ? 1 : 0);
+        if (tid == 0) sm->qtail[c ^ 1] = 0;
+        for (int k0 = 0; k0 < nw; k0 += B) {
+            const int k = k0 + tid;
+            unsigned long long b = k < nw ? pend[k] : 0ull, ready = 0ull;
+            while (b) {  // ready = pending vertices whose parent is done (LDS only)
+                int v4[4];
+                pop4(&b, k, v4);
+                int p4[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) p4[q] = (int)parv[v4[q] >= 0 ? v4[q] : 0];
+                unsigned long long pw[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) pw[q] = pend[p4[q] >> 6];
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (v4[q] >= 0 && !((pw[q] >> (p4[q] & 63)) & 1ull)) ready |= 1ull << (v4[q] & 63);
+            }
+            const int cnt = __popcll(ready);
+            int incl = kd_wave_incl_sum(cnt);
+            int base = 0;
+            if (lane == 63 && incl) base = atomicAdd(&sm->qtail[c], incl);
+            base = __builtin_amdgcn_readlane(base, 63);
+            int pos = base + incl - cnt;
+            unsigned long long listed = 0ull;
+            b = ready;
+            while (b && pos < qcap) {
+                const int bi = __ffsll((long long)b) - 1;
+                b &= b - 1;
+                qv[pos++] = (uint16_t)((k << 6) + bi);
+                listed |= 1ull << bi;
+            }
+            if (k < nw) fix[k] = listed;
+        }
+        lds_barrier();
+        KD_ACC(13);
+        const int cnt = min(sm->qtail[c], qcap);
+        if (cnt == 0) break;
+        for (int j0 = 0; j0 < cnt; j0 += B * 4) {
+            int v4[4], p4[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int j = j0 + q * B + tid;
+                v4[q] = j < cnt ? (int)qv[j] : -1;
+                p4[q] = (int)parv[v4[q] >= 0 ? v4[q] : 0];
+            }
+            double xp[4], xv[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                xp[q] = relv[p4[q]];
+                xv[q] = relv[v4[q] >= 0 ? v4[q] : 0];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (v4[q] >= 0) relv[v4[q]] = xp[q] * (-xv[q]);
+        }
+        wait_stores();  // this level's relv visible before its vertices count as done
+        KD_ACC(14);
+        lds_barrier();
+        for (int k = tid; k < nw; k += B) {
+            const unsigned long long r = fix[k];
+            if (r) pend[k] &= ~r;
+        }
+        lds_barrier();
+        KD_ACC(15);
+    }
+    KD_STAMP(3);
+
+    // ---- D: rel row out + row min ----------------------------------------------
+    if (rrow) {
+        for (int j0 = tid; j0 < nt; j0 += B * 4) {
+            int t4[4];
+            double x4[4], f4[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int j = j0 + q * B;
+                t4[q] = j < nt ? tgt[j] : s;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int t = (t4[q] >= 0 && t4[q] < n) ? t4[q] : s;
+                x4[q] = relv[t];
+                f4[q] = g.has_vf ? g.vf[t] : (double)NAN;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int j = j0 + q * B;
+                if (j >= nt) continue;
+                const int t = t4[q];
+                double Rv = NAN;
+                if (t >= 0 && t < n) {
+                    if (t == s) Rv = isnan(sw_s) ? NAN : cs * sr_s;
+                    else Rv = isnan(f4[q]) ? x4[q] : x4[q] * f4[q];
+                }
+                if (KD_OUT) __builtin_nontemporal_store(Rv, rrow + j);
+            }
+        }
+    }
+    }  // sweep
+    if (row_min && i >= 0) {
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) lmin = fmin(lmin, __shfl_xor(lmin, d, 64));
+        if (lane == 0 && lmin < INFINITY) atomicMin(&sm->rmin, as_u(lmin));
+        __syncthreads();
+        if (tid == 0) row_min[i] = as_d(sm->rmin);
+    }
+}
+
 template <int B>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sssp_delta_kernel(DevDelta g, const int* __restrict__ src, int ns,
                                                        const int* __restrict__ tgt, int nt, long long ld,
@@ -406,6 +755,8 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
     uint2* rrec = reinterpret_cast<uint2*>(smem + L.rrec);
     uint16_t* qv = reinterpret_cast<uint16_t*>(smem + L.qv);
     int* qbeg = reinterpret_cast<int*>(smem + L.qbeg);
+    unsigned long long* tmask = reinterpret_cast<unsigned long long*>(smem + L.tmask);
+    unsigned* tpre = reinterpret_cast<unsigned*>(smem + L.tpre);
     const unsigned delta = (unsigned)g.delta;
     const int qcap = L.qcap;
     const unsigned wmask = g.packed ? 0xFFu : 0xFFFFu;
@@ -426,6 +777,38 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
     __syncthreads();
 #endif
     const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+
+    // the launch's target set, once per workgroup: a strictly increasing list (every
+    // caller here passes the sorted attached set) becomes a bitmask + word prefix in LDS,
+    // so the output loops find a target's position without a global load; any other list
+    // takes the general loops (tgt[j] loads)
+    for (int k = tid; k < nw; k += B) tmask[k] = 0ull;
+    if (tid == 0) sm->tsorted = 1;
+    __syncthreads();
+    for (int j = tid; j < nt; j += B) {
+        const int t = tgt[j];
+        const bool ok = t >= 0 && t < n && (j == 0 || tgt[j - 1] < t);
+        if (!ok) sm->tsorted = 0;  // (every writer stores 0)
+        else atomicOr(&tmask[t >> 6], 1ull << (t & 63));
+    }
+    __syncthreads();
+    if (wid == 0) {
+        int run = 0;
+        for (int k0 = 0; k0 < nw; k0 += 64) {
+            const int k = k0 + lane;
+            const int c = k < nw ? __popcll(tmask[k]) : 0;
+            const int incl = kd_wave_incl_sum(c);
+            if (k < nw) tpre[k] = (unsigned)(run + incl - c);
+            run += __builtin_amdgcn_readlane(incl, 63);
+        }
+    }
+    __syncthreads();
+    const bool tsorted = __builtin_amdgcn_readfirstlane(sm->tsorted) != 0;
+    // position of target vertex v (tsorted), -1 if v is not a target
+    auto tpos = [&](int v) __attribute__((always_inline)) {
+        const unsigned long long wd = tmask[v >> 6], bit = 1ull << (v & 63);
+        return (wd & bit) ? (int)tpre[v >> 6] + __popcll(wd & (bit - 1ull)) : -1;
+    };
 
     // sources: one each to start, then from a queue, so workgroups that drew cheap
     // sources take more and the launch ends within about one source of the mean
@@ -457,6 +840,8 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         };
         const double fs = g.vf[s];
         const double cs = isnan(fs) ? 1.0 : 1.0 * fs;
+        // the (s, s) entry's self-loop, loaded before this source's first store
+        const double sw_s = g.self_w[s], sr_s = g.self_r[s];
     kd_restart:
 #ifdef SHD_STAMPS
         unsigned long long kd_t = 0;
@@ -1157,282 +1542,13 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             }
         }
         KD_STAMP(2);
-        // helper rows (i < 0, multi-GPU plans) only seed others: no output, no phase C
-        double* lrow = lat_out && i >= 0 ? lat_out + (long long)i * ld : nullptr;
-        double* rrow = rel_out && i >= 0 ? rel_out + (long long)i * ld : nullptr;
-        double lmin = INFINITY;
-        for (int j = tid; j < (i >= 0 ? nt : 0); j += B) {
-            const int t = tgt[j];
-            double Lv;
-            if (t < 0 || t >= n) { raise_err(err, SHD_ROUTE_EINVAL); Lv = NAN; }
-            else if (t == s) {
-                const double sw = g.self_w[s];
-                if (isnan(sw)) { raise_err(err, SHD_ROUTE_ENOEDGE); Lv = NAN; }
-                else { Lv = 0.0 + sw; lmin = fmin(lmin, Lv); }
-            } else if (dist[t] == 0xFFFFu) { raise_err(err, SHD_ROUTE_EUNREACH); Lv = NAN; }
-            else { Lv = (double)dist[t]; lmin = fmin(lmin, Lv); }
-            if (lrow) __builtin_nontemporal_store(Lv, lrow + j);
-        }
-        wait_stores();  // wpr of phase B visible to the whole workgroup
-        if (tid == 0) { sm->deep = 0; sm->rmin = kInfBits; }
-        __syncthreads();
-
-        KD_ACC(18);
-        // dist is dead: its LDS becomes the parent array
-        uint16_t* parv = dist;
-        if (g.walk && rrow) {
-            // ---- C': reliability by walking each target's tree path in LDS -------------
-            // parv u16 + rix u8 (index of the parent arc's reliability) + rtab in LDS; each
-            // target walks <= KD_MAXD arcs to the source, then folds the product source-first
-            // (the order the level sweep multiplies in, so the bits agree)
-            // rtl[KD_ONE] = 1.0 is the source's own "arc" (a walk parked at the source keeps
-            // multiplying by an exact 1.0) and rtl[KD_NAN] marks unreachable vertices
-            uint8_t* rixl = reinterpret_cast<uint8_t*>(smem + L.rix);
-            double* rtl = reinterpret_cast<double*>(smem + L.rtabl);
-            for (int k = tid; k < 256; k += B)
-                rtl[k] = k < g.nrtab ? g.rtab[k] : k == KD_ONE ? 1.0 : NAN;
-            for (int v0 = tid; v0 < n; v0 += B * 8) {
-                uint32_t pr[8], dv8[8];
-#pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    pr[q] = wpr[min(v0 + q * B, n - 1)];
-                    dv8[q] = dist[min(v0 + q * B, n - 1)];
-                }
-                // (each thread overwrites only the dist entries it read itself)
-#pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const int v = v0 + q * B;
-                    if (v >= n) continue;
-                    const bool src_v = v == s, unr = !src_v && dv8[q] == 0xFFFFu;
-                    parv[v] = src_v || unr ? (uint16_t)s : (uint16_t)(pr[q] & 0xFFFFu);
-                    rixl[v] = src_v ? (uint8_t)KD_ONE : unr ? (uint8_t)KD_NAN
-                                                     : (uint8_t)min((pr[q] >> 16) & rmask, (uint32_t)(g.nrtab - 1));
-                }
-            }
-            __syncthreads();
-            KD_ACC(19);
-            for (int j0 = tid; j0 < nt; j0 += KD_WQ * B) {
-                // KD_WQ targets per thread: independent parent chains in flight.  A chain that
-                // reaches the source stays there (parv[s] = s, factor 1.0), so a step is two LDS
-                // reads and a byte insert, and the wave stops when every chain is parked.
-                int t2[KD_WQ], cur[KD_WQ];
-                uint32_t pk[KD_WQ][KD_MAXD / 4];
-#pragma unroll
-                for (int q = 0; q < KD_WQ; q++) {
-                    const int j = j0 + q * B;
-                    t2[q] = j < nt ? tgt[j] : -1;
-                    cur[q] = t2[q] >= 0 && t2[q] < n ? t2[q] : s;
-#pragma unroll
-                    for (int k = 0; k < KD_MAXD / 4; k++) pk[q][k] = 0u;
-                }
-                // blocks of 4 arcs (parked chains multiply an exact 1.0, so the padding is
-                // harmless): one packed word per chain and block keeps the loop off the VALU
-                int nb = 0;  // blocks walked, wave-uniform
-#pragma unroll 1
-                for (; nb < KD_MAXD / 4; nb++) {
-                    bool any = false;
-#pragma unroll
-                    for (int q = 0; q < KD_WQ; q++) any = any || cur[q] != s;
-                    if (!__any(any)) break;
-                    uint32_t acc[KD_WQ];
-#pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        uint32_t p[KD_WQ], rx[KD_WQ];
-#pragma unroll
-                        for (int q = 0; q < KD_WQ; q++) { p[q] = parv[cur[q]]; rx[q] = rixl[cur[q]]; }
-#pragma unroll
-                        for (int q = 0; q < KD_WQ; q++) {
-                            acc[q] = e == 0 ? rx[q] : (acc[q] | (rx[q] << (8 * e)));
-                            cur[q] = (int)p[q];
-                        }
-                    }
-#pragma unroll
-                    for (int q = 0; q < KD_WQ; q++) pk[q][nb] = acc[q];
-                }
-                {
-                    bool any = false;
-#pragma unroll
-                    for (int q = 0; q < KD_WQ; q++) any = any || cur[q] != s;
-                    if (any) sm->deep = 1;  // the level sweep below redoes the row
-                }
-                double rr[KD_WQ];
-#pragma unroll
-                for (int q = 0; q < KD_WQ; q++) rr[q] = cs;
-#pragma unroll 1
-                for (int k4 = nb - 1; k4 >= 0; k4--) {  // source-first: the last arc walked first
-                    uint32_t wq[KD_WQ];
-#pragma unroll
-                    for (int q = 0; q < KD_WQ; q++) wq[q] = pk[q][k4];
-#pragma unroll
-                    for (int e = 3; e >= 0; e--) {
-                        double x[KD_WQ];
-#pragma unroll
-                        for (int q = 0; q < KD_WQ; q++) x[q] = rtl[(wq[q] >> (8 * e)) & 0xFFu];
-#pragma unroll
-                        for (int q = 0; q < KD_WQ; q++) rr[q] *= x[q];
-                    }
-                }
-                double f2[KD_WQ];
-#pragma unroll
-                for (int q = 0; q < KD_WQ; q++) f2[q] = g.vf[(t2[q] >= 0 && t2[q] < n) ? t2[q] : s];
-#pragma unroll
-                for (int q = 0; q < KD_WQ; q++) {
-                    const int j = j0 + q * B;
-                    if (j >= nt) continue;
-                    const int t = t2[q];
-                    double Rv = NAN;
-                    if (t >= 0 && t < n) {
-                        if (t == s) Rv = isnan(g.self_w[s]) ? NAN : cs * g.self_r[s];
-                        else Rv = isnan(f2[q]) ? rr[q] : rr[q] * f2[q];
-                    }
-                    __builtin_nontemporal_store(Rv, rrow + j);
-                }
-            }
-            __syncthreads();
-            KD_ACC(13);
-            KD_STAMP(3);
-        }
-        const bool sweep = i >= 0 && (!(g.walk && rrow) || sm->deep);
-        if (sweep) {
-        // parent records: parent | ridx << 16 (writer wave and phase B), KD_SRC_MARK at s
-        for (int v0 = tid; v0 < n; v0 += B * 8) {
-            uint32_t pr[8];
-#pragma unroll
-            for (int q = 0; q < 8; q++) pr[q] = wpr[min(v0 + q * B, n - 1)];
-            double rr[8];
-#pragma unroll
-            for (int q = 0; q < 8; q++) rr[q] = g.rtab[min((int)((pr[q] >> 16) & rmask), g.nrtab - 1)];
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const int v = v0 + q * B;
-                if (v >= n) continue;
-                const bool src_v = pr[q] == KD_SRC_MARK;
-                parv[v] = src_v ? (uint16_t)v : (uint16_t)(pr[q] & 0xFFFFu);
-                relv[v] = src_v ? cs : -rr[q];
-            }
-        }
-        for (int k = tid; k < nw; k += B) {
-            unsigned long long mk = (k == nw - 1 && (n & 63)) ? ((1ull << (n & 63)) - 1ull) : ~0ull;
-            if (k == (s >> 6)) mk &= ~(1ull << (s & 63));
-            pend[k] = mk;
-            fix[k] = 0ull;
-        }
-        wait_stores();
-        __syncthreads();
-        KD_ACC(19);
-
-        if (tid == 0) sm->qtail[0] = sm->qtail[1] = 0;
-        lds_barrier();
-        // ---- C: reliability down the tree ------------------------------------------
-        // per level: pending vertices whose parent is done are compacted into qv, then one
-        // thread per listed vertex loads relv[parent] and its own -r and stores the product
-        for (int c = 0;; c ^= 1) {
-            KD_COUNT(12, tid == 0 ? 1 : 0);
-            if (tid == 0) sm->qtail[c ^ 1] = 0;
-            for (int k0 = 0; k0 < nw; k0 += B) {
-                const int k = k0 + tid;
-                unsigned long long b = k < nw ? pend[k] : 0ull, ready = 0ull;
-                while (b) {  // ready = pending vertices whose parent is done (LDS only)
-                    int v4[4];
-                    pop4(&b, k, v4);
-                    int p4[4];
-#pragma unroll
-                    for (int q = 0; q < 4; q++) p4[q] = (int)parv[v4[q] >= 0 ? v4[q] : 0];
-                    unsigned long long pw[4];
-#pragma unroll
-                    for (int q = 0; q < 4; q++) pw[q] = pend[p4[q] >> 6];
-#pragma unroll
-                    for (int q = 0; q < 4; q++)
-                        if (v4[q] >= 0 && !((pw[q] >> (p4[q] & 63)) & 1ull)) ready |= 1ull << (v4[q] & 63);
-                }
-                const int cnt = __popcll(ready);
-                int incl = kd_wave_incl_sum(cnt);
-                int base = 0;
-                if (lane == 63 && incl) base = atomicAdd(&sm->qtail[c], incl);
-                base = __builtin_amdgcn_readlane(base, 63);
-                int pos = base + incl - cnt;
-                unsigned long long listed = 0ull;
-                b = ready;
-                while (b && pos < qcap) {
-                    const int bi = __ffsll((long long)b) - 1;
-                    b &= b - 1;
-                    qv[pos++] = (uint16_t)((k << 6) + bi);
-                    listed |= 1ull << bi;
-                }
-                if (k < nw) fix[k] = listed;
-            }
-            lds_barrier();
-            KD_ACC(13);
-            const int cnt = min(sm->qtail[c], qcap);
-            if (cnt == 0) break;
-            for (int j0 = 0; j0 < cnt; j0 += B * 4) {
-                int v4[4], p4[4];
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int j = j0 + q * B + tid;
-                    v4[q] = j < cnt ? (int)qv[j] : -1;
-                    p4[q] = (int)parv[v4[q] >= 0 ? v4[q] : 0];
-                }
-                double xp[4], xv[4];
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    xp[q] = relv[p4[q]];
-                    xv[q] = relv[v4[q] >= 0 ? v4[q] : 0];
-                }
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    if (v4[q] >= 0) relv[v4[q]] = xp[q] * (-xv[q]);
-            }
-            wait_stores();  // this level's relv visible before its vertices count as done
-            KD_ACC(14);
-            lds_barrier();
-            for (int k = tid; k < nw; k += B) {
-                const unsigned long long r = fix[k];
-                if (r) pend[k] &= ~r;
-            }
-            lds_barrier();
-            KD_ACC(15);
-        }
-        KD_STAMP(3);
-
-        // ---- D: rel row out + row min ----------------------------------------------
-        if (rrow) {
-            for (int j0 = tid; j0 < nt; j0 += B * 4) {
-                int t4[4];
-                double x4[4], f4[4];
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int j = j0 + q * B;
-                    t4[q] = j < nt ? tgt[j] : s;
-                }
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int t = (t4[q] >= 0 && t4[q] < n) ? t4[q] : s;
-                    x4[q] = relv[t];
-                    f4[q] = g.vf[t];
-                }
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int j = j0 + q * B;
-                    if (j >= nt) continue;
-                    const int t = t4[q];
-                    double Rv = NAN;
-                    if (t >= 0 && t < n) {
-                        if (t == s) Rv = isnan(g.self_w[s]) ? NAN : cs * g.self_r[s];
-                        else Rv = isnan(f4[q]) ? x4[q] : x4[q] * f4[q];
-                    }
-                    __builtin_nontemporal_store(Rv, rrow + j);
-                }
-            }
-        }
-        }  // sweep
-        if (row_min && i >= 0) {
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) lmin = fmin(lmin, __shfl_xor(lmin, d, 64));
-            if (lane == 0 && lmin < INFINITY) atomicMin(&sm->rmin, as_u(lmin));
-            __syncthreads();
-            if (tid == 0) row_min[i] = as_d(sm->rmin);
-        }
+        // output phases in their own function: its registers are allocated for these loops
+        // alone (inlined, phase A's pressure spilled the values they use to scratch, and
+        // every reload waited behind the row's output stores: one in-order vmcnt)
+        kd_output<B>(n, nw, nt, ld, i, s, cs, sw_s, sr_s, tsorted ? 1 : 0, rmask, g.rc, (const KD_GLOBAL int*)tgt,
+                     (KD_GLOBAL double*)lat_out, (KD_GLOBAL double*)rel_out, (KD_GLOBAL double*)row_min, err,
+                     (const KD_GLOBAL uint32_t*)wpr, (KD_GLOBAL double*)relv, g.walk, (const KD_GLOBAL double*)g.rtab,
+                     g.nrtab, (const KD_GLOBAL double*)g.vf, g.has_vf, KD_DFLAGS);
         lds_barrier();
         KD_STAMP(4);
         KD_FLUSH();

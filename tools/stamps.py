@@ -39,11 +39,16 @@ L.shd_route_debug_buffer(eng._h, C.c_void_p(dbg.data_ptr()))
 plan = eng.plan(S) if a.plan else None
 for rep in range(3):
     dbg.zero_()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     if plan is not None:
         plan.rows_async(d_tgt, lat, rel, mn)
     else:
         eng.rows_async(d_src, d_tgt, lat, rel, mn)
+    e1.record()
     eng.sync()
+    torch.cuda.synchronize()
+print(f"launch time (diag build, last rep): {e0.elapsed_time(e1):.3f} ms")
 if plan is not None:
     print("plan", plan.info)
 d_all = dbg.cpu().numpy().astype(np.int64).reshape(-1, 32 if eng.info["kernel"] == 4 else 8)

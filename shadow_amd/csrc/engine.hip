@@ -72,6 +72,7 @@ struct shd_route {
     double* d_kd_rtab = nullptr;    // distinct reliabilities
     int kd_nlight = 0, kd_nrtab = 1, kd_walk = 0, kd_packed = 0, kd_fused = 0;
     int has_vf = 0;  // some vertex has a packet-loss factor (else f_v is absent everywhere)
+    int kd_rone = -1;  // rtab index of exactly 1.0 (-1: none)
     char* d_kd_ws = nullptr;
     int* d_kd_next = nullptr;  // KD source queue counter
     // host copies for seeded planning (shd_route_plan_*): out-CSR, rtab index per arc and
@@ -432,6 +433,8 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 if (rc) return rc;
                 c->kd_nlight = lrow[n];
                 c->kd_nrtab = std::max<int>(1, (int)rtab.size());
+                for (int q = 0; q < (int)rtab.size(); q++)
+                    if (rtab[q] == 1.0) c->kd_rone = q;
                 // 16 waves per CU: 4 per SIMD at <= 128 VGPRs (amdgpu_waves_per_eu(4))
                 const int per_cu = std::max(1, std::min((int)(kLdsBudget / lds), 1024 / blk));
                 c->kd_slots = 256 * per_cu;
@@ -569,7 +572,7 @@ DevDelta kd_args(const shd_route* c) {
     k.fused = c->kd_fused; k.rc = c->kd_qcap;
     k.row = c->d_row; k.orec = c->d_kd_orec; k.oridx = c->d_kd_oridx;
     k.nnz = c->nnz; k.lrow = c->d_kd_lstart; k.lrec = reinterpret_cast<const uint2*>(c->d_kd_lrec); k.nlight = c->kd_nlight;
-    k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab; k.walk = c->kd_walk; k.packed = c->kd_packed;
+    k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab; k.rone = c->kd_rone; k.walk = c->kd_walk; k.packed = c->kd_packed;
     k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg; k.has_vf = c->has_vf; k.dflags = 0;
 #ifdef SHD_STAMPS
     if (const char* e = getenv("SHD_ROUTE_DFLAGS")) k.dflags = atoi(e);

@@ -97,6 +97,7 @@ struct KDJob {
 static_assert(sizeof(KDJob) == 64, "one 64-byte job record");
 constexpr uint32_t KD_EVTAG = 0xFFFF0000u;  // ring record y of a tie event: v | KD_EVTAG
 typedef unsigned short kd_us2 __attribute__((ext_vector_type(2)));
+typedef double kd_d2 __attribute__((ext_vector_type(2)));
 
 struct DevDelta {
     int* next;                          // source queue counter (zeroed before each launch)
@@ -122,6 +123,7 @@ struct DevDelta {
                                         // (directed graphs: every in-arc)
     const double* __restrict__ rtab;    // distinct 1 - loss values, indexed by ridx
     int nrtab;
+    int rone;                           // index of exactly 1.0 in rtab (-1: none)
     int walk;                           // phase C by path walks in LDS (nrtab <= 256, fits)
     int packed;                         // orec = v | w << 16 | ridx << 24 (w < 256, nrtab <= 256)
     const double* __restrict__ vf;
@@ -409,7 +411,7 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                                                     KD_GLOBAL double* __restrict__ rel_out, KD_GLOBAL double* __restrict__ row_min,
                                                     int* __restrict__ err, const KD_GLOBAL uint32_t* __restrict__ wpr,
                                                     KD_GLOBAL double* __restrict__ relv, const int walk,
-                                                    const KD_GLOBAL double* __restrict__ rtab, const int nrtab,
+                                                    const KD_GLOBAL double* __restrict__ rtab, const int nrtab, const int rone,
                                                     const KD_GLOBAL double* __restrict__ vf, const int has_vf, const int dflags) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int RR = kd_rr<B>();
@@ -447,11 +449,18 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
         return Lv;
     };
     if (tsorted) {
-        for (int v = tid; v < (i >= 0 ? n : 0); v += B) {
-            const int j = tpos(v);
-            if (j < 0) continue;
-            const double Lv = lat_of(v);
-            if (lrow && KD_OUT) __builtin_nontemporal_store(Lv, lrow + j);
+        // two adjacent vertices per lane: consecutive positions go out as one 16-B store
+        const int lpar = (int)(((uintptr_t)lrow >> 3) & 1);
+        for (int v = 2 * tid; v < (i >= 0 ? n : 0); v += 2 * B) {
+            const int j0 = tpos(v), j1 = v + 1 < n ? tpos(v + 1) : -1;
+            const double L0 = j0 >= 0 ? lat_of(v) : 0.0, L1 = j1 >= 0 ? lat_of(v + 1) : 0.0;
+            if (!lrow || !KD_OUT) continue;
+            if (j0 >= 0 && j1 == j0 + 1 && !((j0 + lpar) & 1))
+                __builtin_nontemporal_store(kd_d2{L0, L1}, reinterpret_cast<KD_GLOBAL kd_d2*>(lrow + j0));
+            else {
+                if (j0 >= 0) __builtin_nontemporal_store(L0, lrow + j0);
+                if (j1 >= 0) __builtin_nontemporal_store(L1, lrow + j1);
+            }
         }
     } else {
         for (int j = tid; j < (i >= 0 ? nt : 0); j += B) {
@@ -491,8 +500,9 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                 if (v >= n) continue;
                 const bool src_v = v == s, unr = !src_v && dv8[q] == 0xFFFFu;
                 parv[v] = src_v || unr ? (uint16_t)s : (uint16_t)(pr[q] & 0xFFFFu);
-                rixl[v] = src_v ? (uint8_t)KD_ONE : unr ? (uint8_t)KD_NAN
-                                                 : (uint8_t)min((pr[q] >> 16) & rmask, (uint32_t)(g.nrtab - 1));
+                // an arc of reliability exactly 1.0 folds as the KD_ONE slot (same factor)
+                const uint32_t ri = min((pr[q] >> 16) & rmask, (uint32_t)(g.nrtab - 1));
+                rixl[v] = src_v ? (uint8_t)KD_ONE : unr ? (uint8_t)KD_NAN : ri == (uint32_t)rone ? (uint8_t)KD_ONE : (uint8_t)ri;
             }
         }
         __syncthreads();
@@ -500,6 +510,7 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
         // sorted targets: one pass over the vertices, positions from the LDS mask (no
         // global load behind the previous group's stores); else over the target list
         const int lim = tsorted ? n : nt;
+        const int rpar = (int)(((uintptr_t)rrow >> 3) & 1);
         for (int j0 = tid; j0 < lim; j0 += KD_WQ * B) {
             // KD_WQ targets per thread: independent parent chains in flight.  A chain that
             // reaches the source stays there (parv[s] = s, factor 1.0), so a step is two LDS
@@ -510,8 +521,10 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
             for (int q = 0; q < KD_WQ; q++) {
                 const int j = j0 + q * B;
                 if (tsorted) {
-                    jq[q] = j < n ? tpos(j) : -1;
-                    t2[q] = jq[q] >= 0 ? j : -1;
+                    // chains (0, 1) and (2, 3) are adjacent vertices: paired 16-B stores
+                    const int v = (j0 - tid) + (q >> 1) * 2 * B + 2 * tid + (q & 1);
+                    jq[q] = v < n ? tpos(v) : -1;
+                    t2[q] = jq[q] >= 0 ? v : -1;
                 } else {
                     jq[q] = j < nt ? j : -1;
                     t2[q] = j < nt ? tgt[j] : -1;
@@ -562,6 +575,8 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                 for (int q = 0; q < KD_WQ; q++) wq[q] = pk[q][k4];
 #pragma unroll
                 for (int e = 3; e >= 0; e--) {
+                    // (arcs of reliability exactly 1.0 read the KD_ONE slot, as parked chains
+                    // do: one shared address, a broadcast)
                     double x[KD_WQ];
 #pragma unroll
                     for (int q = 0; q < KD_WQ; q++) x[q] = rtl[(wq[q] >> (8 * e)) & 0xFFu];
@@ -572,17 +587,27 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
             double f2[KD_WQ];
 #pragma unroll
             for (int q = 0; q < KD_WQ; q++) f2[q] = g.has_vf ? g.vf[(t2[q] >= 0 && t2[q] < n) ? t2[q] : s] : (double)NAN;
+            double Rv[KD_WQ];
 #pragma unroll
             for (int q = 0; q < KD_WQ; q++) {
-                const int j = jq[q];
-                if (j < 0) continue;
                 const int t = t2[q];
-                double Rv = NAN;
+                Rv[q] = NAN;
                 if (t >= 0 && t < n) {
-                    if (t == s) Rv = isnan(sw_s) ? NAN : cs * sr_s;
-                    else Rv = isnan(f2[q]) ? rr[q] : rr[q] * f2[q];
+                    if (t == s) Rv[q] = isnan(sw_s) ? NAN : cs * sr_s;
+                    else Rv[q] = isnan(f2[q]) ? rr[q] : rr[q] * f2[q];
                 }
-                if (KD_OUT) __builtin_nontemporal_store(Rv, rrow + j);
+            }
+            if (KD_OUT) {
+#pragma unroll
+                for (int q = 0; q < KD_WQ; q += 2) {
+                    const int ja = jq[q], jb = jq[q + 1];
+                    if (tsorted && ja >= 0 && jb == ja + 1 && !((ja + rpar) & 1))
+                        __builtin_nontemporal_store(kd_d2{Rv[q], Rv[q + 1]}, reinterpret_cast<KD_GLOBAL kd_d2*>(rrow + ja));
+                    else {
+                        if (ja >= 0) __builtin_nontemporal_store(Rv[q], rrow + ja);
+                        if (jb >= 0) __builtin_nontemporal_store(Rv[q + 1], rrow + jb);
+                    }
+                }
             }
         }
         __syncthreads();
@@ -1548,7 +1573,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         kd_output<B>(n, nw, nt, ld, i, s, cs, sw_s, sr_s, tsorted ? 1 : 0, rmask, g.rc, (const KD_GLOBAL int*)tgt,
                      (KD_GLOBAL double*)lat_out, (KD_GLOBAL double*)rel_out, (KD_GLOBAL double*)row_min, err,
                      (const KD_GLOBAL uint32_t*)wpr, (KD_GLOBAL double*)relv, g.walk, (const KD_GLOBAL double*)g.rtab,
-                     g.nrtab, (const KD_GLOBAL double*)g.vf, g.has_vf, KD_DFLAGS);
+                     g.nrtab, g.rone, (const KD_GLOBAL double*)g.vf, g.has_vf, KD_DFLAGS);
         lds_barrier();
         KD_STAMP(4);
         KD_FLUSH();

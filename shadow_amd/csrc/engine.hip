@@ -84,7 +84,8 @@ struct shd_route {
     int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD
     // K4 (fw.hpp): u16 all-pairs table + dense u16 weights, Np x Np (Np = n rounded to 64)
     uint16_t* d_fwD = nullptr;
-    uint16_t* d_fwW = nullptr;
+    uint32_t* d_fwinl = nullptr;  // K4 parent search: sorted in-arc keys per vertex (np x np)
+    uint16_t* d_fwpos = nullptr;  // and the start index per small threshold (n x FW_X)
     uint32_t* d_fwkey = nullptr;
     size_t fwkey_cap = 0;
     int fw_np = 0, fw_ready = 0;
@@ -1419,18 +1420,6 @@ int planned_host_rows(shd_route* c, const int32_t* src, int32_t ns, const int32_
 namespace {
 constexpr int kFwMaxN = 12000;  // fw_rows keeps rel f64 + order i32 per vertex in LDS
 
-__global__ void fw_w16_kernel(const double* __restrict__ W, int n, int np, uint16_t* __restrict__ Wd) {
-    const long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (k >= (long long)np * np) return;
-    const int i = (int)(k / np), j = (int)(k % np);
-    uint16_t d = 0xFFFFu;  // self-loops never lie on a shortest path (w > 0)
-    if (i != j && i < n && j < n) {
-        const double w = W[(long long)i * n + j];
-        if (!isnan(w)) d = (uint16_t)w;
-    }
-    Wd[k] = d;
-}
-
 int fw_prepare(shd_route* c) {
     if (c->d_fwD) return SHD_ROUTE_OK;
     if (!c->integer_w || c->multigraph || c->n > kFwMaxN || c->k32_bound <= 0 || c->k32_bound >= 0xFFFF)
@@ -1441,15 +1430,25 @@ int fw_prepare(shd_route* c) {
     const size_t cells = (size_t)np * np;
     if (hipMalloc((void**)&c->d_fwD, 2 * cells) != hipSuccess) return SHD_ROUTE_ENOMEM;
     c->allocs.push_back(c->d_fwD);
-    if (hipMalloc((void**)&c->d_fwW, 2 * cells) != hipSuccess) return SHD_ROUTE_ENOMEM;
-    c->allocs.push_back(c->d_fwW);
+    if (hipMalloc((void**)&c->d_fwinl, 4 * cells) != hipSuccess) return SHD_ROUTE_ENOMEM;
+    c->allocs.push_back(c->d_fwinl);
+    if (hipMalloc((void**)&c->d_fwpos, sizeof(uint16_t) * FW_X * (size_t)c->n) != hipSuccess) return SHD_ROUTE_ENOMEM;
+    c->allocs.push_back(c->d_fwpos);
     c->fw_np = np;
     const size_t lds = a16(sizeof(double) * c->n) + a16(sizeof(int) * c->n) + a16(sizeof(int) * (c->k32_bound + 2));
     if (lds > kLdsBudget) return SHD_ROUTE_EUNSUPPORTED;
     rc = hip_check(hipFuncSetAttribute((const void*)fw_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (rc) return rc;
-    const unsigned blocks = (unsigned)((cells + 255) / 256);
-    hipLaunchKernelGGL(fw_w16_kernel, dim3(blocks), dim3(256), 0, nullptr, c->d_W, c->n, np, c->d_fwW);
+    int sp = 1;
+    while (sp < np) sp <<= 1;
+    rc = hip_check(hipFuncSetAttribute((const void*)fw_inlist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)(4 * sp)));
+    if (rc) return rc;
+    rc = hip_check(hipFuncSetAttribute((const void*)fw_parent_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)(2 * np)));
+    if (rc) return rc;
+    hipLaunchKernelGGL(fw_inlist_kernel, dim3(c->n), dim3(1024), 4 * sp, nullptr, c->d_W, c->n, np, sp, c->d_fwinl,
+                       c->d_fwpos);
     return hip_check(hipGetLastError());
 }
 }  // namespace
@@ -1492,8 +1491,8 @@ int shd_route_fw_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, co
         if (hipMalloc((void**)&c->d_fwkey, need * sizeof(uint32_t)) != hipSuccess) return SHD_ROUTE_ENOMEM;
         c->fwkey_cap = need;
     }
-    hipLaunchKernelGGL(fw_parent_kernel, dim3(np / FW_T, (ns + FW_T - 1) / FW_T), dim3(256), 0, st, c->d_fwD,
-                       c->d_fwW, np, d_src, ns, c->d_fwkey);
+    hipLaunchKernelGGL(fw_parent_kernel, dim3(std::min(ns, 4096)), dim3(1024), 2 * np, st, c->d_fwD, c->d_fwinl,
+                       c->d_fwpos, c->n, np, d_src, ns, c->d_fwkey);
     FWRowsArgs a;
     a.n = c->n; a.np = np; a.bound = c->k32_bound; a.D = c->d_fwD; a.key = c->d_fwkey; a.R = c->d_R;
     a.vf = c->d_vf; a.self_w = c->d_self_w; a.self_r = c->d_self_r;

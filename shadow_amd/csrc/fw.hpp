@@ -22,9 +22,11 @@
 //  The tropical product of two 64x64 u16 tiles: 256 threads, 4 rows x 4 columns each,
 //  A stored transposed in LDS so a thread's 4 rows at step k are one 8-byte read.
 //
+//  fw_inlist   once per graph: every vertex's in-arcs sorted by the tie-rule key
+//              (0xFFFF - w) << 16 | u, with a start index per small threshold
 //  fw_parent   per (source s, vertex v): the tie-rule parent among the tight in-arcs
-//              (D[s][u] + w(u,v) == D[s][v]): largest w, then smallest u -- the key
-//              (0xFFFF - w) << 16 | u, minimised over u in 64-wide LDS chunks
+//              (D[s][u] + w(u,v) == D[s][v]): largest w, then smallest u -- the first
+//              tight arc of v's sorted in-list, scanned from the first arc with w <= D[s][v]
 //  fw_rows     per source: reliability top-down in distance order (parents have smaller
 //              distance: w >= 1), rel[v] = rel[p] * r(p,v), f_t last; lat / rel rows out
 #include "common.hpp"
@@ -53,7 +55,7 @@ __global__ void fw_init_kernel(const double* __restrict__ W, int n, int np, uint
     if (i == j) d = 0;
     else if (i < n && j < n) {
         const double w = W[(long long)i * n + j];
-        if (!isnan(w)) d = (uint16_t)w;
+        if (!isnan(w)) d = w < 65535.0 ? (uint16_t)w : (uint16_t)0xFFFFu;  // >= the bound: never on a path
     }
     D[k] = d;
 }
@@ -175,62 +177,94 @@ __global__ __launch_bounds__(256) void fw_rest_kernel(uint16_t* __restrict__ D, 
     fw_store_block(D, np, ti, tj, r, c, acc);
 }
 
-// parents: key[s][v] = min over u != v with D[s][u] + w(u,v) == D[s][v] of
-// (0xFFFF - w) << 16 | u (largest w, then smallest u: the engine tie rule).  Tiles of 64
-// sources x 64 targets; u in 64-wide chunks through LDS (D[s][u] transposed, w(u,v)).
-// Wd is the dense weight matrix as u16 (0xFFFF = no edge), Np x Np.
-__global__ __launch_bounds__(256) void fw_parent_kernel(const uint16_t* __restrict__ D, const uint16_t* __restrict__ Wd,
-                                                        int np, const int* __restrict__ src, int ns,
-                                                        uint32_t* __restrict__ key) {
-    __shared__ __attribute__((aligned(16))) uint16_t At[FW_T * FW_T];  // [u][s]
-    __shared__ __attribute__((aligned(16))) uint16_t Bt[FW_T * FW_T];  // [u][v]
-    const int r = threadIdx.x / 16, c = threadIdx.x % 16;
-    const int s0 = blockIdx.y * FW_T, v0 = blockIdx.x * FW_T;
-    // target distances of the thread's 4 sources x 4 targets
-    unsigned tgt[4][4], best[4][4];
-    int srow[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int si = s0 + 4 * r + i;
-        srow[i] = si < ns ? src[si] : 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            tgt[i][j] = D[(long long)srow[i] * np + v0 + 4 * c + j];
-            best[i][j] = 0xFFFFFFFFu;
+// In-arc lists for the parent search, built once per graph: row v holds the keys
+// (0xFFFF - w) << 16 | u of every in-arc u -> v (u != v, w < 0xFFFF) in increasing order,
+// i.e. the engine tie rule's preference order (largest w, then smallest u), then FW_END
+// padding; pos[v][x] (x < FW_X) is the first index whose arc has w <= x.  One workgroup
+// per vertex: the column of the dense W, a bitonic sort of sp (power of two >= np) keys
+// in LDS, and a lower bound per threshold.
+constexpr int FW_X = 256;
+constexpr uint32_t FW_END = 0xFFFFFFFFu;
+__global__ __launch_bounds__(1024) void fw_inlist_kernel(const double* __restrict__ W, int n, int np, int sp,
+                                                         uint32_t* __restrict__ inl, uint16_t* __restrict__ pos) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t fkeys[];
+    const int v = blockIdx.x, tid = threadIdx.x, B = blockDim.x;
+    for (int k = tid; k < sp; k += B) {
+        uint32_t key = FW_END;
+        if (k < n && k != v) {
+            const double w = W[(long long)k * n + v];
+            if (!isnan(w) && w < 65535.0) key = ((0xFFFFu - (uint32_t)w) << 16) | (uint32_t)k;
         }
+        fkeys[k] = key;
     }
-    for (int u0 = 0; u0 < np; u0 += FW_T) {
-        __syncthreads();
-        for (int q = threadIdx.x; q < FW_T * FW_T; q += 256) {
-            const int si = q / FW_T, uu = q % FW_T;  // At[u][s] = D[src[s0+si]][u0+uu]
-            const int sv = s0 + si < ns ? src[s0 + si] : 0;
-            At[uu * FW_T + si] = D[(long long)sv * np + u0 + uu];
-            const int ub = q / FW_T, vb = q % FW_T;  // Bt[u][v] = W[u0+ub][v0+vb]
-            Bt[ub * FW_T + vb] = Wd[(long long)(u0 + ub) * np + v0 + vb];
-        }
-        __syncthreads();
-#pragma unroll 4
-        for (int k = 0; k < FW_T; k++) {
-            const uint2 a = *reinterpret_cast<const uint2*>(At + k * FW_T + 4 * r);
-            const uint2 b = *reinterpret_cast<const uint2*>(Bt + k * FW_T + 4 * c);
-            const unsigned ds[4] = {a.x & 0xFFFFu, a.x >> 16, a.y & 0xFFFFu, a.y >> 16};
-            const unsigned wv[4] = {b.x & 0xFFFFu, b.x >> 16, b.y & 0xFFFFu, b.y >> 16};
-            const unsigned u = (unsigned)(u0 + k);
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const unsigned kk = ((0xFFFFu - wv[j]) << 16) | u;
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    if (wv[j] != 0xFFFFu && ds[i] + wv[j] == tgt[i][j]) best[i][j] = min(best[i][j], kk);
+    __syncthreads();
+    for (int size = 2; size <= sp; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = tid; t < sp / 2; t += B) {
+                const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const uint32_t a = fkeys[lo], b = fkeys[hi];
+                if ((a > b) == up) { fkeys[lo] = b; fkeys[hi] = a; }
             }
+            __syncthreads();
         }
     }
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int si = s0 + 4 * r + i;
-        if (si >= ns) continue;
-#pragma unroll
-        for (int j = 0; j < 4; j++) key[(long long)si * np + v0 + 4 * c + j] = best[i][j];
+    for (int k = tid; k < np; k += B) inl[(long long)v * np + k] = fkeys[k];
+    for (int x = tid; x < FW_X; x += B) {
+        const uint32_t thr = (0xFFFFu - (uint32_t)x) << 16;  // w <= x  <=>  key >= thr
+        int lo = 0, hi = sp;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (fkeys[mid] < thr) lo = mid + 1; else hi = mid;
+        }
+        pos[(long long)v * FW_X + x] = (uint16_t)lo;
+    }
+}
+
+// parents: key[s][v] = min over u != v with D[s][u] + w(u,v) == D[s][v] of
+// (0xFFFF - w) << 16 | u (largest w, then smallest u: the engine tie rule), FW_END for the
+// source and unreachable vertices.  One workgroup per source with D[s][.] in LDS; a
+// thread per target scans v's in-arc list in key order from the first arc with
+// w <= D[s][v] (pos table, or a binary search past FW_X) and stops at the first tight
+// arc, which is the minimum key.  A scan visits only the arcs with w in (w*, D[s][v]].
+__global__ __launch_bounds__(1024) void fw_parent_kernel(const uint16_t* __restrict__ D, const uint32_t* __restrict__ inl,
+                                                         const uint16_t* __restrict__ pos, int n, int np,
+                                                         const int* __restrict__ src, int ns,
+                                                         uint32_t* __restrict__ key) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t drow[];
+    for (int i = blockIdx.x; i < ns; i += gridDim.x) {
+        const int s = src[i];
+        if (s < 0 || s >= n) continue;  // fw_rows raises the error for this row
+        __syncthreads();
+        const uint16_t* Ds = D + (long long)s * np;
+        for (int q = threadIdx.x; q < np / 8; q += blockDim.x)
+            reinterpret_cast<uint4*>(drow)[q] = reinterpret_cast<const uint4*>(Ds)[q];
+        __syncthreads();
+        for (int v = threadIdx.x; v < n; v += blockDim.x) {
+            const unsigned d = drow[v];
+            uint32_t best = FW_END;
+            if (v != s && d != 0xFFFFu) {
+                const uint32_t* lv = inl + (long long)v * np;
+                int k;
+                if (d < (unsigned)FW_X) {
+                    k = pos[(long long)v * FW_X + d];
+                } else {
+                    const uint32_t thr = (0xFFFFu - d) << 16;
+                    int lo = 0, hi = pos[(long long)v * FW_X + FW_X - 1];
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (lv[mid] < thr) lo = mid + 1; else hi = mid;
+                    }
+                    k = lo;
+                }
+                for (; k < np; k++) {
+                    const uint32_t e = lv[k];
+                    if (e == FW_END) break;
+                    if (drow[e & 0xFFFFu] + (0xFFFFu - (e >> 16)) == d) { best = e; break; }
+                }
+            }
+            key[(long long)i * np + v] = best;
+        }
     }
 }
 

@@ -44,6 +44,28 @@ def test_fw_rows_bitexact(oracle_mod, name):
     assert np.array_equal(mn, olat.min(axis=1))
 
 
+@pytest.mark.parametrize("name", ["directed", "wide"])
+def test_fw_rows_parent_search(oracle_mod, name):
+    """The parent search's two start rules: the threshold table (w <= 255) and the binary
+    search (distances past 255: weights up to 4000), and directed in-lists."""
+    from shadow_amd import route
+    from tests.golden import make_golden as mg
+    if name == "directed":
+        g = mg._directed(250, 21)
+    else:
+        g = complete_graph(180, seed=9)
+        g.latency = np.where(g.src != g.dst, g.latency * 16 + 100, g.latency)
+    eng = route.RouteEngine(g)
+    T = np.arange(g.n, dtype=np.int32)
+    S = T[::2]
+    lat, rel, mn = _fw_rows(eng, S, T)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(S, T, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(rel, orel)
+    if name == "wide":
+        assert np.nanmax(olat) > 300 and np.nanmin(olat[olat > 20]) < 255  # both start rules
+
+
 def test_fw_table_vs_oracle_floyd_warshall(oracle_mod):
     """The K4 table (every pair, self distance 0) against the oracle's plain FW, and the
     f64 in-place shd_route_fw_async against the same."""

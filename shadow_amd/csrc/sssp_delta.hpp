@@ -84,6 +84,9 @@ constexpr uint32_t KD_SRC_MARK = 0xFFFFFFFEu;  // parent record of the source it
 #define KD_GLOBAL __attribute__((address_space(1)))
 
 constexpr int KD_SEEDS = 2;
+#ifndef KD_JUMPS
+#define KD_JUMPS 1  // phase C pointer-jumping rounds before the walks (C4: 0: 50.5 ms, 1: 48.6, 2: 49.3, 3: 51.5, to convergence: 54.2)
+#endif
 struct KDJob {
     int row;               // output row
     int s;                 // source vertex
@@ -172,6 +175,7 @@ struct KDSmall {
     int nev;            // seeded: tie events the writer wave stored
     int evovf;          // seeded: more tie events than the slice holds (rerun unseeded)
     int tsorted;        // the target list is strictly increasing: positions from tmask/tpre
+    int jflag[3];       // phase C pointer jumping: "some pointer moved" per round (mod 3)
     KDJob job;          // the current job (kept in LDS: read where needed, not held in
                         // registers across phase A, whose expansion needs all of them)
 #ifdef SHD_STAMPS
@@ -506,6 +510,58 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
             }
         }
         __syncthreads();
+        // Lossless arcs (slot KD_ONE: exactly 1.0) multiply as exact no-ops, so a chain only
+        // needs the lossy ones (20% of the arcs on the BASELINE topologies): parv[v] becomes the
+        // nearest proper ancestor whose own arc is lossy (or s) by pointer jumping, each round
+        // doubling the lossless runs skipped (4-6 rounds).  A jump reads a pointer that may be
+        // mid-update in another thread; the old and the new value both skip only lossless
+        // vertices, so any interleaving gives the same products.  Run to convergence the
+        // walks below would take ~2.2 arcs per target instead of ~9.5 (wave maxima 6-7 vs ~18),
+        // but every round is a full pass of two LDS gathers per vertex, bank-conflict bound
+        // like the walk steps it saves: one round pays (KD_JUMPS).  (Path halving inside the
+        // walks instead, writing the skip back, measured the same as one round; both together
+        // slower.)
+        {
+            const int per = (n + B - 1) / B;  // vertices per thread: v = tid + k * B
+            unsigned long long live = per >= 64 ? ~0ull : ((1ull << per) - 1ull);
+            if (tid < 3) sm->jflag[tid] = 0;
+            __syncthreads();
+            // (round r raises slot r % 3 and clears slot (r + 1) % 3 before its barrier: the
+            // slot of round r - 1 may still be read after that barrier)
+            for (int rnd = 0; rnd < KD_JUMPS; rnd++) {
+                int any = 0;
+                for (int k0 = 0; k0 < per; k0 += 4) {
+                    const unsigned lb = k0 < 64 ? (unsigned)((live >> k0) & 0xFull) : 0xFu;
+                    if (!lb) continue;
+                    int vq[4], jq[4];
+                    bool act[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        vq[q] = tid + (k0 + q) * B;
+                        act[q] = ((lb >> q) & 1u) && vq[q] < n;
+                        jq[q] = act[q] ? (int)parv[vq[q]] : s;
+                    }
+                    unsigned rq[4], jj[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) { rq[q] = rixl[jq[q]]; jj[q] = parv[jq[q]]; }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        if (!act[q]) {
+                            if (k0 + q < 64) live &= ~(1ull << (k0 + q));
+                        } else if (jq[q] == s || rq[q] != (unsigned)KD_ONE) {
+                            if (k0 + q < 64) live &= ~(1ull << (k0 + q));
+                        } else {
+                            parv[vq[q]] = (uint16_t)jj[q];
+                            any = 1;
+                        }
+                    }
+                }
+                if (any) sm->jflag[rnd % 3] = 1;
+                if (tid == 0) sm->jflag[(rnd + 1) % 3] = 0;
+                __syncthreads();
+                if (!sm->jflag[rnd % 3]) break;
+            }
+        }
         KD_ACC(19);
         // sorted targets: one pass over the vertices, positions from the LDS mask (no
         // global load behind the previous group's stores); else over the target list

@@ -341,23 +341,25 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
     // ~12% of arcs are light; light in-arcs are the tail of each (-w)-sorted in-row
     const bool want_kd = !force || !strcmp(force, "kd") || !strcmp(force, "auto");
     if (want_kd && c->nnz > 0) {
-        int delta = 1;
-        if (const char* e = getenv("SHD_ROUTE_DELTA")) delta = std::max(1, atoi(e));
-        else {
-            // (12th percentile: 30 on C2-C4.  Seeded rows expand few vertices per bucket, so
-            // fewer, wider buckets pay: C4 seeded 57 -> 53 ms from the 6th percentile's 15)
-            std::vector<int> ws(c->nnz);
-            for (int a = 0; a < c->nnz; a++) ws[a] = (int)w[a];
-            const size_t k = (size_t)c->nnz * 12 / 100;
-            std::nth_element(ws.begin(), ws.begin() + k, ws.end());
-            delta = std::max(1, ws[k]);
-        }
         // one 1024-thread workgroup per CU when dist fills the LDS; smaller graphs run several
         // 256-thread workgroups (sources) per CU
         int blk = n > 16384 ? 1024 : 256;
         if (const char* e = getenv("SHD_ROUTE_KDBLOCK")) {
             const int b = atoi(e);
             if (b == 256 || b == 1024) blk = b;  // (512/768: the phase-A ring sizing assumes 256 or 1024)
+        }
+        int delta = 1;
+        if (const char* e = getenv("SHD_ROUTE_DELTA")) delta = std::max(1, atoi(e));
+        else {
+            // 1024-thread rows: the 12th percentile (30 on C4; seeded rows expand few vertices
+            // per bucket, so fewer, wider buckets pay: C4 57 -> 53 ms from the 6th percentile's
+            // 15; 20/45/60/90: 52.2/51.3/53.4/59.7 ms against 50.7).  256-thread rows (three
+            // compute waves) take the 18th (45 on C3: 3.00-3.03 ms against 3.06-3.12 at 30)
+            std::vector<int> ws(c->nnz);
+            for (int a = 0; a < c->nnz; a++) ws[a] = (int)w[a];
+            const size_t k = (size_t)c->nnz * (blk >= 1024 ? 12 : 18) / 100;
+            std::nth_element(ws.begin(), ws.begin() + k, ws.end());
+            delta = std::max(1, ws[k]);
         }
         const size_t base = kd_dispatch(blk, [&](auto B) { return kd_lds_bytes<decltype(B)::value>(n, 0); });
         if (base + 2 * 512 <= kLdsBudget) {

@@ -1118,9 +1118,11 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     int rb = 0;
                     if (lane == 0) {
                         rb = atomicAdd(&sm->rtail, nr);
-                        for (int w8 = 0; rb + nr - __hip_atomic_load(&sm->rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > RR
-                                         && w8 < (1 << 22); w8++)
+                        int w8 = 0;
+                        for (; rb + nr - __hip_atomic_load(&sm->rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > RR
+                               && w8 < (1 << 22); w8++)
                             __builtin_amdgcn_s_sleep(1);
+                        if (w8 >= (1 << 22)) raise_err(err, SHD_ROUTE_EDEVICE);
                     }
                     rb = __builtin_amdgcn_readfirstlane(rb);
                     if (mine) {
@@ -1369,8 +1371,12 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                 for (;;) {
                     const int rt = __hip_atomic_load(&sm->rtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if (rt > rd) {
-                        // up to 4 x 64 records per pass
-                        const int k = min(4 * 64, rt - rd);
+                        // up to 4 x 64 records per pass, and at most RR - 64: a compute wave whose
+                        // reservation (<= 64 slots) starts inside the pass then never waits for ring
+                        // space the pass has not released (with RR = 256 a full pass could hold the
+                        // first slots of a reservation whose owner was still waiting to write them:
+                        // both sides spun to their caps, a ~110 ms stall per occurrence on C3)
+                        const int k = min(min(4 * 64, RR - 64), rt - rd);
                         int uu[4], ev[4];
                         uint32_t xx[4];
 #pragma unroll
@@ -1382,10 +1388,12 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                                 const int slot = (rd + q * 64 + lane) & (RR - 1);
                                 volatile unsigned long long* sp = reinterpret_cast<volatile unsigned long long*>(&rrec[slot]);
                                 unsigned long long rv = *sp;
-                                for (int w8 = 0; (rv >> 32) == 0xFFFFFFFFull && w8 < (1 << 22); w8++) {
+                                int w8 = 0;
+                                for (; (rv >> 32) == 0xFFFFFFFFull && w8 < (1 << 22); w8++) {
                                     __builtin_amdgcn_s_sleep(1);
                                     rv = *sp;
                                 }
+                                if (w8 >= (1 << 22)) raise_err(err, SHD_ROUTE_EDEVICE);
                                 const uint32_t x = (uint32_t)rv, y = (uint32_t)(rv >> 32);
                                 *sp = 0xFFFFFFFF00000000ull;
                                 const int u = (int)(y & 0xFFFFu);

@@ -885,11 +885,6 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
     }
     __syncthreads();
     const bool tsorted = __builtin_amdgcn_readfirstlane(sm->tsorted) != 0;
-    // position of target vertex v (tsorted), -1 if v is not a target
-    auto tpos = [&](int v) __attribute__((always_inline)) {
-        const unsigned long long wd = tmask[v >> 6], bit = 1ull << (v & 63);
-        return (wd & bit) ? (int)tpre[v >> 6] + __popcll(wd & (bit - 1ull)) : -1;
-    };
 
     // sources: one each to start, then from a queue, so workgroups that drew cheap
     // sources take more and the launch ends within about one source of the mean

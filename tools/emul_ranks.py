@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Compute time of every rank of a W-way strong split of one config, each rank's plan run in
+turn on this one GPU (diagnostic for the multi-GPU partition: the slowest rank sets N>1 time).
+  python tools/emul_ranks.py --config c4 --world 8 [--reps 3]"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from shadow_amd.graph import config  # noqa: E402
+from shadow_amd.route import RouteEngine  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="c4")
+ap.add_argument("--world", type=int, nargs="+", default=[8])
+ap.add_argument("--reps", type=int, default=3)
+a = ap.parse_args()
+g = config(a.config)
+eng = RouteEngine(g)
+T = g.targets()
+dev = torch.device("cuda", 0)
+d_tgt = torch.from_numpy(np.ascontiguousarray(T, np.int32)).to(dev)
+st = torch.cuda.current_stream(dev)
+for W in a.world:
+    res = []
+    for r in range(W):
+        t0 = time.perf_counter()
+        plan = eng.plan(T, W, r)
+        tp = time.perf_counter() - t0
+        ns = len(plan.sources)
+        lat = torch.empty((max(ns, 1), len(T)), dtype=torch.float64, device=dev)
+        rel = torch.empty_like(lat)
+        mn = torch.full((max(ns, 1),), float("inf"), dtype=torch.float64, device=dev)
+        plan.rows_async(d_tgt, lat, rel, mn, stream=st.cuda_stream)
+        eng.sync(st.cuda_stream)
+        ms = []
+        for _ in range(a.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            plan.rows_async(d_tgt, lat, rel, mn, stream=st.cuda_stream)
+            e1.record(st)
+            eng.sync(st.cuda_stream)
+            ms.append(e0.elapsed_time(e1))
+        info = plan.info
+        res.append(min(ms))
+        print(f"W={W} rank {r}: rows {ns} helpers {info['helpers']} roots {info['roots']} levels {info['levels']} "
+              f"kernel {min(ms):.2f} ms (plan {tp * 1e3:.0f} ms)", flush=True)
+        del lat, rel, plan
+        torch.cuda.empty_cache()
+    print(f"W={W}: max {max(res):.2f} ms  mean {np.mean(res):.2f} ms", flush=True)

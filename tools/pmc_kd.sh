@@ -6,7 +6,7 @@ mkdir -p gpurun_out/pmc_kd
 run() {
   local name=$1; shift
   timeout -s KILL 90 rocprofv3 --pmc "$@" -d gpurun_out/pmc_kd/${name} -o run --output-format csv \
-    -- python3 bench.py --config c4 --sources 2048 --steps 1 --warmup 1 --no-cpu-baseline --verify 0 > gpurun_out/pmc_kd/${name}.log 2>&1 || echo "pass $name failed"
+    -- python3 bench.py --config c4 --steps 1 --warmup 1 --no-cpu-baseline --verify 0 > gpurun_out/pmc_kd/${name}.log 2>&1 || echo "pass $name failed"
 }
 run sq1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU
 run sq2 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE

@@ -1299,6 +1299,13 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                     if (--left[d] == 0) cq.push({ready[d], d});
                 }
             }
+            if (getenv("SHD_ROUTE_PLAN_DEBUG")) {
+                int hist[KD_SEEDS + 1] = {0};
+                for (int j = 0; j < nj; j++) hist[nsd[j]]++;
+                fprintf(stderr, "plan world %d rank %d: jobs %d levels %d seeds:", world, rank, nj, nlev);
+                for (int k = 0; k <= KD_SEEDS; k++) fprintf(stderr, " %d:%d", k, hist[k]);
+                fprintf(stderr, "\n");
+            }
             jobs.resize(nj);
             int qi = 0;
             for (int j : qorder) {

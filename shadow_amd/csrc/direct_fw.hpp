@@ -3,6 +3,11 @@
 #include "common.hpp"
 namespace shd {
 // K3: direct paths from dense per-pair latency / reliability (complete graphs).
+// One workgroup per source row; each lane takes two adjacent targets per step, so a sorted
+// contiguous target list (the attached set of a complete graph) streams W, R and the
+// outputs as 16-byte accesses (loads streamed once: nontemporal), two steps in flight;
+// any other list falls back to 8-byte accesses per target.
+typedef double k3_d2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(kBlock) void direct_rows_kernel(
     int n, const double* __restrict__ W, const double* __restrict__ R, const double* __restrict__ vf,
     const int* __restrict__ src, int ns, const int* __restrict__ tgt, int nt, long long ld,
@@ -14,28 +19,50 @@ __global__ __launch_bounds__(kBlock) void direct_rows_kernel(
         if (threadIdx.x == 0) rmin = kInfBits;
         __syncthreads();
         double lmin = INFINITY;
-        const double fs = (s >= 0 && s < n) ? vf[s] : NAN;
-        for (int j = threadIdx.x; j < nt; j += kBlock) {
-            const int t = tgt[j];
-            double Lv = NAN, Rv = NAN;
-            if (s < 0 || s >= n || t < 0 || t >= n) {
-                raise_err(err, SHD_ROUTE_EINVAL);
-            } else {
-                const double w = W[(long long)s * n + t];
-                if (isnan(w)) {
-                    raise_err(err, SHD_ROUTE_ENOEDGE);
-                } else {
-                    const double ft = vf[t];
-                    double Rr = 1.0;
-                    if (!isnan(fs)) Rr *= fs;
-                    if (!isnan(ft)) Rr *= ft;
-                    Lv = 0.0 + w;
-                    Rv = Rr * R[(long long)s * n + t];
-                }
+        const bool sok = s >= 0 && s < n;
+        const double fs = sok ? vf[s] : NAN;
+        const long long sb = (long long)(sok ? s : 0) * n;
+        double* lrow = lat_out ? lat_out + (long long)i * ld : nullptr;
+        double* rrow = rel_out ? rel_out + (long long)i * ld : nullptr;
+        // (lat, rel) of target t from its w, r and vertex factor (topology.c:1877-1927)
+        auto entry = [&](int t, double w, double r, double ft, double& Lv, double& Rv) __attribute__((always_inline)) {
+            Lv = NAN; Rv = NAN;
+            if (!sok || t < 0 || t >= n) raise_err(err, SHD_ROUTE_EINVAL);
+            else if (isnan(w)) raise_err(err, SHD_ROUTE_ENOEDGE);
+            else {
+                double Rr = 1.0;
+                if (!isnan(fs)) Rr *= fs;
+                if (!isnan(ft)) Rr *= ft;
+                Lv = 0.0 + w;
+                Rv = Rr * r;
             }
-            if (lat_out) lat_out[(long long)i * ld + j] = Lv;
-            if (rel_out) rel_out[(long long)i * ld + j] = Rv;
             lmin = fmin(lmin, Lv);
+        };
+        const bool out_even = !(((uintptr_t)lrow | (uintptr_t)rrow) & 8);
+#pragma unroll 2
+        for (int j0 = 2 * (int)threadIdx.x; j0 < nt; j0 += 2 * kBlock) {
+            const bool two = j0 + 1 < nt;
+            const int t0 = tgt[j0], t1 = two ? tgt[j0 + 1] : -1;
+            double w0 = NAN, w1 = NAN, r0 = NAN, r1 = NAN, f0 = NAN, f1 = NAN;
+            if (sok && two && t1 == t0 + 1 && t0 >= 0 && t1 < n && !((sb + t0) & 1) && !(t0 & 1)) {
+                const k3_d2 w = __builtin_nontemporal_load(reinterpret_cast<const k3_d2*>(W + sb + t0));
+                const k3_d2 r = __builtin_nontemporal_load(reinterpret_cast<const k3_d2*>(R + sb + t0));
+                const k3_d2 f = *reinterpret_cast<const k3_d2*>(vf + t0);
+                w0 = w.x; w1 = w.y; r0 = r.x; r1 = r.y; f0 = f.x; f1 = f.y;
+            } else {
+                if (sok && t0 >= 0 && t0 < n) { w0 = W[sb + t0]; r0 = R[sb + t0]; f0 = vf[t0]; }
+                if (sok && t1 >= 0 && t1 < n) { w1 = W[sb + t1]; r1 = R[sb + t1]; f1 = vf[t1]; }
+            }
+            double L0, R0, L1 = NAN, R1 = NAN;
+            entry(t0, w0, r0, f0, L0, R0);
+            if (two) entry(t1, w1, r1, f1, L1, R1);
+            if (two && out_even) {  // (j0 is even: the pair is 16-byte aligned with the row)
+                if (lrow) __builtin_nontemporal_store(k3_d2{L0, L1}, reinterpret_cast<k3_d2*>(lrow + j0));
+                if (rrow) __builtin_nontemporal_store(k3_d2{R0, R1}, reinterpret_cast<k3_d2*>(rrow + j0));
+            } else {
+                if (lrow) { __builtin_nontemporal_store(L0, lrow + j0); if (two) __builtin_nontemporal_store(L1, lrow + j0 + 1); }
+                if (rrow) { __builtin_nontemporal_store(R0, rrow + j0); if (two) __builtin_nontemporal_store(R1, rrow + j0 + 1); }
+            }
         }
         if (row_min) {
 #pragma unroll

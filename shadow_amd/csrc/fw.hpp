@@ -67,12 +67,16 @@ __device__ inline void fw_tile_product(const uint16_t* At, const uint16_t* Bt, u
     for (int k = 0; k < FW_T; k++) {
         const uint2 a = *reinterpret_cast<const uint2*>(At + k * FW_T + 4 * r);
         const uint2 b = *reinterpret_cast<const uint2*>(Bt + k * FW_T + 4 * c);
-        const uint32_t a2[4] = {(a.x & 0xFFFFu) * 0x10001u, (a.x >> 16) * 0x10001u, (a.y & 0xFFFFu) * 0x10001u,
-                                (a.y >> 16) * 0x10001u};
+        // a row value broadcast to both halves is a shuffle the packed add takes as an
+        // op_sel modifier: no instruction of its own
+        const fw_us2 ax = __builtin_bit_cast(fw_us2, a.x), ay = __builtin_bit_cast(fw_us2, a.y);
+        const fw_us2 bx = __builtin_bit_cast(fw_us2, b.x), by = __builtin_bit_cast(fw_us2, b.y);
+        const fw_us2 a2[4] = {__builtin_shufflevector(ax, ax, 0, 0), __builtin_shufflevector(ax, ax, 1, 1),
+                              __builtin_shufflevector(ay, ay, 0, 0), __builtin_shufflevector(ay, ay, 1, 1)};
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            acc[i][0] = fw_pkmin(acc[i][0], fw_pkadd(a2[i], b.x));
-            acc[i][1] = fw_pkmin(acc[i][1], fw_pkadd(a2[i], b.y));
+            acc[i][0] = fw_pkmin(acc[i][0], __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(a2[i], bx)));
+            acc[i][1] = fw_pkmin(acc[i][1], __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(a2[i], by)));
         }
     }
 }

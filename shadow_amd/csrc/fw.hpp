@@ -97,16 +97,24 @@ __device__ inline void fw_store_block(uint16_t* D, int np, int ti, int tj, int r
 }
 // a global tile into LDS, [row][col] (transpose = false) or [col][row]
 __device__ inline void fw_stage(const uint16_t* D, int np, int ti, int tj, uint16_t* L, bool transpose) {
-    for (int q = threadIdx.x; q < FW_T * FW_T / 4; q += 256) {
-        const int row = q / (FW_T / 4), c4 = (q % (FW_T / 4)) * 4;
-        const uint2 v = *reinterpret_cast<const uint2*>(D + (long long)(ti * FW_T + row) * np + tj * FW_T + c4);
-        if (!transpose) *reinterpret_cast<uint2*>(L + row * FW_T + c4) = v;
-        else {
-            L[(c4 + 0) * FW_T + row] = (uint16_t)(v.x & 0xFFFFu);
-            L[(c4 + 1) * FW_T + row] = (uint16_t)(v.x >> 16);
-            L[(c4 + 2) * FW_T + row] = (uint16_t)(v.y & 0xFFFFu);
-            L[(c4 + 3) * FW_T + row] = (uint16_t)(v.y >> 16);
+    if (!transpose) {
+        for (int q = threadIdx.x; q < FW_T * FW_T / 4; q += 256) {
+            const int row = q / (FW_T / 4), c4 = (q % (FW_T / 4)) * 4;
+            *reinterpret_cast<uint2*>(L + row * FW_T + c4) =
+                *reinterpret_cast<const uint2*>(D + (long long)(ti * FW_T + row) * np + tj * FW_T + c4);
         }
+        return;
+    }
+    // transposed: a wave's lanes take 64 consecutive rows of one 4-column strip, so the
+    // 2-byte LDS writes of a wave land on consecutive addresses (lanes of one row would all
+    // write one bank: 16-way conflicts)
+    for (int q = threadIdx.x; q < FW_T * FW_T / 4; q += 256) {
+        const int row = q % FW_T, c4 = (q / FW_T) * 4;
+        const uint2 v = *reinterpret_cast<const uint2*>(D + (long long)(ti * FW_T + row) * np + tj * FW_T + c4);
+        L[(c4 + 0) * FW_T + row] = (uint16_t)(v.x & 0xFFFFu);
+        L[(c4 + 1) * FW_T + row] = (uint16_t)(v.x >> 16);
+        L[(c4 + 2) * FW_T + row] = (uint16_t)(v.y & 0xFFFFu);
+        L[(c4 + 3) * FW_T + row] = (uint16_t)(v.y >> 16);
     }
 }
 
@@ -116,6 +124,9 @@ __global__ __launch_bounds__(256) void fw_diag_kernel(uint16_t* __restrict__ D, 
     const int r = threadIdx.x / 16, c = threadIdx.x % 16;
     fw_stage(D, np, kb, kb, T, false);
     __syncthreads();
+    // step k reads row k and column k, which step k leaves unchanged (D[k][k] = 0:
+    // min(D[i][k], D[i][k] + 0) = D[i][k]), so its writes need no barrier before them: one
+    // barrier per step (writes of step k before the reads of step k + 1)
     for (int k = 0; k < FW_T; k++) {
         uint32_t col[4];
 #pragma unroll
@@ -128,7 +139,6 @@ __global__ __launch_bounds__(256) void fw_diag_kernel(uint16_t* __restrict__ D, 
             v[i][0] = fw_pkmin(x.x, fw_pkadd(col[i], rowk.x));
             v[i][1] = fw_pkmin(x.y, fw_pkadd(col[i], rowk.y));
         }
-        __syncthreads();  // every read of step k done before its writes
 #pragma unroll
         for (int i = 0; i < 4; i++)
             *reinterpret_cast<uint2*>(T + (4 * r + i) * FW_T + 4 * c) = make_uint2(v[i][0], v[i][1]);

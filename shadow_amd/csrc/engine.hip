@@ -1240,16 +1240,58 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // seeds of each job: the kseeds neighbours u (jobs of this rank, smaller rank, level
         // below the cap) with the smallest w(s,u) + closeness(u), i.e. the likely gateways
         // of most shortest paths from s
+        // A row with fewer such neighbours (a multi-GPU rank holds only its own rows) takes
+        // two-hop seeds s -> x -> u (u one of this rank's rows, x any neighbour of degree
+        // <= 256): D0 = w(s,x) + w(x,u) + d_u(.) is as consistent as a neighbour's, and u's
+        // own record is the arc (x,u), tight whenever u keeps D0.
+        bool two_hop = true;
+        if (const char* e = getenv("SHD_ROUTE_SEED2HOP")) two_hop = atoi(e) != 0;
         std::vector<int> fl(n, -1);  // first job of a vertex, once its level is below the cap
+        std::vector<std::array<int, KD_SEEDS>> srec(nj);
+        struct Hop { double cost; int u, off; uint32_t rec; };
+        std::vector<Hop> hops;
         int nlev = 1, q = 0;
         for (int p : order) {
-            const int j = jpos_of[p];
+            const int j = jpos_of[p], s = src[p];
             int arcs[KD_SEEDS];
-            const int m = q++ >= nroot_min ? best_seeds(p, fl, kseeds, arcs) : 0;
+            const bool seedable = q++ >= nroot_min;
+            int m = seedable ? best_seeds(p, fl, kseeds, arcs) : 0;
             for (int k = 0; k < m; k++) {
-                const int a = arcs[k], u = c->h_col[a], sj = first[u];
-                seedjob[j][k] = sj; su[j][k] = u;
-                wr[j][k] = (int)c->h_w[a] | ((int)c->h_ridx[a] << 16);
+                const int a = arcs[k], u = c->h_col[a];
+                su[j][k] = u;
+                wr[j][k] = (int)c->h_w[a];
+                srec[j][k] = (int)((uint32_t)s | ((uint32_t)c->h_ridx[a] << 16) | ((uint32_t)c->h_w[a] << 24));
+            }
+            if (two_hop && seedable && m < kseeds) {
+                hops.clear();
+                for (int a = c->h_row[s]; a < c->h_row[s + 1]; a++) {
+                    const int x = c->h_col[a];
+                    if (x == s || c->h_row[x + 1] - c->h_row[x] > 256) continue;
+                    for (int b = c->h_row[x]; b < c->h_row[x + 1]; b++) {
+                        const int u = c->h_col[b];
+                        if (u == s || u == x || fl[u] < 0 || rk[u] >= rk[s]) continue;
+                        bool dup = false;
+                        for (int k = 0; k < m; k++) dup = dup || su[j][k] == u;
+                        if (dup) continue;
+                        hops.push_back({c->h_w[a] + c->h_w[b] + c->close[u], u, (int)(c->h_w[a] + c->h_w[b]),
+                                        (uint32_t)x | ((uint32_t)c->h_ridx[b] << 16) | ((uint32_t)c->h_w[b] << 24)});
+                    }
+                }
+                std::sort(hops.begin(), hops.end(), [](const Hop& x, const Hop& y) {
+                    return x.cost != y.cost ? x.cost < y.cost : x.u != y.u ? x.u < y.u : x.rec < y.rec;
+                });
+                for (const Hop& h : hops) {
+                    if (m == kseeds) break;
+                    bool dup = false;
+                    for (int k = 0; k < m; k++) dup = dup || su[j][k] == h.u;
+                    if (dup) continue;
+                    su[j][m] = h.u; wr[j][m] = h.off; srec[j][m] = (int)h.rec;
+                    m++;
+                }
+            }
+            for (int k = 0; k < m; k++) {
+                const int sj = first[su[j][k]];
+                seedjob[j][k] = sj;
                 lvl[j] = std::max(lvl[j], lvl[sj] + 1);
                 if (slot[sj] < 0) slot[sj] = P->nslots++;
             }
@@ -1313,7 +1355,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 std::memset(&J, 0, sizeof(J));
                 J.row = job_row[j]; J.s = src[job_pos[j]]; J.store = slot[j]; J.nseed = nsd[j];
                 for (int k = 0; k < nsd[j]; k++) {
-                    J.seed[k] = slot[seedjob[j][k]]; J.u[k] = su[j][k]; J.wr[k] = wr[j][k];
+                    J.seed[k] = slot[seedjob[j][k]]; J.u[k] = su[j][k]; J.wr[k] = wr[j][k]; J.rec[k] = srec[j][k];
                 }
             }
             P->seeded = 1;

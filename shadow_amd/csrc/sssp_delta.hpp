@@ -93,9 +93,12 @@ struct KDJob {
     int store;             // row-store slot this row is kept in for later seeds, -1 = not kept
     int nseed;             // seeds used (0 = unseeded: a root)
     int seed[KD_SEEDS];    // row-store slots of the seeds' rows
-    int u[KD_SEEDS];       // seed vertices (neighbours of s)
-    int wr[KD_SEEDS];      // w(s,u) | ridx(s,u) << 16
-    int pad[16 - 4 - 3 * KD_SEEDS];
+    int u[KD_SEEDS];       // seed vertices: neighbours of s, or two hops away (s -> x -> u)
+    int wr[KD_SEEDS];      // offset: the length of the s -> u path the seed's row is shifted by
+    int rec[KD_SEEDS];     // parent record of u itself if it keeps D0: s | ridx(s,u) << 16 |
+                           // w(s,u) << 24 for a neighbour, x | ridx(x,u) << 16 | w(x,u) << 24
+                           // for a two-hop seed (arc (x,u) is tight whenever u keeps D0)
+    int pad[16 - 4 - 4 * KD_SEEDS];
 };
 static_assert(sizeof(KDJob) == 64, "one 64-byte job record");
 constexpr uint32_t KD_EVTAG = 0xFFFF0000u;  // ring record y of a tie event: v | KD_EVTAG
@@ -391,7 +394,8 @@ __device__ inline void kd_relax_list(const uint32_t* wimp, int cnt, int lane, un
         const int sl_ = __builtin_amdgcn_readfirstlane(q_ < nseed ? sm->job.seed[q_] : 0);             \
         const unsigned wr_ = (unsigned)__builtin_amdgcn_readfirstlane(q_ < nseed ? sm->job.wr[q_] : 0); \
         su[q_] = __builtin_amdgcn_readfirstlane(q_ < nseed ? sm->job.u[q_] : -1);                      \
-        sslot[q_] = sl_; wsu[q_] = wr_ & 0xFFFFu; rsu[q_] = wr_ >> 16;                                 \
+        sslot[q_] = sl_; wsu[q_] = wr_ & 0xFFFFu;                                                      \
+        rsu[q_] = (unsigned)__builtin_amdgcn_readfirstlane(q_ < nseed ? sm->job.rec[q_] : 0);          \
         sdrow[q_] = g.drow + (size_t)sl_ * g.rstride;                                                  \
         sprow[q_] = g.prow + (size_t)sl_ * g.rstride;                                                  \
     }                                                                                                  \
@@ -986,7 +990,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         const unsigned d = (h & 1) ? (d2 >> 16) : (d2 & 0xFFFFu);
                         const unsigned c = q < nseed ? min(0xFFFFu, wsu[q] + d) : 0xFFFFFu;
                         const uint32_t p = kd_comp(pq[q], h);
-                        const uint32_t r = v == su[q] ? ((uint32_t)s | (rsu[q] << 16) | (wsu[q] << 24)) : p;
+                        const uint32_t r = v == su[q] ? rsu[q] : p;  // (rsu: the seed vertex's record)
                         const uint32_t k = __builtin_amdgcn_perm(~r, r, 0x07010002u);  // (255-w) | p | ridx
                         if (c < dbest || (c == dbest && k < kbest)) { dbest = c; kbest = k; rbest = r; }
                     }

@@ -20,6 +20,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c2")
 ap.add_argument("--sources", type=int, default=0)
 ap.add_argument("--plan", action="store_true", help="seeded plan over the sources (rows in source order)")
+ap.add_argument("--world", type=int, default=1, help="with --plan: rank --rank of a W-way split")
+ap.add_argument("--rank", type=int, default=0)
 a = ap.parse_args()
 g = config(a.config)
 eng = route.RouteEngine(g)
@@ -36,7 +38,12 @@ nwg = (len(S) + 7) // 8
 dbg = torch.zeros((len(S) + nwg) * 32, dtype=torch.int64, device=dev)
 L.shd_route_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
 L.shd_route_debug_buffer(eng._h, C.c_void_p(dbg.data_ptr()))
-plan = eng.plan(S) if a.plan else None
+plan = eng.plan(S, a.world, a.rank) if a.plan else None
+if plan is not None and a.world > 1:
+    S = plan.sources
+    lat = torch.empty((len(S), len(T)), dtype=torch.float64, device=dev)
+    rel = torch.empty_like(lat)
+    mn = torch.empty(len(S), dtype=torch.float64, device=dev)
 for rep in range(3):
     dbg.zero_()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -1233,7 +1233,10 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // default depth cap: about half the rows each workgroup slot runs in turn, so that
         // seed chains are shorter than a slot's queue, and at least 8 (C4: 195 rows per
         // slot, no cap in effect; C3: 9 per slot, cap 8: 3.5 -> 3.1 ms against cap 4)
-        int kseeds = 2, nroot_min = c->kd_slots, depth = std::max(8, nj / std::max(1, 2 * c->kd_slots));
+        // (seeds per row: three on 1024-thread rows, C4 48.6 -> 48.1 ms; two on 256-thread
+        // rows, whose init pass costs relatively more: C3 3.00 vs 3.07 ms with three)
+        int kseeds = std::min(KD_SEEDS, c->kd_block >= 1024 ? 3 : 2), nroot_min = c->kd_slots;
+        int depth = std::max(8, nj / std::max(1, 2 * c->kd_slots));
         if (const char* e = getenv("SHD_ROUTE_SEEDS")) kseeds = std::max(1, std::min(KD_SEEDS, atoi(e)));
         if (const char* e = getenv("SHD_ROUTE_SEED_ROOTS")) nroot_min = std::max(0, atoi(e));
         if (const char* e = getenv("SHD_ROUTE_SEED_DEPTH")) depth = std::max(1, atoi(e));

@@ -83,11 +83,14 @@ constexpr uint32_t KD_SRC_MARK = 0xFFFFFFFEu;  // parent record of the source it
 // lgkmcnt too, so every LDS wait would also wait for the output stores
 #define KD_GLOBAL __attribute__((address_space(1)))
 
-constexpr int KD_SEEDS = 2;
+#ifndef KD_NSEEDS
+#define KD_NSEEDS 3  // seeds per row at most (KDJob holds up to 3; the planner's default: engine.hip)
+#endif
+constexpr int KD_SEEDS = KD_NSEEDS;
 #ifndef KD_JUMPS
 #define KD_JUMPS 1  // phase C pointer-jumping rounds before the walks (C4: 0: 50.5 ms, 1: 48.6, 2: 49.3, 3: 51.5, to convergence: 54.2)
 #endif
-struct KDJob {
+struct __attribute__((aligned(64))) KDJob {  // padded to 64 bytes (copied as 16 ints)
     int row;               // output row
     int s;                 // source vertex
     int store;             // row-store slot this row is kept in for later seeds, -1 = not kept
@@ -98,7 +101,6 @@ struct KDJob {
     int rec[KD_SEEDS];     // parent record of u itself if it keeps D0: s | ridx(s,u) << 16 |
                            // w(s,u) << 24 for a neighbour, x | ridx(x,u) << 16 | w(x,u) << 24
                            // for a two-hop seed (arc (x,u) is tight whenever u keeps D0)
-    int pad[16 - 4 - 4 * KD_SEEDS];
 };
 static_assert(sizeof(KDJob) == 64, "one 64-byte job record");
 constexpr uint32_t KD_EVTAG = 0xFFFF0000u;  // ring record y of a tie event: v | KD_EVTAG

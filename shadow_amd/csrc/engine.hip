@@ -1235,7 +1235,9 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // slot, no cap in effect; C3: 9 per slot, cap 8: 3.5 -> 3.1 ms against cap 4)
         // (seeds per row: three on 1024-thread rows, C4 48.6 -> 48.1 ms; two on 256-thread
         // rows, whose init pass costs relatively more: C3 3.00 vs 3.07 ms with three)
-        int kseeds = std::min(KD_SEEDS, c->kd_block >= 1024 ? 3 : 2), nroot_min = c->kd_slots;
+        // (multi-GPU ranks: two; a rank's third candidates are mostly two-hop rows, and the
+        // extra init pass costs more than they save: 8-way C4 rank 9.6 vs 9.4 ms with three)
+        int kseeds = std::min(KD_SEEDS, c->kd_block >= 1024 && world == 1 ? 3 : 2), nroot_min = c->kd_slots;
         int depth = std::max(8, nj / std::max(1, 2 * c->kd_slots));
         if (const char* e = getenv("SHD_ROUTE_SEEDS")) kseeds = std::max(1, std::min(KD_SEEDS, atoi(e)));
         if (const char* e = getenv("SHD_ROUTE_SEED_ROOTS")) nroot_min = std::max(0, atoi(e));

@@ -5,6 +5,8 @@
 #include <chrono>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <sys/mman.h>
 #include <queue>
 #include <thread>
 #include "sssp_f64.hpp"
@@ -1592,14 +1594,56 @@ __global__ __launch_bounds__(256) void tri_pack_kernel(const double* __restrict_
 
 extern "C" {
 
+// Pinned host memory for the fill's triangle (C4: 20 GB).  hipHostMalloc faults and pins
+// 4 KiB pages one by one (3.4 s for 20 GiB on the box); anonymous memory advised as
+// transparent huge pages, first-touched by 16 threads and then registered takes 0.15 s
+// for the same D2H rate (tools/micro/pin_bench.cpp).  hipHostMalloc stays the fallback.
+namespace {
+std::mutex g_host_mu;
+std::map<void*, size_t> g_host_maps;  // registered mappings -> their length
+}  // namespace
+
 void* shd_route_host_alloc(size_t bytes) {
+    if (!bytes) bytes = 1;
+    const size_t len = (bytes + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
+    void* m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m != MAP_FAILED) {
+        (void)madvise(m, len, MADV_HUGEPAGE);
+        const int nth = (int)std::max<size_t>(1, std::min<size_t>(16, len >> 28));  // a thread per 256 MiB, <= 16
+        std::vector<std::thread> th;
+        const size_t per = (len / nth + 4095) & ~(size_t)4095;
+        for (int t = 0; t < nth; t++)
+            th.emplace_back([=] {
+                char* b = (char*)m;
+                for (size_t o = per * t; o < std::min(len, per * (t + 1)); o += 4096) b[o] = 0;
+            });
+        for (auto& x : th) x.join();
+        if (hipHostRegister(m, len, hipHostRegisterPortable) == hipSuccess) {
+            std::lock_guard<std::mutex> lk(g_host_mu);
+            g_host_maps[m] = len;
+            return m;
+        }
+        munmap(m, len);
+    }
     void* p = nullptr;
-    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) return nullptr;
     return p;
 }
 
 void shd_route_host_free(void* p) {
-    if (p) (void)hipHostFree(p);
+    if (!p) return;
+    size_t len = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_host_mu);
+        auto it = g_host_maps.find(p);
+        if (it != g_host_maps.end()) { len = it->second; g_host_maps.erase(it); }
+    }
+    if (len) {
+        (void)hipHostUnregister(p);
+        munmap(p, len);
+    } else {
+        (void)hipHostFree(p);
+    }
 }
 
 int shd_route_fill_triangle(shd_route_t* c, const int32_t* A, int32_t na, int32_t world, int32_t rank, uint32_t flags,

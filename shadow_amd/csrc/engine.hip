@@ -1323,6 +1323,9 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             // earliest.  A row still follows all of its seeds in the queue (no deadlock),
             // but rows no longer wait at every level boundary for seeds just started.
             const int W = std::max(1, c->kd_slots);
+            double root_cost = 3.4, flag_at = 0.7;
+            if (const char* e = getenv("SHD_ROUTE_ROOTCOST")) root_cost = std::max(0.1, atof(e));
+            if (const char* e = getenv("SHD_ROUTE_FLAGAT")) flag_at = std::max(0.0, std::min(1.0, atof(e)));
             std::vector<std::vector<int>> dep(nj);
             std::vector<int> left(nj);
             for (int j = 0; j < nj; j++) {
@@ -1340,11 +1343,11 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 const DI f = free_at.top(); free_at.pop();
                 const DI jr = cq.top(); cq.pop();
                 const int j = jr.second;
-                const double t = nsd[j] ? 1.0 : 3.4, start = std::max(f.first, jr.first);
+                const double t = nsd[j] ? 1.0 : root_cost, start = std::max(f.first, jr.first);
                 free_at.push({start + t, f.second});
                 qorder.push_back(j);
                 for (int d : dep[j]) {
-                    ready[d] = std::max(ready[d], start + 0.7 * t);
+                    ready[d] = std::max(ready[d], start + flag_at * t);
                     if (--left[d] == 0) cq.push({ready[d], d});
                 }
             }

@@ -33,7 +33,10 @@
 
 namespace shd {
 
-constexpr int FW_T = 64;  // tile edge
+#ifndef FW_TILE
+#define FW_TILE 64  // (128 with 8 x 8 blocks measured 5.5 ms against 3.9: 2 waves per SIMD, 128-step pivots)
+#endif
+constexpr int FW_T = FW_TILE;  // tile edge (64: 4 x 4 per thread, 128: 8 x 8)
 
 typedef unsigned short fw_us2 __attribute__((ext_vector_type(2)));
 
@@ -60,102 +63,136 @@ __global__ void fw_init_kernel(const double* __restrict__ W, int n, int np, uint
     D[k] = d;
 }
 
-// one 64x64 tile product C = min(C, A (x) B); At is A transposed ([k][i]), B is [k][j];
-// the thread's C block (rows 4r.., cols 4c..) in acc[4][2] (packed column pairs)
-__device__ inline void fw_tile_product(const uint16_t* At, const uint16_t* Bt, uint32_t acc[4][2], int r, int c) {
-#pragma unroll 8
-    for (int k = 0; k < FW_T; k++) {
-        const uint2 a = *reinterpret_cast<const uint2*>(At + k * FW_T + 4 * r);
-        const uint2 b = *reinterpret_cast<const uint2*>(Bt + k * FW_T + 4 * c);
+// R consecutive u16 as R/2 packed words (8 or 16 bytes: one LDS or global access)
+template <int H>
+__device__ inline void fw_ld(const uint16_t* p, uint32_t (&v)[H]) {
+    if constexpr (H == 2) {
+        const uint2 x = *reinterpret_cast<const uint2*>(p);
+        v[0] = x.x; v[1] = x.y;
+    } else {
+        static_assert(H == 4, "4 or 8 columns per thread");
+        const uint4 x = *reinterpret_cast<const uint4*>(p);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    }
+}
+template <int H>
+__device__ inline void fw_st(uint16_t* p, const uint32_t (&v)[H]) {
+    if constexpr (H == 2) *reinterpret_cast<uint2*>(p) = make_uint2(v[0], v[1]);
+    else *reinterpret_cast<uint4*>(p) = make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// One T x T tile product C = min(C, A (x) B); At is A transposed ([k][i]), B is [k][j].
+// 256 threads as 16 x 16, each an R x R block (R = T / 16: rows R r.., columns R c..) held
+// as R x R/2 packed column pairs.  Per k: one R-wide read of A's column and of B's row
+// (8- or 16-byte LDS reads) for R^2 relaxations.
+template <int T>
+__device__ inline void fw_tile_product(const uint16_t* At, const uint16_t* Bt, uint32_t (&acc)[T / 16][T / 32], int r, int c) {
+    constexpr int R = T / 16, H = R / 2;
+#pragma unroll 4
+    for (int k = 0; k < T; k++) {
+        uint32_t av[H], bv[H];
+        fw_ld<H>(At + k * T + R * r, av);
+        fw_ld<H>(Bt + k * T + R * c, bv);
         // a row value broadcast to both halves is a shuffle the packed add takes as an
         // op_sel modifier: no instruction of its own
-        const fw_us2 ax = __builtin_bit_cast(fw_us2, a.x), ay = __builtin_bit_cast(fw_us2, a.y);
-        const fw_us2 bx = __builtin_bit_cast(fw_us2, b.x), by = __builtin_bit_cast(fw_us2, b.y);
-        const fw_us2 a2[4] = {__builtin_shufflevector(ax, ax, 0, 0), __builtin_shufflevector(ax, ax, 1, 1),
-                              __builtin_shufflevector(ay, ay, 0, 0), __builtin_shufflevector(ay, ay, 1, 1)};
+        fw_us2 a2[R];
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            acc[i][0] = fw_pkmin(acc[i][0], __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(a2[i], bx)));
-            acc[i][1] = fw_pkmin(acc[i][1], __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(a2[i], by)));
+        for (int h = 0; h < H; h++) {
+            const fw_us2 x = __builtin_bit_cast(fw_us2, av[h]);
+            a2[2 * h] = __builtin_shufflevector(x, x, 0, 0);
+            a2[2 * h + 1] = __builtin_shufflevector(x, x, 1, 1);
         }
+#pragma unroll
+        for (int i = 0; i < R; i++)
+#pragma unroll
+            for (int h = 0; h < H; h++)
+                acc[i][h] = fw_pkmin(acc[i][h], __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(
+                                                                                a2[i], __builtin_bit_cast(fw_us2, bv[h]))));
     }
 }
 
-// tile (ti, tj) of D <-> registers of the thread's 4x4 block
-__device__ inline void fw_load_block(const uint16_t* D, int np, int ti, int tj, int r, int c, uint32_t acc[4][2]) {
+// tile (ti, tj) of D <-> registers of the thread's R x R block
+template <int T>
+__device__ inline void fw_load_block(const uint16_t* D, int np, int ti, int tj, int r, int c, uint32_t (&acc)[T / 16][T / 32]) {
+    constexpr int R = T / 16;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint2 v = *reinterpret_cast<const uint2*>(D + (long long)(ti * FW_T + 4 * r + i) * np + tj * FW_T + 4 * c);
-        acc[i][0] = v.x; acc[i][1] = v.y;
-    }
+    for (int i = 0; i < R; i++) fw_ld<R / 2>(D + (long long)(ti * T + R * r + i) * np + tj * T + R * c, acc[i]);
 }
-__device__ inline void fw_store_block(uint16_t* D, int np, int ti, int tj, int r, int c, const uint32_t acc[4][2]) {
+template <int T>
+__device__ inline void fw_store_block(uint16_t* D, int np, int ti, int tj, int r, int c, const uint32_t (&acc)[T / 16][T / 32]) {
+    constexpr int R = T / 16;
 #pragma unroll
-    for (int i = 0; i < 4; i++)
-        *reinterpret_cast<uint2*>(D + (long long)(ti * FW_T + 4 * r + i) * np + tj * FW_T + 4 * c) =
-            make_uint2(acc[i][0], acc[i][1]);
+    for (int i = 0; i < R; i++) fw_st<R / 2>(D + (long long)(ti * T + R * r + i) * np + tj * T + R * c, acc[i]);
 }
 // a global tile into LDS, [row][col] (transpose = false) or [col][row]
+template <int T>
 __device__ inline void fw_stage(const uint16_t* D, int np, int ti, int tj, uint16_t* L, bool transpose) {
     if (!transpose) {
-        for (int q = threadIdx.x; q < FW_T * FW_T / 4; q += 256) {
-            const int row = q / (FW_T / 4), c4 = (q % (FW_T / 4)) * 4;
-            *reinterpret_cast<uint2*>(L + row * FW_T + c4) =
-                *reinterpret_cast<const uint2*>(D + (long long)(ti * FW_T + row) * np + tj * FW_T + c4);
+        for (int q = threadIdx.x; q < T * T / 4; q += 256) {
+            const int row = q / (T / 4), c4 = (q % (T / 4)) * 4;
+            *reinterpret_cast<uint2*>(L + row * T + c4) =
+                *reinterpret_cast<const uint2*>(D + (long long)(ti * T + row) * np + tj * T + c4);
         }
         return;
     }
     // transposed: a wave's lanes take 64 consecutive rows of one 4-column strip, so the
     // 2-byte LDS writes of a wave land on consecutive addresses (lanes of one row would all
     // write one bank: 16-way conflicts)
-    for (int q = threadIdx.x; q < FW_T * FW_T / 4; q += 256) {
-        const int row = q % FW_T, c4 = (q / FW_T) * 4;
-        const uint2 v = *reinterpret_cast<const uint2*>(D + (long long)(ti * FW_T + row) * np + tj * FW_T + c4);
-        L[(c4 + 0) * FW_T + row] = (uint16_t)(v.x & 0xFFFFu);
-        L[(c4 + 1) * FW_T + row] = (uint16_t)(v.x >> 16);
-        L[(c4 + 2) * FW_T + row] = (uint16_t)(v.y & 0xFFFFu);
-        L[(c4 + 3) * FW_T + row] = (uint16_t)(v.y >> 16);
+    for (int q = threadIdx.x; q < T * T / 4; q += 256) {
+        const int row = q % T, c4 = (q / T) * 4;
+        const uint2 v = *reinterpret_cast<const uint2*>(D + (long long)(ti * T + row) * np + tj * T + c4);
+        L[(c4 + 0) * T + row] = (uint16_t)(v.x & 0xFFFFu);
+        L[(c4 + 1) * T + row] = (uint16_t)(v.x >> 16);
+        L[(c4 + 2) * T + row] = (uint16_t)(v.y & 0xFFFFu);
+        L[(c4 + 3) * T + row] = (uint16_t)(v.y >> 16);
     }
 }
 
-// pivot tile kb: 64 dependent steps (D[i][j] = min(D[i][j], D[i][k] + D[k][j]))
+// pivot tile kb: T dependent steps (D[i][j] = min(D[i][j], D[i][k] + D[k][j]))
+template <int T>
 __global__ __launch_bounds__(256) void fw_diag_kernel(uint16_t* __restrict__ D, int np, int kb) {
-    __shared__ __attribute__((aligned(16))) uint16_t T[FW_T * FW_T];
+    constexpr int R = T / 16, H = R / 2;
+    __shared__ __attribute__((aligned(16))) uint16_t L[T * T];
     const int r = threadIdx.x / 16, c = threadIdx.x % 16;
-    fw_stage(D, np, kb, kb, T, false);
+    fw_stage<T>(D, np, kb, kb, L, false);
     __syncthreads();
     // step k reads row k and column k, which step k leaves unchanged (D[k][k] = 0:
     // min(D[i][k], D[i][k] + 0) = D[i][k]), so its writes need no barrier before them: one
     // barrier per step (writes of step k before the reads of step k + 1)
-    for (int k = 0; k < FW_T; k++) {
-        uint32_t col[4];
+    for (int k = 0; k < T; k++) {
+        fw_us2 col[R];
 #pragma unroll
-        for (int i = 0; i < 4; i++) col[i] = (uint32_t)T[(4 * r + i) * FW_T + k] * 0x10001u;
-        const uint2 rowk = *reinterpret_cast<const uint2*>(T + k * FW_T + 4 * c);
-        uint32_t v[4][2];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const uint2 x = *reinterpret_cast<const uint2*>(T + (4 * r + i) * FW_T + 4 * c);
-            v[i][0] = fw_pkmin(x.x, fw_pkadd(col[i], rowk.x));
-            v[i][1] = fw_pkmin(x.y, fw_pkadd(col[i], rowk.y));
+        for (int i = 0; i < R; i++) {
+            const unsigned short x = L[(R * r + i) * T + k];
+            col[i] = fw_us2{x, x};
         }
+        uint32_t rowk[H];
+        fw_ld<H>(L + k * T + R * c, rowk);
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-            *reinterpret_cast<uint2*>(T + (4 * r + i) * FW_T + 4 * c) = make_uint2(v[i][0], v[i][1]);
+        for (int i = 0; i < R; i++) {
+            uint32_t x[H];
+            fw_ld<H>(L + (R * r + i) * T + R * c, x);
+#pragma unroll
+            for (int h = 0; h < H; h++)
+                x[h] = fw_pkmin(x[h], __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(
+                                                                      col[i], __builtin_bit_cast(fw_us2, rowk[h]))));
+            fw_st<H>(L + (R * r + i) * T + R * c, x);
+        }
         __syncthreads();
     }
-    for (int q = threadIdx.x; q < FW_T * FW_T / 4; q += 256) {
-        const int row = q / (FW_T / 4), c4 = (q % (FW_T / 4)) * 4;
-        *reinterpret_cast<uint2*>(D + (long long)(kb * FW_T + row) * np + kb * FW_T + c4) =
-            *reinterpret_cast<const uint2*>(T + row * FW_T + c4);
+    for (int q = threadIdx.x; q < T * T / 4; q += 256) {
+        const int row = q / (T / 4), c4 = (q % (T / 4)) * 4;
+        *reinterpret_cast<uint2*>(D + (long long)(kb * T + row) * np + kb * T + c4) =
+            *reinterpret_cast<const uint2*>(L + row * T + c4);
     }
 }
 
 // panels of pivot kb: blockIdx.y = 0 row panel (kb, b), 1 column panel (b, kb), b != kb
+template <int T>
 __global__ __launch_bounds__(256) void fw_panel_kernel(uint16_t* __restrict__ D, int np, int kb) {
-    __shared__ __attribute__((aligned(16))) uint16_t At[FW_T * FW_T];
-    __shared__ __attribute__((aligned(16))) uint16_t Bt[FW_T * FW_T];
-    const int nb = np / FW_T;
+    __shared__ __attribute__((aligned(16))) uint16_t At[T * T];
+    __shared__ __attribute__((aligned(16))) uint16_t Bt[T * T];
+    const int nb = np / T;
     int b = blockIdx.x;
     if (b >= kb) b++;
     if (b >= nb) return;
@@ -163,32 +200,33 @@ __global__ __launch_bounds__(256) void fw_panel_kernel(uint16_t* __restrict__ D,
     const bool rowp = blockIdx.y == 0;
     const int ti = rowp ? kb : b, tj = rowp ? b : kb;
     // row panel: C = D* (x) C (A = pivot, B = the panel); column panel: C = C (x) D*
-    fw_stage(D, np, rowp ? kb : ti, rowp ? kb : tj, At, true);
-    fw_stage(D, np, rowp ? ti : kb, rowp ? tj : kb, Bt, false);
+    fw_stage<T>(D, np, rowp ? kb : ti, rowp ? kb : tj, At, true);
+    fw_stage<T>(D, np, rowp ? ti : kb, rowp ? tj : kb, Bt, false);
     __syncthreads();
-    uint32_t acc[4][2];
-    fw_load_block(D, np, ti, tj, r, c, acc);
-    fw_tile_product(At, Bt, acc, r, c);
-    fw_store_block(D, np, ti, tj, r, c, acc);
+    uint32_t acc[T / 16][T / 32];
+    fw_load_block<T>(D, np, ti, tj, r, c, acc);
+    fw_tile_product<T>(At, Bt, acc, r, c);
+    fw_store_block<T>(D, np, ti, tj, r, c, acc);
 }
 
 // every tile (i, j), i, j != kb: C = min(C, D[i][kb] (x) D[kb][j])
+template <int T>
 __global__ __launch_bounds__(256) void fw_rest_kernel(uint16_t* __restrict__ D, int np, int kb) {
-    __shared__ __attribute__((aligned(16))) uint16_t At[FW_T * FW_T];
-    __shared__ __attribute__((aligned(16))) uint16_t Bt[FW_T * FW_T];
-    const int nb = np / FW_T;
+    __shared__ __attribute__((aligned(16))) uint16_t At[T * T];
+    __shared__ __attribute__((aligned(16))) uint16_t Bt[T * T];
+    const int nb = np / T;
     int ti = blockIdx.y, tj = blockIdx.x;
     if (ti >= kb) ti++;
     if (tj >= kb) tj++;
     if (ti >= nb || tj >= nb) return;
     const int r = threadIdx.x / 16, c = threadIdx.x % 16;
-    fw_stage(D, np, ti, kb, At, true);
-    fw_stage(D, np, kb, tj, Bt, false);
+    fw_stage<T>(D, np, ti, kb, At, true);
+    fw_stage<T>(D, np, kb, tj, Bt, false);
     __syncthreads();
-    uint32_t acc[4][2];
-    fw_load_block(D, np, ti, tj, r, c, acc);
-    fw_tile_product(At, Bt, acc, r, c);
-    fw_store_block(D, np, ti, tj, r, c, acc);
+    uint32_t acc[T / 16][T / 32];
+    fw_load_block<T>(D, np, ti, tj, r, c, acc);
+    fw_tile_product<T>(At, Bt, acc, r, c);
+    fw_store_block<T>(D, np, ti, tj, r, c, acc);
 }
 
 // In-arc lists for the parent search, built once per graph: row v holds the keys

@@ -83,6 +83,11 @@ struct shd_route {
     std::vector<double> h_w;
     std::vector<uint16_t> h_ridx;
     std::vector<double> close;
+    // landmark rows (planner): the most central vertices' distances and tie-rule parent
+    // records computed on the host, uploaded as seed rows for the plan's roots
+    std::vector<int> lm_v;
+    std::vector<std::vector<double>> lm_d;
+    std::vector<std::vector<uint32_t>> lm_p;
     int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD
     // K4 (fw.hpp): u16 all-pairs table + dense u16 weights, Np x Np (Np = n rounded to 64)
     uint16_t* d_fwD = nullptr;
@@ -1049,6 +1054,7 @@ struct shd_route_plan {
     shd_route* c = nullptr;
     int world = 1, rank = 0, ns_all = 0;
     int seeded = 0, nroots = 0, nhelpers = 0, nslots = 0;
+    int nland = 0;                 // landmark seed rows after the kept rows' slots (flags preset)
     std::vector<int32_t> row_pos;  // caller-list position of each output row of this rank
     std::vector<int> lvl_off;      // jobs of launch k: [lvl_off[k], lvl_off[k + 1])
     KDJob* d_jobs = nullptr;
@@ -1112,6 +1118,47 @@ void ensure_close(shd_route* c) {
         for (int k = 0; k < L; k++) sum += D[k][v];
         c->close[v] = sum / L;
     }
+}
+
+// Landmark rows: the k most central vertices (closeness order), each row as the KD
+// kernel would compute it -- exact integer distances (u16) and the engine tie-rule parent
+// record of every vertex (largest w, then smallest parent over the tight in-arcs: an
+// undirected simple graph's in-arcs are its out-arcs) -- so that a row seeded from one is
+// bit-identical to a row seeded from a device row.  Host threads, once per context.
+void ensure_landmarks(shd_route* c, int k) {
+    if ((int)c->lm_v.size() >= k) return;
+    ensure_close(c);
+    const int n = c->n;
+    std::vector<int> ord(n);
+    std::iota(ord.begin(), ord.end(), 0);
+    std::partial_sort(ord.begin(), ord.begin() + k, ord.end(), [&](int a, int b) {
+        return c->close[a] != c->close[b] ? c->close[a] < c->close[b] : a < b;
+    });
+    c->lm_v.assign(ord.begin(), ord.begin() + k);
+    c->lm_d.assign(k, {});
+    c->lm_p.assign(k, {});
+    std::vector<std::thread> th;
+    for (int q = 0; q < k; q++)
+        th.emplace_back([c, q, n] {
+            const int L = c->lm_v[q];
+            host_dijkstra(c, L, c->lm_d[q]);
+            const std::vector<double>& d = c->lm_d[q];
+            std::vector<uint32_t>& P = c->lm_p[q];
+            P.assign(n, KD_NONE);
+            for (int v = 0; v < n; v++) {
+                if (v == L) { P[v] = KD_SRC_MARK; continue; }
+                if (!(d[v] < INFINITY)) continue;
+                int bu = -1, bw = -1, ba = -1;
+                for (int a = c->h_row[v]; a < c->h_row[v + 1]; a++) {
+                    const int y = c->h_col[a];
+                    const int w = (int)c->h_w[a];
+                    if (d[y] + c->h_w[a] != d[v]) continue;
+                    if (w > bw || (w == bw && y < bu)) { bw = w; bu = y; ba = a; }
+                }
+                if (ba >= 0) P[v] = (uint32_t)bu | ((uint32_t)c->h_ridx[ba] << 16) | ((uint32_t)bw << 24);
+            }
+        });
+    for (auto& t : th) t.join();
 }
 
 }  // namespace
@@ -1253,6 +1300,15 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // own record is the arc (x,u), tight whenever u keeps D0.
         bool two_hop = true;
         if (const char* e = getenv("SHD_ROUTE_SEED2HOP")) two_hop = atoi(e) != 0;
+        // The roots (the rows that would start unseeded) seed from host-computed landmark
+        // rows instead: D0 = d(s, L) + d_L(.) is consistent for any landmark L, and L's own
+        // record is the last arc (x, L) of a shortest s -> L path (tight whenever L keeps
+        // D0).  C3 roots are a ninth of the rows and cost ~3.4 seeded rows each unseeded.
+        int nland = c->multigraph ? 0 : std::min(16, n);
+        if (const char* e = getenv("SHD_ROUTE_LANDMARKS")) nland = c->multigraph ? 0 : std::max(0, std::min(atoi(e), n));
+        if (nland > 0) ensure_landmarks(c, nland);
+        std::vector<std::array<int, KD_SEEDS>> lmseed(nj);  // landmark index of seed k, or -1
+        for (auto& a : lmseed) a.fill(-1);
         std::vector<int> fl(n, -1);  // first job of a vertex, once its level is below the cap
         std::vector<std::array<int, KD_SEEDS>> srec(nj);
         struct Hop { double cost; int u, off; uint32_t rec; };
@@ -1263,6 +1319,29 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             int arcs[KD_SEEDS];
             const bool seedable = q++ >= nroot_min;
             int m = seedable ? best_seeds(p, fl, kseeds, arcs) : 0;
+            if (!seedable && nland > 0) {
+                // nearest landmarks by d(s, L) (undirected: d_L(s)), up to kseeds
+                std::vector<std::pair<double, int>> lc;
+                for (int l = 0; l < nland; l++)
+                    if (c->lm_d[l][s] < INFINITY && c->lm_d[l][s] < 65535.0) lc.push_back({c->lm_d[l][s], l});
+                std::sort(lc.begin(), lc.end());
+                int mk = 0;
+                for (const auto& pr : lc) {
+                    if (mk == kseeds) break;
+                    const int l = pr.second, L = c->lm_v[l];
+                    uint32_t rec = KD_SRC_MARK;
+                    if (L != s) {
+                        // the last arc (x, L) of the shortest s -> L path in L's tree
+                        int x = s;
+                        while ((int)(c->lm_p[l][x] & 0xFFFFu) != L) x = (int)(c->lm_p[l][x] & 0xFFFFu);
+                        const uint32_t px = c->lm_p[l][x];  // L | ridx(x,L) << 16 | w << 24
+                        rec = (uint32_t)x | (px & 0xFFFF0000u);
+                    }
+                    su[j][mk] = L; wr[j][mk] = (int)pr.first; srec[j][mk] = (int)rec; lmseed[j][mk] = l;
+                    mk++;
+                }
+                nsd[j] = mk;
+            }
             for (int k = 0; k < m; k++) {
                 const int a = arcs[k], u = c->h_col[a];
                 su[j][k] = u;
@@ -1302,16 +1381,35 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 lvl[j] = std::max(lvl[j], lvl[sj] + 1);
                 if (slot[sj] < 0) slot[sj] = P->nslots++;
             }
-            nsd[j] = m;
-            if (!m) P->nroots++;
+            if (seedable || nland == 0) nsd[j] = m;
+            if (!nsd[j]) P->nroots++;
             nlev = std::max(nlev, lvl[j] + 1);
             if (first[src[p]] == j && lvl[j] + 1 < depth) fl[src[p]] = p;
         }
         const long long rs = kd_row_stride(n);
-        P->store_bytes = (uint64_t)P->nslots * (uint64_t)rs * 6u;
-        bool ok = P->nslots > 0 &&
-                  hipMalloc((void**)&P->d_drow, sizeof(uint16_t) * (size_t)rs * P->nslots) == hipSuccess &&
-                  hipMalloc((void**)&P->d_prow, sizeof(uint32_t) * (size_t)rs * P->nslots) == hipSuccess;
+        bool uses_lm = false;
+        for (int j = 0; j < nj && !uses_lm; j++) uses_lm = nsd[j] > 0 && lmseed[j][0] >= 0;
+        P->nland = uses_lm ? nland : 0;
+        const int ntot = P->nslots + P->nland;
+        P->store_bytes = (uint64_t)ntot * (uint64_t)rs * 6u;
+        bool ok = ntot > 0 &&
+                  hipMalloc((void**)&P->d_drow, sizeof(uint16_t) * (size_t)rs * ntot) == hipSuccess &&
+                  hipMalloc((void**)&P->d_prow, sizeof(uint32_t) * (size_t)rs * ntot) == hipSuccess;
+        if (ok && P->nland) {
+            // landmark rows into the slots after the kept rows' (pads: unreached, no record)
+            std::vector<uint16_t> hd((size_t)rs * P->nland, 0xFFFFu);
+            std::vector<uint32_t> hp((size_t)rs * P->nland, KD_NONE);
+            for (int l = 0; l < P->nland; l++)
+                for (int v = 0; v < n; v++) {
+                    const double d = c->lm_d[l][v];
+                    hd[(size_t)l * rs + v] = d < 65535.0 ? (uint16_t)d : (uint16_t)0xFFFFu;
+                    hp[(size_t)l * rs + v] = c->lm_p[l][v];
+                }
+            ok = hipMemcpy(P->d_drow + (size_t)rs * P->nslots, hd.data(), sizeof(uint16_t) * hd.size(),
+                           hipMemcpyHostToDevice) == hipSuccess &&
+                 hipMemcpy(P->d_prow + (size_t)rs * P->nslots, hp.data(), sizeof(uint32_t) * hp.size(),
+                           hipMemcpyHostToDevice) == hipSuccess;
+        }
         if (ok) {
             std::vector<int> cnt(nlev + 1, 0);
             for (int j = 0; j < nj; j++) cnt[lvl[j] + 1]++;
@@ -1323,19 +1421,21 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             // earliest.  A row still follows all of its seeds in the queue (no deadlock),
             // but rows no longer wait at every level boundary for seeds just started.
             const int W = std::max(1, c->kd_slots);
-            double root_cost = 3.4, flag_at = 0.7;
+            double root_cost = 3.4, flag_at = 0.7, lm_cost = 2.0;  // (landmark-seeded roots)
+            if (const char* e = getenv("SHD_ROUTE_LMCOST")) lm_cost = std::max(0.1, atof(e));
             if (const char* e = getenv("SHD_ROUTE_ROOTCOST")) root_cost = std::max(0.1, atof(e));
             if (const char* e = getenv("SHD_ROUTE_FLAGAT")) flag_at = std::max(0.0, std::min(1.0, atof(e)));
             std::vector<std::vector<int>> dep(nj);
             std::vector<int> left(nj);
             for (int j = 0; j < nj; j++) {
-                left[j] = nsd[j];
-                for (int k = 0; k < nsd[j]; k++) dep[seedjob[j][k]].push_back(j);
+                left[j] = 0;
+                for (int k = 0; k < nsd[j]; k++)
+                    if (lmseed[j][k] < 0) { dep[seedjob[j][k]].push_back(j); left[j]++; }
             }
             std::vector<double> ready(nj, 0.0);
             typedef std::pair<double, int> DI;
             std::priority_queue<DI, std::vector<DI>, std::greater<DI>> cq, free_at;
-            for (int j = 0; j < nj; j++) if (!nsd[j]) cq.push({0.0, j});
+            for (int j = 0; j < nj; j++) if (!left[j]) cq.push({0.0, j});
             for (int w = 0; w < W; w++) free_at.push({0.0, w});
             std::vector<int> qorder;
             qorder.reserve(nj);
@@ -1343,7 +1443,8 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 const DI f = free_at.top(); free_at.pop();
                 const DI jr = cq.top(); cq.pop();
                 const int j = jr.second;
-                const double t = nsd[j] ? 1.0 : root_cost, start = std::max(f.first, jr.first);
+                const double t = !nsd[j] ? root_cost : lmseed[j][0] >= 0 ? lm_cost : 1.0;
+                const double start = std::max(f.first, jr.first);
                 free_at.push({start + t, f.second});
                 qorder.push_back(j);
                 for (int d : dep[j]) {
@@ -1365,19 +1466,20 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 std::memset(&J, 0, sizeof(J));
                 J.row = job_row[j]; J.s = src[job_pos[j]]; J.store = slot[j]; J.nseed = nsd[j];
                 for (int k = 0; k < nsd[j]; k++) {
-                    J.seed[k] = slot[seedjob[j][k]]; J.u[k] = su[j][k]; J.wr[k] = wr[j][k]; J.rec[k] = srec[j][k];
+                    J.seed[k] = lmseed[j][k] >= 0 ? P->nslots + lmseed[j][k] : slot[seedjob[j][k]];
+                    J.u[k] = su[j][k]; J.wr[k] = wr[j][k]; J.rec[k] = srec[j][k];
                 }
             }
             P->seeded = 1;
         } else {
             if (P->d_drow) (void)hipFree(P->d_drow);
             P->d_drow = nullptr;
-            P->nslots = 0; P->nroots = 0; P->store_bytes = 0;
+            P->nslots = 0; P->nroots = 0; P->nland = 0; P->store_bytes = 0;
         }
     }
     if (P->seeded) {
         if (hipMalloc((void**)&P->d_jobs, sizeof(KDJob) * jobs.size()) != hipSuccess ||
-            hipMalloc((void**)&P->d_next, sizeof(int) * (1 + (size_t)P->nslots)) != hipSuccess)
+            hipMalloc((void**)&P->d_next, sizeof(int) * (1 + (size_t)P->nslots + P->nland)) != hipSuccess)
             return SHD_ROUTE_ENOMEM;
         if (hipMemcpy(P->d_jobs, jobs.data(), sizeof(KDJob) * jobs.size(), hipMemcpyHostToDevice) != hipSuccess)
             return SHD_ROUTE_EDEVICE;
@@ -1433,6 +1535,8 @@ int shd_route_rows_planned_async(shd_route_t* c, const shd_route_plan_t* P, cons
     // one launch: jobs in level order from one queue; a seeded job waits for its seed's
     // ready flag (set once the kept row is complete, before that row's phase C)
     if (hipMemsetAsync(P->d_next, 0, sizeof(int) * (1 + (size_t)P->nslots), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    if (P->nland && hipMemsetD32Async((hipDeviceptr_t)(P->d_next + 1 + P->nslots), 1, (size_t)P->nland, st) != hipSuccess)
+        return SHD_ROUTE_EDEVICE;  // landmark rows: complete before the launch
     DevDelta k = kd_args(c);
     k.drow = P->d_drow; k.drow_out = P->d_drow; k.prow = P->d_prow; k.rstride = kd_row_stride(c->n);
     k.jobs = P->d_jobs;

@@ -2,6 +2,7 @@
 #include "common.hpp"
 
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <map>
 #include <memory>
@@ -1138,8 +1139,11 @@ void ensure_landmarks(shd_route* c, int k) {
     c->lm_d.assign(k, {});
     c->lm_p.assign(k, {});
     std::vector<std::thread> th;
-    for (int q = 0; q < k; q++)
-        th.emplace_back([c, q, n] {
+    std::atomic<int> next{0};
+    const int nth = std::max(1, std::min(k, 16));
+    for (int t = 0; t < nth; t++)
+        th.emplace_back([c, n, k, &next] {
+          for (int q = next++; q < k; q = next++) {
             const int L = c->lm_v[q];
             host_dijkstra(c, L, c->lm_d[q]);
             const std::vector<double>& d = c->lm_d[q];
@@ -1157,6 +1161,7 @@ void ensure_landmarks(shd_route* c, int k) {
                 }
                 if (ba >= 0) P[v] = (uint32_t)bu | ((uint32_t)c->h_ridx[ba] << 16) | ((uint32_t)bw << 24);
             }
+          }
         });
     for (auto& t : th) t.join();
 }
@@ -1304,7 +1309,10 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // rows instead: D0 = d(s, L) + d_L(.) is consistent for any landmark L, and L's own
         // record is the last arc (x, L) of a shortest s -> L path (tight whenever L keeps
         // D0).  C3 roots are a ninth of the rows and cost ~3.4 seeded rows each unseeded.
-        int nland = c->multigraph ? 0 : std::min(16, n);
+        // (C3, 1024 roots over 256-thread rows: 16/32/64/256 landmarks 2.90/2.89/2.80/2.76 ms;
+        // C4's 256 roots are 0.5% of its rows: 16 and 64 measure the same, and each landmark
+        // is a host Dijkstra of the plan (~40 ms at C4))
+        int nland = c->multigraph ? 0 : std::min(c->kd_block >= 1024 ? 16 : 64, n);
         if (const char* e = getenv("SHD_ROUTE_LANDMARKS")) nland = c->multigraph ? 0 : std::max(0, std::min(atoi(e), n));
         if (nland > 0) ensure_landmarks(c, nland);
         std::vector<std::array<int, KD_SEEDS>> lmseed(nj);  // landmark index of seed k, or -1

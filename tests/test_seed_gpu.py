@@ -5,8 +5,9 @@ row store, and settles the parents of the vertices that keep that distance from 
 parent records plus the tie events of the expansion.  Everything must stay bit-exact
 against the oracle (engine tie rule), including: many launches (deep seed forests),
 workgroups running many rows back to back (small grid), tie-event lists that overflow
-(the row reruns unseeded), directed graphs (plans fall back to plain rows), and the
-full C3/C4 tables against the committed golden row digests.
+(the row reruns unseeded), directed graphs (plans fall back to plain rows), rows seeded
+from host-computed landmark rows or two-hop rows, and the full C3/C4 tables against the
+committed golden row digests.
 """
 import hashlib
 import json
@@ -125,6 +126,36 @@ def test_full_table_planned_matches_golden(monkeypatch, cfg):
     assert np.array_equal(blk, blk.T)
     del d_lat, d_rel
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n,landmarks", [(20, None), (40, None), (300, "1"), (300, "64"), (300, "0")])
+def test_landmark_seeded_roots(oracle_mod, monkeypatch, n, landmarks):
+    """Full grid (every workgroup slot starts with a landmark-seeded row): graphs smaller
+    than the landmark set (every vertex a landmark: roots seeded by their own exact row),
+    one landmark, many, none; two-hop fills.  Bit-exact against the oracle."""
+    from shadow_amd import route
+    from shadow_amd.graph import internet_like
+    monkeypatch.setenv("SHD_ROUTE_KERNEL", "kd")
+    monkeypatch.delenv("SHD_ROUTE_KDGRID", raising=False)
+    monkeypatch.delenv("SHD_ROUTE_SEED", raising=False)
+    if landmarks is not None:
+        monkeypatch.setenv("SHD_ROUTE_LANDMARKS", landmarks)
+    g = internet_like(n, 2, seed=40 + n, name=f"ba{n}")
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 4
+    T = g.targets()
+    plan = eng.plan(T)
+    if landmarks != "0":
+        # every row is a first row here (the grid has more slots than there are rows): all
+        # seeded from landmark rows
+        assert plan.info["seeded"] == 1 and plan.info["roots"] == 0
+    else:
+        assert plan.info["seeded"] == 0  # all rows unseeded: no row store, plain rows
+    lat, rel, mn = _plan_rows(eng, plan, T)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(T[plan.positions], T, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(rel, orel)
+    assert np.array_equal(mn, olat.min(axis=1))
 
 
 def test_c3_writer_ring_no_stall(monkeypatch):

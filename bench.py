@@ -167,7 +167,7 @@ def timed(fn, reps, sync, barrier=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=25)  # C4: ~1.2 s timed
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"])

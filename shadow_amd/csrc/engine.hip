@@ -1202,13 +1202,15 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     // the best seeds of position p among the positions marked in `avail` (first[v]: the
     // available position of vertex v): neighbours of smaller rank by w(s,u) + closeness(u)
     std::vector<std::pair<double, int>> cand;
+    double alpha = 1.0;  // seed score w(s,u) + alpha * closeness(u)
+    if (const char* e = getenv("SHD_ROUTE_SEEDALPHA")) alpha = atof(e);
     auto best_seeds = [&](int p, const std::vector<int>& first, int k, int* arc_out) {
         const int s = src[p];
         cand.clear();
         for (int a = c->h_row[s]; a < c->h_row[s + 1]; a++) {
             const int u = c->h_col[a];
             if (u == s || first[u] < 0 || rk[u] >= rk[s]) continue;
-            cand.push_back({c->h_w[a] + c->close[u], a});
+            cand.push_back({c->h_w[a] + alpha * c->close[u], a});
         }
         std::sort(cand.begin(), cand.end(), [&](const std::pair<double, int>& x, const std::pair<double, int>& y) {
             return x.first != y.first ? x.first < y.first : c->h_col[x.second] < c->h_col[y.second];

@@ -142,13 +142,16 @@ int shd_route_min_reduce_async(shd_route_t* ctx, const double* d_vals, int64_t c
  * w(s,u) + d_u(v) are path lengths that already satisfy every arc, so only the vertices
  * that improve on them are expanded, and the rows come out bit-identical to unseeded
  * rows (same distances, same engine tie rule for parents, same source-first products).
- * The plan orders the rows by depth in the seed forest into one launch, where a row
- * waits for its seed row's ready flag, and keeps the seeding rows (u16 distances +
- * parent records per vertex) in a device row store.
- * Rows of a multi-GPU job: with world > 1 this rank's output rows are the contiguous
- * block rank of the caller's list (shd_route_plan_rows gives their positions).  Plans
- * need the KD kernel on an undirected integer-latency topology (else the plan falls
- * back to plain rows); SHD_ROUTE_SEED=0 in the environment disables seeding. */
+ * Up to three seeds per row; a row short of neighbour seeds takes rows two hops away,
+ * and the first rows of the launch take landmark rows (the most central vertices' rows,
+ * computed on the host when the plan is built).  The plan orders the rows into one
+ * launch, where a row waits for its seeds' ready flags, and keeps the seeding rows (u16
+ * distances + parent records per vertex) in a device row store.
+ * Rows of a multi-GPU job: with world > 1 this rank's output rows are whole subtrees of
+ * the seed forest (shd_route_plan_rows gives their positions in the caller's list), the
+ * forest's top rows recomputed on every rank as helper rows.  Plans need the KD kernel
+ * on an undirected integer-latency topology (else the plan falls back to plain rows);
+ * SHD_ROUTE_SEED=0 in the environment disables seeding. */
 typedef struct shd_route_plan shd_route_plan_t;
 
 typedef struct shd_route_plan_info {
@@ -156,7 +159,7 @@ typedef struct shd_route_plan_info {
     int32_t seeded;        /* 1 = seeded launches, 0 = plain rows */
     int32_t launches;      /* kernel launches per shd_route_rows_planned_async */
     int32_t levels;        /* depth of the seed forest (longest chain of seeded rows) */
-    int32_t roots;         /* rows computed from scratch */
+    int32_t roots;         /* rows computed from scratch (no neighbour, two-hop or landmark seed) */
     int32_t helpers;       /* rows computed only to seed others (no output) */
     int32_t stored_rows;   /* rows kept in the row store */
     int32_t world, rank;

@@ -1250,7 +1250,9 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // T = the rows whose subtree holds more than a quarter of a rank's share (the
         // forest's skeleton near its roots); every other row hangs in a subtree of at most
         // that size whose head's parent is in T (or which is a whole small tree)
-        const int cap = std::max(1, ns / (4 * world));
+        int capdiv = 4;
+        if (const char* e = getenv("SHD_ROUTE_TOPCAP")) capdiv = std::max(1, atoi(e));
+        const int cap = std::max(1, ns / (capdiv * world));
         std::vector<int> top, heads;
         for (int p : pos) {
             if (sub[p] > cap) top.push_back(p);

@@ -159,24 +159,27 @@ __global__ __launch_bounds__(256) void fw_diag_kernel(uint16_t* __restrict__ D, 
     // step k reads row k and column k, which step k leaves unchanged (D[k][k] = 0:
     // min(D[i][k], D[i][k] + 0) = D[i][k]), so its writes need no barrier before them: one
     // barrier per step (writes of step k before the reads of step k + 1)
+    // the thread's own block lives in registers across the steps; LDS carries its updates
+    // for the other threads' column-k / row-k reads
+    uint32_t x[R][H];
+#pragma unroll
+    for (int i = 0; i < R; i++) fw_ld<H>(L + (R * r + i) * T + R * c, x[i]);
     for (int k = 0; k < T; k++) {
         fw_us2 col[R];
 #pragma unroll
         for (int i = 0; i < R; i++) {
-            const unsigned short x = L[(R * r + i) * T + k];
-            col[i] = fw_us2{x, x};
+            const unsigned short y = L[(R * r + i) * T + k];
+            col[i] = fw_us2{y, y};
         }
         uint32_t rowk[H];
         fw_ld<H>(L + k * T + R * c, rowk);
 #pragma unroll
         for (int i = 0; i < R; i++) {
-            uint32_t x[H];
-            fw_ld<H>(L + (R * r + i) * T + R * c, x);
 #pragma unroll
             for (int h = 0; h < H; h++)
-                x[h] = fw_pkmin(x[h], __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(
-                                                                      col[i], __builtin_bit_cast(fw_us2, rowk[h]))));
-            fw_st<H>(L + (R * r + i) * T + R * c, x);
+                x[i][h] = fw_pkmin(x[i][h], __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(
+                                                                            col[i], __builtin_bit_cast(fw_us2, rowk[h]))));
+            fw_st<H>(L + (R * r + i) * T + R * c, x[i]);
         }
         __syncthreads();
     }
@@ -199,12 +202,12 @@ __global__ __launch_bounds__(256) void fw_panel_kernel(uint16_t* __restrict__ D,
     const int r = threadIdx.x / 16, c = threadIdx.x % 16;
     const bool rowp = blockIdx.y == 0;
     const int ti = rowp ? kb : b, tj = rowp ? b : kb;
+    uint32_t acc[T / 16][T / 32];
+    fw_load_block<T>(D, np, ti, tj, r, c, acc);
     // row panel: C = D* (x) C (A = pivot, B = the panel); column panel: C = C (x) D*
     fw_stage<T>(D, np, rowp ? kb : ti, rowp ? kb : tj, At, true);
     fw_stage<T>(D, np, rowp ? ti : kb, rowp ? tj : kb, Bt, false);
     __syncthreads();
-    uint32_t acc[T / 16][T / 32];
-    fw_load_block<T>(D, np, ti, tj, r, c, acc);
     fw_tile_product<T>(At, Bt, acc, r, c);
     fw_store_block<T>(D, np, ti, tj, r, c, acc);
 }
@@ -220,11 +223,12 @@ __global__ __launch_bounds__(256) void fw_rest_kernel(uint16_t* __restrict__ D, 
     if (tj >= kb) tj++;
     if (ti >= nb || tj >= nb) return;
     const int r = threadIdx.x / 16, c = threadIdx.x % 16;
+    // C's loads are issued first: their latency overlaps the panel staging and its barrier
+    uint32_t acc[T / 16][T / 32];
+    fw_load_block<T>(D, np, ti, tj, r, c, acc);
     fw_stage<T>(D, np, ti, kb, At, true);
     fw_stage<T>(D, np, kb, tj, Bt, false);
     __syncthreads();
-    uint32_t acc[T / 16][T / 32];
-    fw_load_block<T>(D, np, ti, tj, r, c, acc);
     fw_tile_product<T>(At, Bt, acc, r, c);
     fw_store_block<T>(D, np, ti, tj, r, c, acc);
 }

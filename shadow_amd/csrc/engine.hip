@@ -1642,7 +1642,8 @@ int shd_route_fw_table_async(shd_route_t* c, void* stream) {
     const unsigned blocks = (unsigned)(((size_t)np * np + 255) / 256);
     hipLaunchKernelGGL(fw_init_kernel, dim3(blocks), dim3(256), 0, st, c->d_W, c->n, np, c->d_fwD);
     for (int kb = 0; kb < nb; kb++) {
-        hipLaunchKernelGGL(fw_diag_kernel<FW_T>, dim3(1), dim3(256), 0, st, c->d_fwD, np, kb);
+        // pivot tiles after the first are closed inside the previous fw_rest launch
+        if (kb == 0) hipLaunchKernelGGL(fw_diag_kernel<FW_T>, dim3(1), dim3(256), 0, st, c->d_fwD, np, kb);
         if (nb > 1) {
             hipLaunchKernelGGL(fw_panel_kernel<FW_T>, dim3(nb - 1, 2), dim3(256), 0, st, c->d_fwD, np, kb);
             hipLaunchKernelGGL(fw_rest_kernel<FW_T>, dim3(nb - 1, nb - 1), dim3(256), 0, st, c->d_fwD, np, kb);

@@ -15,7 +15,8 @@
 // contraction, so MFMA does not apply.
 //
 //  fw_init     D[i][j] = w(i,j) (0 on the diagonal, 0xFFFF = no edge), padded to 64
-//  fw_diag     the pivot tile: 64 dependent steps in LDS (one workgroup)
+//  fw_diag     the first pivot tile: 64 dependent steps in LDS (one workgroup); every later
+//              pivot tile is closed by its own workgroup inside the previous fw_rest launch
 //  fw_panel    row / column panel tiles: D* (x) P and P (x) D* with the closed pivot
 //              tile D* -- one tropical product each, no dependent steps
 //  fw_rest     every other tile: C = min(C, colpanel (x) rowpanel)
@@ -148,22 +149,16 @@ __device__ inline void fw_stage(const uint16_t* D, int np, int ti, int tj, uint1
     }
 }
 
-// pivot tile kb: T dependent steps (D[i][j] = min(D[i][j], D[i][k] + D[k][j]))
+// Closing a pivot tile: T dependent steps D[i][j] = min(D[i][j], D[i][k] + D[k][j]) on the
+// thread blocks x (registers) with the tile mirrored in L (row-major, staged and synced).
+// Step k reads row k and column k, which step k leaves unchanged (D[k][k] = 0:
+// min(D[i][k], D[i][k] + 0) = D[i][k]), so its writes need no barrier before them: one
+// barrier per step (writes of step k before the reads of step k + 1).  The thread's own
+// block lives in registers across the steps; LDS carries its updates for the other
+// threads' column-k / row-k reads.
 template <int T>
-__global__ __launch_bounds__(256) void fw_diag_kernel(uint16_t* __restrict__ D, int np, int kb) {
+__device__ inline void fw_close(uint16_t* L, uint32_t (&x)[T / 16][T / 32], int r, int c) {
     constexpr int R = T / 16, H = R / 2;
-    __shared__ __attribute__((aligned(16))) uint16_t L[T * T];
-    const int r = threadIdx.x / 16, c = threadIdx.x % 16;
-    fw_stage<T>(D, np, kb, kb, L, false);
-    __syncthreads();
-    // step k reads row k and column k, which step k leaves unchanged (D[k][k] = 0:
-    // min(D[i][k], D[i][k] + 0) = D[i][k]), so its writes need no barrier before them: one
-    // barrier per step (writes of step k before the reads of step k + 1)
-    // the thread's own block lives in registers across the steps; LDS carries its updates
-    // for the other threads' column-k / row-k reads
-    uint32_t x[R][H];
-#pragma unroll
-    for (int i = 0; i < R; i++) fw_ld<H>(L + (R * r + i) * T + R * c, x[i]);
     for (int k = 0; k < T; k++) {
         fw_us2 col[R];
 #pragma unroll
@@ -183,11 +178,21 @@ __global__ __launch_bounds__(256) void fw_diag_kernel(uint16_t* __restrict__ D, 
         }
         __syncthreads();
     }
-    for (int q = threadIdx.x; q < T * T / 4; q += 256) {
-        const int row = q / (T / 4), c4 = (q % (T / 4)) * 4;
-        *reinterpret_cast<uint2*>(D + (long long)(kb * T + row) * np + kb * T + c4) =
-            *reinterpret_cast<const uint2*>(L + row * T + c4);
-    }
+}
+
+// pivot tile kb on its own (the first pivot; later pivots are closed inside fw_rest)
+template <int T>
+__global__ __launch_bounds__(256) void fw_diag_kernel(uint16_t* __restrict__ D, int np, int kb) {
+    constexpr int R = T / 16, H = R / 2;
+    __shared__ __attribute__((aligned(16))) uint16_t L[T * T];
+    const int r = threadIdx.x / 16, c = threadIdx.x % 16;
+    fw_stage<T>(D, np, kb, kb, L, false);
+    __syncthreads();
+    uint32_t x[R][H];
+#pragma unroll
+    for (int i = 0; i < R; i++) fw_ld<H>(L + (R * r + i) * T + R * c, x[i]);
+    fw_close<T>(L, x, r, c);
+    fw_store_block<T>(D, np, kb, kb, r, c, x);
 }
 
 // panels of pivot kb: blockIdx.y = 0 row panel (kb, b), 1 column panel (b, kb), b != kb
@@ -212,13 +217,22 @@ __global__ __launch_bounds__(256) void fw_panel_kernel(uint16_t* __restrict__ D,
     fw_store_block<T>(D, np, ti, tj, r, c, acc);
 }
 
-// every tile (i, j), i, j != kb: C = min(C, D[i][kb] (x) D[kb][j])
+// every tile (i, j), i, j != kb: C = min(C, D[i][kb] (x) D[kb][j]).  The workgroup of tile
+// (kb + 1, kb + 1) -- dispatched first -- then closes it as the next pivot tile while the
+// other tiles of this launch run, so the serial pivot steps leave the critical path
 template <int T>
 __global__ __launch_bounds__(256) void fw_rest_kernel(uint16_t* __restrict__ D, int np, int kb) {
+    constexpr int R = T / 16, H = R / 2;
     __shared__ __attribute__((aligned(16))) uint16_t At[T * T];
     __shared__ __attribute__((aligned(16))) uint16_t Bt[T * T];
     const int nb = np / T;
-    int ti = blockIdx.y, tj = blockIdx.x;
+    int by = blockIdx.y, bx = blockIdx.x;
+    // swap block (0, 0) with the next pivot's block (kb, kb) (tile (kb + 1, kb + 1))
+    if (kb + 1 < nb) {
+        if (bx == 0 && by == 0) bx = by = kb;
+        else if (bx == kb && by == kb) bx = by = 0;
+    }
+    int ti = by, tj = bx;
     if (ti >= kb) ti++;
     if (tj >= kb) tj++;
     if (ti >= nb || tj >= nb) return;
@@ -230,6 +244,13 @@ __global__ __launch_bounds__(256) void fw_rest_kernel(uint16_t* __restrict__ D, 
     fw_stage<T>(D, np, kb, tj, Bt, false);
     __syncthreads();
     fw_tile_product<T>(At, Bt, acc, r, c);
+    if (ti == kb + 1 && tj == kb + 1) {
+        __syncthreads();  // every thread's product is done with At
+#pragma unroll
+        for (int i = 0; i < R; i++) fw_st<H>(At + (R * r + i) * T + R * c, acc[i]);
+        __syncthreads();
+        fw_close<T>(At, acc, r, c);
+    }
     fw_store_block<T>(D, np, ti, tj, r, c, acc);
 }
 

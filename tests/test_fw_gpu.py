@@ -44,6 +44,19 @@ def test_fw_rows_bitexact(oracle_mod, name):
     assert np.array_equal(mn, olat.min(axis=1))
 
 
+def test_fw_rows_all_sources_sparse(oracle_mod):
+    """Every source of a sparse 700-vertex graph (11 pivot tiles, multi-hop paths through
+    each): the pivot tiles closed inside the rest launches give the oracle's full table."""
+    from shadow_amd import route
+    g = internet_like(700, 2, seed=23)
+    eng = route.RouteEngine(g)
+    T = np.arange(g.n, dtype=np.int32)
+    lat, rel, _ = _fw_rows(eng, T, T)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(T, T, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(rel, orel)
+
+
 @pytest.mark.parametrize("name", ["directed", "wide"])
 def test_fw_rows_parent_search(oracle_mod, name):
     """The parent search's two start rules: the threshold table (w <= 255) and the binary

@@ -28,12 +28,13 @@ def _fw_rows(eng, S, T):
     return lat.cpu().numpy(), rel.cpu().numpy(), mn.cpu().numpy()
 
 
-@pytest.mark.parametrize("name", ["k200", "ba300", "ties", "k130_odd"])
+@pytest.mark.parametrize("name", ["k200", "ba300", "ties", "k130_odd", "ba100"])
 def test_fw_rows_bitexact(oracle_mod, name):
     from shadow_amd import route
     from tests.golden import make_golden as mg
     g = {"k200": lambda: complete_graph(200, seed=5), "ba300": lambda: internet_like(300, 3, seed=17),
-         "ties": lambda: mg._ties(300, 33), "k130_odd": lambda: complete_graph(130, seed=6)}[name]()
+         "ties": lambda: mg._ties(300, 33), "k130_odd": lambda: complete_graph(130, seed=6),
+         "ba100": lambda: internet_like(100, 2, seed=9)}[name]()  # (2 pivot tiles)
     eng = route.RouteEngine(g)
     T = np.arange(g.n, dtype=np.int32)
     S = T[::3]

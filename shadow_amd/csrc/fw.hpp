@@ -334,10 +334,26 @@ __global__ __launch_bounds__(1024) void fw_parent_kernel(const uint16_t* __restr
                     }
                     k = lo;
                 }
-                for (; k < np; k++) {
+                // to a 4-arc boundary one arc at a time, then 4 arcs per trip (one 16-byte
+                // load, four independent LDS gathers, the first tight one in key order)
+                bool done = false;
+                for (; k < np && (k & 3); k++) {
                     const uint32_t e = lv[k];
-                    if (e == FW_END) break;
-                    if (drow[e & 0xFFFFu] + (0xFFFFu - (e >> 16)) == d) { best = e; break; }
+                    if (e == FW_END) { done = true; break; }
+                    if (drow[e & 0xFFFFu] + (0xFFFFu - (e >> 16)) == d) { best = e; done = true; break; }
+                }
+                for (; !done && k < np; k += 4) {  // (np: a multiple of 64)
+                    const uint4 e4 = *reinterpret_cast<const uint4*>(lv + k);
+                    const uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
+                    unsigned dd[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) dd[q] = drow[e[q] == FW_END ? 0u : (e[q] & 0xFFFFu)];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        if (done) continue;
+                        if (e[q] == FW_END) done = true;
+                        else if (dd[q] + (0xFFFFu - (e[q] >> 16)) == d) { best = e[q]; done = true; }
+                    }
                 }
             }
             key[(long long)i * np + v] = best;

@@ -261,6 +261,9 @@ __global__ __launch_bounds__(256) void fw_rest_kernel(uint16_t* __restrict__ D, 
 // per vertex: the column of the dense W, a bitonic sort of sp (power of two >= np) keys
 // in LDS, and a lower bound per threshold.
 constexpr int FW_X = 256;
+#ifndef FW_SCAN
+#define FW_SCAN 8  // in-arcs per parent-scan trip (4 or 8)
+#endif
 constexpr uint32_t FW_END = 0xFFFFFFFFu;
 __global__ __launch_bounds__(1024) void fw_inlist_kernel(const double* __restrict__ W, int n, int np, int sp,
                                                          uint32_t* __restrict__ inl, uint16_t* __restrict__ pos) {
@@ -337,19 +340,23 @@ __global__ __launch_bounds__(1024) void fw_parent_kernel(const uint16_t* __restr
                 // to a 4-arc boundary one arc at a time, then 4 arcs per trip (one 16-byte
                 // load, four independent LDS gathers, the first tight one in key order)
                 bool done = false;
-                for (; k < np && (k & 3); k++) {
+                for (; k < np && (k & (FW_SCAN - 1)); k++) {
                     const uint32_t e = lv[k];
                     if (e == FW_END) { done = true; break; }
                     if (drow[e & 0xFFFFu] + (0xFFFFu - (e >> 16)) == d) { best = e; done = true; break; }
                 }
-                for (; !done && k < np; k += 4) {  // (np: a multiple of 64)
-                    const uint4 e4 = *reinterpret_cast<const uint4*>(lv + k);
-                    const uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
-                    unsigned dd[4];
+                for (; !done && k < np; k += FW_SCAN) {  // (np: a multiple of 64)
+                    uint32_t e[FW_SCAN];
 #pragma unroll
-                    for (int q = 0; q < 4; q++) dd[q] = drow[e[q] == FW_END ? 0u : (e[q] & 0xFFFFu)];
+                    for (int q4 = 0; q4 < FW_SCAN; q4 += 4) {
+                        const uint4 e4 = *reinterpret_cast<const uint4*>(lv + k + q4);
+                        e[q4] = e4.x; e[q4 + 1] = e4.y; e[q4 + 2] = e4.z; e[q4 + 3] = e4.w;
+                    }
+                    unsigned dd[FW_SCAN];
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
+                    for (int q = 0; q < FW_SCAN; q++) dd[q] = drow[e[q] == FW_END ? 0u : (e[q] & 0xFFFFu)];
+#pragma unroll
+                    for (int q = 0; q < FW_SCAN; q++) {
                         if (done) continue;
                         if (e[q] == FW_END) done = true;
                         else if (dd[q] + (0xFFFFu - (e[q] >> 16)) == d) { best = e[q]; done = true; }

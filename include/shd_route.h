@@ -194,6 +194,22 @@ int shd_route_rows_planned_async(shd_route_t* ctx, const shd_route_plan_t* plan,
  * larger request is SHD_ROUTE_ENOMEM (shard it over more devices). */
 int shd_route_fill_triangle(shd_route_t* ctx, const int32_t* A, int32_t na, int32_t world, int32_t rank,
                             uint32_t flags, double* lr_out, double* min_out, double* seconds_out);
+/* ---- multi-GPU table assembly payload (no reference equivalent: Shadow 1.14 is one
+ * process, master.c:414-416).  The Path cache needs each unordered pair once
+ * (topology.c:1307-1336: the first writer stores both directions), so the rows a rank
+ * sends to the others are their upper triangles: row r of d_lat / d_rel (row stride ld,
+ * na targets = the sorted attached list) is the row of attached position d_pos[r] and
+ * keeps the targets j >= d_pos[r], packed at element offset d_off[r] - d_off[0] of
+ * d_out_lat / d_out_rel (d_off: int64 per row, the caller's prefix sums of na - pos).
+ * With SHD_ROUTE_PAYLOAD_LAT16 latencies go out as u16 (exact: integer latencies whose
+ * shortest paths are below 65535 ms, proven at create; NaN -> 0xFFFF; else
+ * SHD_ROUTE_EUNSUPPORTED), otherwise as f64; rel always as f64.  C4 over 8 GPUs: 10 B
+ * per pair of the triangle instead of 16 B per pair of the square (0.31x the bytes). */
+#define SHD_ROUTE_PAYLOAD_LAT16 0x1u
+int shd_route_tri_payload_async(shd_route_t* ctx, const double* d_lat, const double* d_rel, int64_t ld,
+                                const int32_t* d_pos, const int64_t* d_off, int32_t nrows, int32_t na, uint32_t flags,
+                                void* d_out_lat, double* d_out_rel, void* stream);
+
 void* shd_route_host_alloc(size_t bytes);  /* pinned host memory (NULL on failure) */
 void shd_route_host_free(void* p);
 

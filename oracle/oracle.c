@@ -702,6 +702,78 @@ double orc_bench_parallel(const orc_graph* g, const int32_t* src, int32_t ns,
     return dt;
 }
 
+/* C5 CPU baseline: the reference's fill of a complete graph, every
+ * pair by _topology_lookupDirectPath (topology.c:1877-1927: get_eid + factor products),
+ * rows spread over `threads` OpenMP threads, each row written to a per-thread buffer
+ * as the cache store would. */
+double orc_bench_direct(const orc_graph* g, const int32_t* A, int32_t na, int32_t threads,
+                        double* checksum, int32_t* threads_used) {
+    int32_t used = 1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#endif
+    double sum = 0;
+    double t0 = now_s();
+#pragma omp parallel reduction(+ : sum)
+    {
+#ifdef _OPENMP
+#pragma omp single
+        used = omp_get_num_threads();
+#endif
+        double* row = malloc(sizeof(double) * 2 * (size_t)na);
+#pragma omp for schedule(dynamic, 4)
+        for (int32_t i = 0; i < na; i++) {
+            for (int32_t j = 0; j < na; j++) {
+                double L = -1, R = 0;
+                orc_direct(g, A[i], A[j], &L, &R);
+                row[2 * j] = L; row[2 * j + 1] = R;
+            }
+            sum += row[2 * (i % na)] + row[2 * (na - 1) + 1];
+        }
+        free(row);
+    }
+    double dt = now_s() - t0;
+    if (checksum) *checksum = sum;
+    if (threads_used) *threads_used = used;
+    return dt;
+}
+
+/* C5 CPU baseline for K4: `nk` k-phases (k0 .. k0+nk-1) of f64 Floyd-Warshall over the
+ * n x n matrix d, rows of each phase spread over `threads` OpenMP threads (the caller
+ * extrapolates x n / nk to the whole table). */
+double orc_bench_fw_phases(int32_t n, double* d, int32_t k0, int32_t nk, int32_t threads,
+                           int32_t* threads_used) {
+    int32_t used = 1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#endif
+    double t0 = now_s();
+    for (int32_t k = k0; k < k0 + nk && k < n; k++) {
+#pragma omp parallel
+        {
+#ifdef _OPENMP
+#pragma omp single
+            used = omp_get_num_threads();
+#endif
+            const double* dk = d + (int64_t)k * n;
+#pragma omp for schedule(static)
+            for (int32_t i = 0; i < n; i++) {
+                if (i == k) continue;
+                double* di = d + (int64_t)i * n;
+                double dik = di[k];
+                if (isinf(dik)) continue;
+                for (int32_t j = 0; j < n; j++) {
+                    double c = dik + dk[j];
+                    di[j] = c < di[j] ? c : di[j];
+                }
+            }
+        }
+    }
+    double dt = now_s() - t0;
+    if (threads_used) *threads_used = used;
+    return dt;
+}
+
 void orc_floyd_warshall(int32_t n, double* d) {
     for (int32_t k = 0; k < n; k++)
         for (int32_t i = 0; i < n; i++) {

@@ -93,6 +93,13 @@ double orc_bench_faithful(const orc_graph* g, const int32_t* src, int32_t ns,
 double orc_bench_parallel(const orc_graph* g, const int32_t* src, int32_t ns,
                           const int32_t* tgt, int32_t nt, int32_t threads,
                           double* checksum, int32_t* threads_used);
+/* C5 (complete graph): the direct fill of every pair of A (topology.c:1877-1927), rows
+ * over OpenMP threads; and nk k-phases of f64 Floyd-Warshall from k0 over n x n d
+ * (extrapolate x n/nk).  Both return elapsed seconds. */
+double orc_bench_direct(const orc_graph* g, const int32_t* A, int32_t na, int32_t threads,
+                        double* checksum, int32_t* threads_used);
+double orc_bench_fw_phases(int32_t n, double* d, int32_t k0, int32_t nk, int32_t threads,
+                           int32_t* threads_used);
 
 /* Blocked-free reference Floyd-Warshall over dense n x n (for K4 parity),
  * d is n*n row-major with +inf for no edge; in-place. */

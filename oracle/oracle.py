@@ -65,6 +65,12 @@ def lib():
         L.orc_bench_parallel.argtypes = [P, i32p, C.c_int32, i32p, C.c_int32, C.c_int32,
                                          C.POINTER(C.c_double), C.POINTER(C.c_int32)]
         L.orc_floyd_warshall.argtypes = [C.c_int32, f64p]
+        L.orc_bench_direct.restype = C.c_double
+        L.orc_bench_direct.argtypes = [P, i32p, C.c_int32, C.c_int32, C.POINTER(C.c_double),
+                                       C.POINTER(C.c_int32)]
+        L.orc_bench_fw_phases.restype = C.c_double
+        L.orc_bench_fw_phases.argtypes = [C.c_int32, f64p, C.c_int32, C.c_int32, C.c_int32,
+                                          C.POINTER(C.c_int32)]
         _lib = L
     return _lib
 
@@ -165,6 +171,19 @@ class OracleGraph:
         cs = C.c_double(); used = C.c_int32()
         dt = lib().orc_bench_parallel(self.h, s, len(s), t, len(t), int(threads), C.byref(cs), C.byref(used))
         return dt, cs.value, used.value
+
+    def bench_direct(self, attached, threads=0):
+        a = np.ascontiguousarray(attached, np.int32)
+        cs = C.c_double(); used = C.c_int32()
+        dt = lib().orc_bench_direct(self.h, a, len(a), int(threads), C.byref(cs), C.byref(used))
+        return dt, used.value
+
+
+def bench_fw_phases(d: np.ndarray, k0: int, nk: int, threads: int = 0):
+    """nk k-phases of f64 Floyd-Warshall over d (in place); returns (seconds, threads)."""
+    used = C.c_int32()
+    dt = lib().orc_bench_fw_phases(d.shape[0], d, int(k0), int(nk), int(threads), C.byref(used))
+    return dt, used.value
 
 
 def runahead_ns(min_latency: float) -> int:

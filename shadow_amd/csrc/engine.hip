@@ -966,8 +966,10 @@ extern "C" {
 
 int shd_route_rows(shd_route_t* c, const int32_t* src, int32_t ns, const int32_t* tgt, int32_t nt,
                    uint32_t flags, double* lat_out, double* rel_out, double* row_min_out) {
-    // many KD rows: one seeded plan over all of them when the whole table fits the device
-    if (c && c->sel == 4 && c->kd_fused && ns >= 2 && nt >= 1 && src && tgt &&
+    // many KD rows (at least one per resident workgroup slot, so the plan's landmark rows,
+    // row store and table pay off): one seeded plan over all of them when the whole table
+    // fits the device; small batches and any device allocation failure take the chunked rows
+    if (c && c->sel == 4 && c->kd_fused && ns >= 2 && ns >= c->kd_slots && nt >= 1 && src && tgt &&
         !((flags & SHD_ROUTE_DISPATCH) && (c->complete || c->prefer_direct))) {
         const int rc = planned_host_rows(c, src, ns, tgt, nt, flags, lat_out, rel_out, row_min_out);
         if (rc != SHD_ROUTE_EUNSUPPORTED) return rc;
@@ -1072,29 +1074,65 @@ struct shd_route_plan {
 
 namespace {
 
-// Dijkstra over the host out-CSR (all distances from `src`)
-void host_dijkstra(const shd_route* c, int src, std::vector<double>& d) {
-    const int n = c->n;
-    d.assign(n, INFINITY);
-    std::vector<std::pair<double, int>> h;
-    auto cmp = [](const std::pair<double, int>& a, const std::pair<double, int>& b) { return a.first > b.first; };
-    d[src] = 0;
-    h.push_back({0.0, src});
-    while (!h.empty()) {
-        std::pop_heap(h.begin(), h.end(), cmp);
-        auto [du, u] = h.back();
-        h.pop_back();
-        if (du > d[u]) continue;
-        for (int a = c->h_row[u]; a < c->h_row[u + 1]; a++) {
-            const double nd = du + c->h_w[a];
-            if (nd < d[c->h_col[a]]) { d[c->h_col[a]] = nd; h.push_back({nd, c->h_col[a]}); std::push_heap(h.begin(), h.end(), cmp); }
+// Exact rows of `verts` on the device for the planner: one unplanned KD launch whose jobs
+// write no output row (row -1) but keep their row in store slot k, the format seeded rows
+// read (u16 distances, 0xFFFF = unreached, and the engine tie-rule parent record
+// `parent | ridx << 16 | w << 24` of every vertex).  Copied back into d_out / p_out
+// (p_out nullable).  Blocks: the planner runs once per context, before any planned launch.
+int device_store_rows(shd_route* c, const std::vector<int>& verts, std::vector<std::vector<double>>& d_out,
+                      std::vector<std::vector<uint32_t>>* p_out) {
+    const int k = (int)verts.size(), n = c->n;
+    if (k == 0) return SHD_ROUTE_OK;
+    const long long rs = kd_row_stride(n);
+    std::vector<KDJob> jobs(k);
+    for (int q = 0; q < k; q++) {
+        std::memset(&jobs[q], 0, sizeof(KDJob));
+        jobs[q].row = -1; jobs[q].s = verts[q]; jobs[q].store = q; jobs[q].nseed = 0;
+    }
+    DevBuf dj, dd, dp, dn;
+    if (dj.alloc(sizeof(KDJob) * k) || dd.alloc(sizeof(uint16_t) * (size_t)rs * k) ||
+        dp.alloc(sizeof(uint32_t) * (size_t)rs * k) || dn.alloc(sizeof(int) * (1 + (size_t)k)))
+        return SHD_ROUTE_ENOMEM;
+    // the context's scratch is shared with its rows launches: none may be in flight
+    if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
+    int rc = take_err(c);
+    if (rc) return rc;
+    if (hipMemcpy(dj.p, jobs.data(), sizeof(KDJob) * k, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(dn.p, 0, sizeof(int) * (1 + (size_t)k)) != hipSuccess)
+        return SHD_ROUTE_EDEVICE;
+    DevDelta g = kd_args(c);
+    g.jobs = (const KDJob*)dj.p;
+    g.drow = (const uint16_t*)dd.p; g.drow_out = (uint16_t*)dd.p; g.prow = (uint32_t*)dp.p; g.rstride = rs;
+    g.done = (int*)dn.p + 1;
+    if ((rc = kd_launch(c, g, (int*)dn.p, nullptr, k, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr)))
+        return rc;
+    if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
+    if ((rc = take_err(c))) return rc;
+    std::vector<uint16_t> hd((size_t)rs * k);
+    if (hipMemcpy(hd.data(), dd.p, sizeof(uint16_t) * hd.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        return SHD_ROUTE_EDEVICE;
+    d_out.assign(k, {});
+    for (int q = 0; q < k; q++) {
+        d_out[q].resize(n);
+        for (int v = 0; v < n; v++) {
+            const uint16_t x = hd[(size_t)q * rs + v];
+            d_out[q][v] = x == 0xFFFFu ? INFINITY : (double)x;
         }
     }
+    if (p_out) {
+        std::vector<uint32_t> hp((size_t)rs * k);
+        if (hipMemcpy(hp.data(), dp.p, sizeof(uint32_t) * hp.size(), hipMemcpyDeviceToHost) != hipSuccess)
+            return SHD_ROUTE_EDEVICE;
+        p_out->assign(k, {});
+        for (int q = 0; q < k; q++) (*p_out)[q].assign(hp.begin() + (size_t)q * rs, hp.begin() + (size_t)q * rs + n);
+    }
+    return SHD_ROUTE_OK;
 }
 
-// closeness estimate: mean distance from 16 pseudo-random landmarks (deterministic)
-void ensure_close(shd_route* c) {
-    if (!c->close.empty()) return;
+// closeness estimate: mean distance from 16 pseudo-random landmarks (deterministic), their
+// rows computed on the device
+int ensure_close(shd_route* c) {
+    if (!c->close.empty()) return SHD_ROUTE_OK;
     const int n = c->n, L = std::min(n, 16);
     std::vector<int> lm;
     uint64_t x = 0x243F6A8885A308D3ull;
@@ -1107,63 +1145,40 @@ void ensure_close(shd_route* c) {
         const int v = (int)(z % (uint64_t)n);
         if (std::find(lm.begin(), lm.end(), v) == lm.end()) lm.push_back(v);
     }
-    std::vector<std::vector<double>> D(L);
-    {
-        std::vector<std::thread> th;
-        for (int k = 0; k < L; k++) th.emplace_back([&, k] { host_dijkstra(c, lm[k], D[k]); });
-        for (auto& t : th) t.join();
-    }
+    std::vector<std::vector<double>> D;
+    const int rc = device_store_rows(c, lm, D, nullptr);
+    if (rc) return rc;
     c->close.assign(n, 0.0);
     for (int v = 0; v < n; v++) {
         double sum = 0;
         for (int k = 0; k < L; k++) sum += D[k][v];
         c->close[v] = sum / L;
     }
+    return SHD_ROUTE_OK;
 }
 
-// Landmark rows: the k most central vertices (closeness order), each row as the KD
-// kernel would compute it -- exact integer distances (u16) and the engine tie-rule parent
-// record of every vertex (largest w, then smallest parent over the tight in-arcs: an
-// undirected simple graph's in-arcs are its out-arcs) -- so that a row seeded from one is
-// bit-identical to a row seeded from a device row.  Host threads, once per context.
-void ensure_landmarks(shd_route* c, int k) {
-    if ((int)c->lm_v.size() >= k) return;
-    ensure_close(c);
+// Landmark rows: the k most central vertices (closeness order), each row exactly as the
+// KD kernel computes it -- exact integer distances (u16) and the engine tie-rule parent
+// record of every vertex -- so that a row seeded from one is bit-identical to a row seeded
+// from any other device row.  One device launch, once per context.
+int ensure_landmarks(shd_route* c, int k) {
+    if ((int)c->lm_v.size() >= k) return SHD_ROUTE_OK;
+    int rc = ensure_close(c);
+    if (rc) return rc;
     const int n = c->n;
     std::vector<int> ord(n);
     std::iota(ord.begin(), ord.end(), 0);
     std::partial_sort(ord.begin(), ord.begin() + k, ord.end(), [&](int a, int b) {
         return c->close[a] != c->close[b] ? c->close[a] < c->close[b] : a < b;
     });
-    c->lm_v.assign(ord.begin(), ord.begin() + k);
-    c->lm_d.assign(k, {});
-    c->lm_p.assign(k, {});
-    std::vector<std::thread> th;
-    std::atomic<int> next{0};
-    const int nth = std::max(1, std::min(k, 16));
-    for (int t = 0; t < nth; t++)
-        th.emplace_back([c, n, k, &next] {
-          for (int q = next++; q < k; q = next++) {
-            const int L = c->lm_v[q];
-            host_dijkstra(c, L, c->lm_d[q]);
-            const std::vector<double>& d = c->lm_d[q];
-            std::vector<uint32_t>& P = c->lm_p[q];
-            P.assign(n, KD_NONE);
-            for (int v = 0; v < n; v++) {
-                if (v == L) { P[v] = KD_SRC_MARK; continue; }
-                if (!(d[v] < INFINITY)) continue;
-                int bu = -1, bw = -1, ba = -1;
-                for (int a = c->h_row[v]; a < c->h_row[v + 1]; a++) {
-                    const int y = c->h_col[a];
-                    const int w = (int)c->h_w[a];
-                    if (d[y] + c->h_w[a] != d[v]) continue;
-                    if (w > bw || (w == bw && y < bu)) { bw = w; bu = y; ba = a; }
-                }
-                if (ba >= 0) P[v] = (uint32_t)bu | ((uint32_t)c->h_ridx[ba] << 16) | ((uint32_t)bw << 24);
-            }
-          }
-        });
-    for (auto& t : th) t.join();
+    std::vector<int> lv(ord.begin(), ord.begin() + k);
+    std::vector<std::vector<double>> D;
+    std::vector<std::vector<uint32_t>> Pr;
+    if ((rc = device_store_rows(c, lv, D, &Pr))) return rc;
+    c->lm_v = lv;
+    c->lm_d = std::move(D);
+    c->lm_p = std::move(Pr);
+    return SHD_ROUTE_OK;
 }
 
 }  // namespace
@@ -1178,6 +1193,9 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     for (int p = 0; p < ns; p++) if (src[p] < 0 || src[p] >= c->n) return SHD_ROUTE_EINVAL;
     auto P = std::make_unique<shd_route_plan>();
     P->c = c; P->world = world; P->rank = rank; P->ns_all = ns;
+    const auto t_start = std::chrono::steady_clock::now();
+    double t_close = 0, t_land = 0, t_seeds = 0, t_store = 0, t_sched = 0;  // SHD_ROUTE_PLAN_DEBUG stage times
+    auto since = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
     const int n = c->n;
     const char* env = getenv("SHD_ROUTE_SEED");
     const bool want = (!env || atoi(env) != 0) && c->sel == 4 && c->kd_fused && !c->complete && !c->prefer_direct &&
@@ -1185,7 +1203,9 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     // closeness rank of every vertex: a row may only be seeded by rows of smaller rank
     std::vector<int> rk;
     if (want) {
-        ensure_close(c);
+        const int rc = ensure_close(c);
+        if (rc) return rc;
+        t_close = since();
         std::vector<int> ord(n);
         rk.resize(n);
         std::iota(ord.begin(), ord.end(), 0);
@@ -1318,7 +1338,12 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // is a host Dijkstra of the plan (~40 ms at C4))
         int nland = c->multigraph ? 0 : std::min(c->kd_block >= 1024 ? 16 : 64, n);
         if (const char* e = getenv("SHD_ROUTE_LANDMARKS")) nland = c->multigraph ? 0 : std::max(0, std::min(atoi(e), n));
-        if (nland > 0) ensure_landmarks(c, nland);
+        if (nland > 0) {
+            const double t0 = since();
+            const int rc = ensure_landmarks(c, nland);
+            if (rc) return rc;
+            t_land = since() - t0;
+        }
         std::vector<std::array<int, KD_SEEDS>> lmseed(nj);  // landmark index of seed k, or -1
         for (auto& a : lmseed) a.fill(-1);
         std::vector<int> fl(n, -1);  // first job of a vertex, once its level is below the cap
@@ -1398,6 +1423,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             nlev = std::max(nlev, lvl[j] + 1);
             if (first[src[p]] == j && lvl[j] + 1 < depth) fl[src[p]] = p;
         }
+        t_seeds = since();
         const long long rs = kd_row_stride(n);
         bool uses_lm = false;
         for (int j = 0; j < nj && !uses_lm; j++) uses_lm = nsd[j] > 0 && lmseed[j][0] >= 0;
@@ -1422,6 +1448,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                  hipMemcpy(P->d_prow + (size_t)rs * P->nslots, hp.data(), sizeof(uint32_t) * hp.size(),
                            hipMemcpyHostToDevice) == hipSuccess;
         }
+        t_store = since();
         if (ok) {
             std::vector<int> cnt(nlev + 1, 0);
             for (int j = 0; j < nj; j++) cnt[lvl[j] + 1]++;
@@ -1464,12 +1491,14 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                     if (--left[d] == 0) cq.push({ready[d], d});
                 }
             }
+            t_sched = since();
             if (getenv("SHD_ROUTE_PLAN_DEBUG")) {
                 int hist[KD_SEEDS + 1] = {0};
                 for (int j = 0; j < nj; j++) hist[nsd[j]]++;
                 fprintf(stderr, "plan world %d rank %d: jobs %d levels %d seeds:", world, rank, nj, nlev);
                 for (int k = 0; k <= KD_SEEDS; k++) fprintf(stderr, " %d:%d", k, hist[k]);
-                fprintf(stderr, "\n");
+                fprintf(stderr, "  closeness rows %.2f ms, landmark rows %.2f ms, seeds done %.2f, store %.2f, schedule %.2f ms\n",
+                        1e3 * t_close, 1e3 * t_land, 1e3 * t_seeds, 1e3 * t_store, 1e3 * t_sched);
             }
             jobs.resize(nj);
             int qi = 0;
@@ -1505,6 +1534,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             return SHD_ROUTE_EDEVICE;
         P->nroots = nr;
     }
+    if (getenv("SHD_ROUTE_PLAN_DEBUG")) fprintf(stderr, "  plan total %.2f ms\n", 1e3 * since());
     *out = P.release();
     return SHD_ROUTE_OK;
 }
@@ -1570,13 +1600,13 @@ int planned_host_rows(shd_route* c, const int32_t* src, int32_t ns, const int32_
     if (hipMemGetInfo(&fr, &tot) != hipSuccess || 2 * table + ((size_t)ns << 20) > fr / 2) return SHD_ROUTE_EUNSUPPORTED;
     shd_route_plan_t* P = nullptr;
     int rc = shd_route_plan_create(c, src, ns, 1, 0, &P);
+    if (rc == SHD_ROUTE_ENOMEM) return SHD_ROUTE_EUNSUPPORTED;  // the chunked rows need far less
     if (rc) return rc;
     std::unique_ptr<shd_route_plan, void (*)(shd_route_plan*)> guard(P, shd_route_plan_destroy);
     if (!P->seeded) return SHD_ROUTE_EUNSUPPORTED;
     DevBuf dtgt, dlat, drel, dmin;
-    if ((rc = dtgt.alloc(sizeof(int32_t) * nt)) || (rc = dlat.alloc(table)) || (rc = drel.alloc(table)) ||
-        (rc = dmin.alloc(sizeof(double) * ns)))
-        return rc;
+    if (dtgt.alloc(sizeof(int32_t) * nt) || dlat.alloc(table) || drel.alloc(table) || dmin.alloc(sizeof(double) * ns))
+        return SHD_ROUTE_EUNSUPPORTED;
     if (hipMemcpy(dtgt.p, tgt, sizeof(int32_t) * nt, hipMemcpyHostToDevice) != hipSuccess) return SHD_ROUTE_EDEVICE;
     rc = shd_route_rows_planned_async(c, P, (const int32_t*)dtgt.p, nt, nt, flags, (double*)dlat.p, (double*)drel.p,
                                       (double*)dmin.p, nullptr);
@@ -1597,36 +1627,52 @@ int planned_host_rows(shd_route* c, const int32_t* src, int32_t ns, const int32_
 namespace {
 constexpr int kFwMaxN = 12000;  // fw_rows keeps rel f64 + order i32 per vertex in LDS
 
-int fw_prepare(shd_route* c) {
+// Builds the K4 state once per context: eligibility first (nothing is allocated for an
+// ineligible graph, so every call answers EUNSUPPORTED), then the buffers into locals,
+// published in the context only when every step has succeeded; the in-list build is
+// enqueued on the caller's stream, ahead of the table launches that follow it there.
+int fw_prepare(shd_route* c, hipStream_t st) {
     if (c->d_fwD) return SHD_ROUTE_OK;
     if (!c->integer_w || c->multigraph || c->n > kFwMaxN || c->k32_bound <= 0 || c->k32_bound >= 0xFFFF)
         return SHD_ROUTE_EUNSUPPORTED;
-    int rc = ensure_dense(c);
-    if (rc) return rc;
-    const int np = (c->n + FW_T - 1) / FW_T * FW_T;
-    const size_t cells = (size_t)np * np;
-    if (hipMalloc((void**)&c->d_fwD, 2 * cells) != hipSuccess) return SHD_ROUTE_ENOMEM;
-    c->allocs.push_back(c->d_fwD);
-    if (hipMalloc((void**)&c->d_fwinl, 4 * cells) != hipSuccess) return SHD_ROUTE_ENOMEM;
-    c->allocs.push_back(c->d_fwinl);
-    if (hipMalloc((void**)&c->d_fwpos, sizeof(uint16_t) * FW_X * (size_t)c->n) != hipSuccess) return SHD_ROUTE_ENOMEM;
-    c->allocs.push_back(c->d_fwpos);
-    c->fw_np = np;
     const size_t lds = a16(sizeof(double) * c->n) + a16(sizeof(int) * c->n) + a16(sizeof(int) * (c->k32_bound + 2));
     if (lds > kLdsBudget) return SHD_ROUTE_EUNSUPPORTED;
-    rc = hip_check(hipFuncSetAttribute((const void*)fw_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    if (rc) return rc;
+    const int np = (c->n + FW_T - 1) / FW_T * FW_T;
     int sp = 1;
     while (sp < np) sp <<= 1;
-    rc = hip_check(hipFuncSetAttribute((const void*)fw_inlist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)(4 * sp)));
+    if ((size_t)4 * sp > kLdsBudget) return SHD_ROUTE_EUNSUPPORTED;
+    int rc = ensure_dense(c);
     if (rc) return rc;
-    rc = hip_check(hipFuncSetAttribute((const void*)fw_parent_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)(2 * np)));
-    if (rc) return rc;
-    hipLaunchKernelGGL(fw_inlist_kernel, dim3(c->n), dim3(1024), 4 * sp, nullptr, c->d_W, c->n, np, sp, c->d_fwinl,
-                       c->d_fwpos);
-    return hip_check(hipGetLastError());
+    if ((rc = hip_check(hipFuncSetAttribute((const void*)fw_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)lds))) ||
+        (rc = hip_check(hipFuncSetAttribute((const void*)fw_inlist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)(4 * sp)))) ||
+        (rc = hip_check(hipFuncSetAttribute((const void*)fw_parent_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)(2 * np)))))
+        return rc;
+    const size_t cells = (size_t)np * np;
+    uint16_t* D = nullptr;
+    uint32_t* inl = nullptr;
+    uint16_t* pos = nullptr;
+    auto undo = [&](int code) {
+        if (D) (void)hipFree(D);
+        if (inl) (void)hipFree(inl);
+        if (pos) (void)hipFree(pos);
+        return code;
+    };
+    if (hipMalloc((void**)&D, 2 * cells) != hipSuccess || hipMalloc((void**)&inl, 4 * cells) != hipSuccess ||
+        hipMalloc((void**)&pos, sizeof(uint16_t) * FW_X * (size_t)c->n) != hipSuccess)
+        return undo(SHD_ROUTE_ENOMEM);
+    hipLaunchKernelGGL(fw_inlist_kernel, dim3(c->n), dim3(1024), 4 * sp, st, c->d_W, c->n, np, sp, inl, pos);
+    if ((rc = hip_check(hipGetLastError()))) return undo(rc);
+    c->d_fwD = D;
+    c->d_fwinl = inl;
+    c->d_fwpos = pos;
+    c->allocs.push_back(D);
+    c->allocs.push_back(inl);
+    c->allocs.push_back(pos);
+    c->fw_np = np;
+    return SHD_ROUTE_OK;
 }
 }  // namespace
 
@@ -1635,9 +1681,9 @@ extern "C" {
 int shd_route_fw_table_async(shd_route_t* c, void* stream) {
     if (!c) return SHD_ROUTE_EINVAL;
     if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
-    int rc = fw_prepare(c);
-    if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
+    int rc = fw_prepare(c, st);
+    if (rc) return rc;
     const int np = c->fw_np, nb = np / FW_T;
     const unsigned blocks = (unsigned)(((size_t)np * np + 255) / 256);
     hipLaunchKernelGGL(fw_init_kernel, dim3(blocks), dim3(256), 0, st, c->d_W, c->n, np, c->d_fwD);
@@ -1710,6 +1756,34 @@ __global__ __launch_bounds__(256) void tri_pack_kernel(const double* __restrict_
         if ((threadIdx.x & 63) == 0 && m < INFINITY) atomicMin(mn, as_u(m));
     }
 }
+
+// multi-GPU table assembly payload: row r (caller position pos[r] in the attached list)
+// keeps its upper-triangle targets j >= pos[r]; lat goes out as u16 (integer latencies
+// below 65535, NaN -> 0xFFFF) or f64, rel as f64, each into its own packed array at
+// element offset off[r] - off[0]
+template <bool L16>
+__global__ __launch_bounds__(256) void tri_payload_kernel(const double* __restrict__ lat, const double* __restrict__ rel,
+                                                          long long ld, const int* __restrict__ pos,
+                                                          const long long* __restrict__ off, int nrows, int na,
+                                                          void* __restrict__ out_lat, double* __restrict__ out_rel) {
+    const long long base = off[0];
+    for (int r = blockIdx.x; r < nrows; r += gridDim.x) {
+        const int i = pos[r];
+        const double* lr = lat + (long long)r * ld;
+        const double* rr = rel + (long long)r * ld;
+        const long long o = off[r] - base;
+        for (int j = i + threadIdx.x; j < na; j += 256) {
+            const double L = __builtin_nontemporal_load(lr + j);
+            if (L16) {
+                const uint16_t x = isnan(L) ? (uint16_t)0xFFFFu : (uint16_t)L;
+                static_cast<uint16_t*>(out_lat)[o + (j - i)] = x;
+            } else {
+                static_cast<double*>(out_lat)[o + (j - i)] = L;
+            }
+            out_rel[o + (j - i)] = __builtin_nontemporal_load(rr + j);
+        }
+    }
+}
 }  // namespace
 
 extern "C" {
@@ -1722,6 +1796,26 @@ namespace {
 std::mutex g_host_mu;
 std::map<void*, size_t> g_host_maps;  // registered mappings -> their length
 }  // namespace
+
+int shd_route_tri_payload_async(shd_route_t* c, const double* d_lat, const double* d_rel, int64_t ld,
+                                const int32_t* d_pos, const int64_t* d_off, int32_t nrows, int32_t na, uint32_t flags,
+                                void* d_out_lat, double* d_out_rel, void* stream) {
+    if (!c || nrows < 0 || na < 0 || ld < na || (nrows && (!d_lat || !d_rel || !d_pos || !d_off || !d_out_lat || !d_out_rel)))
+        return SHD_ROUTE_EINVAL;
+    const bool l16 = (flags & SHD_ROUTE_PAYLOAD_LAT16) != 0;
+    if (l16 && !(c->integer_w && c->k32_bound > 0 && c->k32_bound < 0xFFFF)) return SHD_ROUTE_EUNSUPPORTED;
+    if (nrows == 0) return SHD_ROUTE_OK;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(std::min(nrows, 8192));
+    if (l16)
+        hipLaunchKernelGGL(tri_payload_kernel<true>, grid, dim3(256), 0, st, d_lat, d_rel, (long long)ld, d_pos,
+                           (const long long*)d_off, nrows, na, d_out_lat, d_out_rel);
+    else
+        hipLaunchKernelGGL(tri_payload_kernel<false>, grid, dim3(256), 0, st, d_lat, d_rel, (long long)ld, d_pos,
+                           (const long long*)d_off, nrows, na, d_out_lat, d_out_rel);
+    return hip_check(hipGetLastError());
+}
 
 void* shd_route_host_alloc(size_t bytes) {
     if (!bytes) bytes = 1;

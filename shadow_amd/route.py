@@ -24,6 +24,7 @@ ENOEDGE = -4
 EUNREACH = -5
 EUNSUPPORTED = -6
 DISPATCH = 0x1
+PAYLOAD_LAT16 = 0x1
 
 
 class RouteError(RuntimeError):
@@ -68,7 +69,7 @@ EXPORTS = (
     "shd_route_self", "shd_route_min_reduce_async", "shd_route_fw_async",
     "shd_route_plan_create", "shd_route_plan_destroy", "shd_route_plan_get_info", "shd_route_plan_rows",
     "shd_route_rows_planned_async", "shd_route_fw_table_async", "shd_route_fw_rows_async",
-    "shd_route_fill_triangle", "shd_route_host_alloc", "shd_route_host_free",
+    "shd_route_fill_triangle", "shd_route_host_alloc", "shd_route_host_free", "shd_route_tri_payload_async",
 )
 
 _lib = None
@@ -113,6 +114,8 @@ def load_library():
     L.shd_route_fw_table_async.argtypes = [P, P]
     L.shd_route_fw_rows_async.restype = C.c_int
     L.shd_route_fw_rows_async.argtypes = [P, P, I32, P, I32, I64, P, P, P, P]
+    L.shd_route_tri_payload_async.restype = C.c_int
+    L.shd_route_tri_payload_async.argtypes = [P, P, P, I64, P, P, I32, I32, U32, P, P, P]
     L.shd_route_plan_create.restype = C.c_int
     L.shd_route_plan_create.argtypes = [P, P, I32, I32, I32, C.POINTER(P)]
     L.shd_route_plan_destroy.argtypes = [P]
@@ -243,6 +246,17 @@ class RouteEngine:
         if rc not in (OK, ENOEDGE, EUNREACH):
             raise RouteError(rc, "shd_route_fill_triangle")
         return mn.value, sec.value
+
+    def tri_payload_async(self, d_lat, d_rel, d_pos, d_off, na, out_lat, out_rel, lat16=True, stream=None, ld=None):
+        """shd_route_tri_payload_async: the upper-triangle payload of this rank's rows
+        (row r = attached position d_pos[r], targets j >= it) at offsets d_off - d_off[0]."""
+        nrows = int(d_pos.numel())
+        ld = int(d_lat.shape[1]) if ld is None else int(ld)
+        ptr = lambda t: C.c_void_p(t.data_ptr())
+        _check(load_library().shd_route_tri_payload_async(
+            self._h, ptr(d_lat), ptr(d_rel), ld, ptr(d_pos), ptr(d_off), nrows, int(na),
+            PAYLOAD_LAT16 if lat16 else 0, ptr(out_lat), ptr(out_rel), C.c_void_p(stream) if stream else None),
+            "shd_route_tri_payload_async")
 
     def plan(self, sources, world: int = 1, rank: int = 0) -> "RoutePlan":
         return RoutePlan(self, sources, world, rank)

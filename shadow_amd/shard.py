@@ -65,3 +65,76 @@ def allgather_inplace(full, dist, group=None):
     blk = full.shape[0] // world
     dist.all_gather_into_tensor(full, full[rank * blk:(rank + 1) * blk], group=group)
     return full
+
+
+# ---- reduced table-assembly payload (upper triangles, u16 latency) -------------------
+# The Path cache needs each unordered pair once (topology.c:1307-1336: the first writer
+# stores both directions), so a rank sends only the upper triangle of its rows: row of
+# attached position i keeps targets j >= i.  Segments are packed per rank in plan row
+# order; the gathered buffer holds rank k's segment at k * seg (seg = the largest rank's
+# element count).  Latency goes as u16 where exact (integer latencies below 65535 ms),
+# reliability as f64: 10 B per triangle pair against 16 B per square pair.
+
+def tri_offsets(pos, na: int):
+    """int64 element offsets of each row's triangle segment (row of position p holds
+    na - p entries), and the total."""
+    import numpy as np
+    pos = np.asarray(pos, np.int64)
+    ln = na - pos
+    off = np.zeros(len(pos) + 1, np.int64)
+    np.cumsum(ln, out=off[1:])
+    return off, int(off[-1])
+
+
+class TriangleIndex:
+    """Where pair (i, j), i <= j, of the attached list lives in the gathered payload:
+    every rank's row positions in its plan order (all_gather'ed), one lookup table."""
+
+    def __init__(self, pos_by_rank, na: int, seg: int):
+        import numpy as np
+        self.na, self.seg = na, seg
+        self.rank_of = np.full(na, -1, np.int32)
+        self.start = np.zeros(na, np.int64)  # element index of row i's segment
+        for k, pos in enumerate(pos_by_rank):
+            off, _ = tri_offsets(pos, na)
+            pos = np.asarray(pos, np.int64)
+            self.rank_of[pos] = k
+            self.start[pos] = k * seg + off[:-1]
+
+    def index(self, i, j):
+        """element index of pair (i, j) (either order)."""
+        import numpy as np
+        i, j = np.minimum(i, j), np.maximum(i, j)
+        return self.start[i] + (j - i)
+
+
+def pack_triangle_host(lat_rows, rel_rows, pos, na: int, lat16: bool = True):
+    """Host statement of shd_route_tri_payload_async (tests): the rows' triangles in row
+    order, latency as u16 (NaN -> 0xFFFF) or f64."""
+    import numpy as np
+    off, tot = tri_offsets(pos, na)
+    L = np.empty(tot, np.uint16 if lat16 else np.float64)
+    R = np.empty(tot, np.float64)
+    for r, p in enumerate(pos):
+        seg = lat_rows[r, p:na]
+        L[off[r]:off[r + 1]] = np.where(np.isnan(seg), 0xFFFF, seg).astype(np.uint16) if lat16 else seg
+        R[off[r]:off[r + 1]] = rel_rows[r, p:na]
+    return L, R
+
+
+def allgather_payload(lat_seg, rel_seg, seg: int, dist, group=None):
+    """All-gather every rank's packed segment (padded to `seg` elements) into
+    [world * seg] latency and reliability buffers (RCCL over xGMI with nccl)."""
+    import torch
+    world = dist.get_world_size(group)
+    def pad(x):
+        if x.numel() == seg:
+            return x
+        y = torch.empty(seg, dtype=x.dtype, device=x.device)
+        y[: x.numel()] = x
+        return y
+    out_l = torch.empty(world * seg, dtype=lat_seg.dtype, device=lat_seg.device)
+    out_r = torch.empty(world * seg, dtype=rel_seg.dtype, device=rel_seg.device)
+    dist.all_gather_into_tensor(out_l, pad(lat_seg), group=group)
+    dist.all_gather_into_tensor(out_r, pad(rel_seg), group=group)
+    return out_l, out_r

@@ -128,3 +128,77 @@ def test_fw_unsupported_fractional():
     with pytest.raises(route.RouteError) as e:
         eng.fw_table_async()
     assert e.value.code == route.EUNSUPPORTED
+
+
+def test_fw_ineligible_stays_unsupported():
+    """A graph whose K4 rows state overflows LDS (12 n + 4 (bound + 2) bytes): every
+    fw_table call answers EUNSUPPORTED (nothing is half-built by the first), and rows
+    from the table are refused."""
+    import torch
+    from shadow_amd import route
+    g = internet_like(10000, 2, seed=31)
+    g.latency = np.where(g.src != g.dst, g.latency * 40, g.latency)
+    eng = route.RouteEngine(g)
+    assert eng.info["integer_weights"] == 1 and 12 * g.n + 4 * (eng.info["dist_bound"] + 2) > 160 * 1024
+    for _ in range(2):
+        with pytest.raises(route.RouteError) as e:
+            eng.fw_table_async()
+        assert e.value.code == route.EUNSUPPORTED
+    dev = torch.device("cuda", 0)
+    S = torch.zeros(1, dtype=torch.int32, device=dev)
+    lat = torch.empty((1, 1), dtype=torch.float64, device=dev)
+    with pytest.raises(route.RouteError) as e:
+        eng.fw_rows_async(S, S, lat, lat.clone(), None)
+    assert e.value.code == route.EINVAL
+
+
+def test_fw_on_side_stream(oracle_mod):
+    """Table (with its first-call in-list build) and rows enqueued on a non-default torch
+    stream: the in-lists are built on that stream, ahead of the kernels that read them."""
+    import torch
+    from shadow_amd import route
+    g = internet_like(600, 3, seed=41)
+    eng = route.RouteEngine(g)
+    dev = torch.device("cuda", 0)
+    T = np.arange(g.n, dtype=np.int32)
+    S = T[::5]
+    st = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(st):
+        d_src = torch.from_numpy(S).to(dev)
+        d_tgt = torch.from_numpy(T).to(dev)
+        lat = torch.empty((len(S), len(T)), dtype=torch.float64, device=dev)
+        rel = torch.empty_like(lat)
+        eng.fw_table_async(st.cuda_stream)
+        eng.fw_rows_async(d_src, d_tgt, lat, rel, None, stream=st.cuda_stream)
+    eng.sync(st.cuda_stream)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(S, T, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat.cpu().numpy(), olat)
+    assert np.array_equal(rel.cpu().numpy(), orel)
+
+
+def test_c5_direct_table_full(oracle_mod):
+    """C5's reference semantics on the whole table: K3 (direct_rows_kernel) over all
+    4,000 x 4,000 pairs with the topology.c:2019 dispatch (complete graph -> every pair
+    DIRECT, topology.c:1877-1927) against the oracle's eager direct-mode table, and K5
+    (runahead min over the row minima, topology.c:1374-1385) against its min latency."""
+    import torch
+    from shadow_amd import route
+    g = config("c5")
+    eng = route.RouteEngine(g)
+    assert eng.info["is_complete"] == 1
+    T = np.arange(g.n, dtype=np.int32)
+    dev = torch.device("cuda", 0)
+    d_src = torch.from_numpy(T).to(dev)
+    lat = torch.empty((g.n, g.n), dtype=torch.float64, device=dev)
+    rel = torch.empty_like(lat)
+    mn = torch.full((g.n,), float("inf"), dtype=torch.float64, device=dev)
+    out = torch.full((1,), float("inf"), dtype=torch.float64, device=dev)
+    eng.rows_async(d_src, d_src, lat, rel, mn, dispatch=True)
+    eng.min_reduce_async(mn, out)
+    eng.sync()
+    tab = oracle_mod.OracleGraph(g).eager_table(T)
+    assert tab["is_direct"].all()
+    assert np.array_equal(lat.cpu().numpy(), tab["lat"])
+    assert np.array_equal(rel.cpu().numpy(), tab["rel"])
+    assert np.array_equal(mn.cpu().numpy(), tab["lat"].min(axis=1))
+    assert float(out.item()) == tab["min_latency"]

@@ -89,23 +89,65 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a, np.float64).tobytes()).hexdigest()
 
 
+def _digest16(row):
+    return hashlib.sha256(row.tobytes()).digest()[:16]
+
+
+def _check_every_row(d_lat, d_rel, d_min, row_src, gold, block=2048):
+    """Every row of the device table against the golden digests (tests/golden/
+    full_digests.npz: first 16 bytes of SHA-256 of each oracle row): rows come over in
+    pinned blocks and are hashed on host threads (hashlib releases the GIL)."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    src = gold["src"]
+    k_of = {int(v): k for k, v in enumerate(src)}
+    ks = np.array([k_of[int(s)] for s in row_src])
+    nr, nt = len(row_src), d_lat.shape[1]
+    assert np.array_equal(d_min[:nr].cpu().numpy(), gold["row_min"][ks])
+    bl = torch.empty((block, nt), dtype=torch.float64, pin_memory=True)
+    br = torch.empty((block, nt), dtype=torch.float64, pin_memory=True)
+    bad = []
+    with ThreadPoolExecutor(16) as ex:
+        for r0 in range(0, nr, block):
+            r1 = min(nr, r0 + block)
+            bl[: r1 - r0].copy_(d_lat[r0:r1])
+            br[: r1 - r0].copy_(d_rel[r0:r1])
+            L, R = bl.numpy(), br.numpy()
+            dl = list(ex.map(lambda i: _digest16(L[i]), range(r1 - r0)))
+            dr = list(ex.map(lambda i: _digest16(R[i]), range(r1 - r0)))
+            for i in range(r1 - r0):
+                k = ks[r0 + i]
+                if dl[i] != gold["lat_d"][k].tobytes() or dr[i] != gold["rel_d"][k].tobytes():
+                    bad.append(int(row_src[r0 + i]))
+    assert not bad, (len(bad), bad[:16])
+    return nr
+
+
+def _gold(cfg):
+    z = np.load(os.path.join(GOLD, "full_digests.npz"))
+    return {k: z[f"{cfg}__{k}"] for k in ("src", "lat_d", "rel_d", "row_min")}
+
+
 @pytest.mark.parametrize("cfg", ["c3", "c4"])
-def test_full_table_planned_matches_golden(monkeypatch, cfg):
-    """The whole C3 (9.3k x 9.3k) / C4 (50k x 50k, 40 GB) table by one seeded plan in
-    HBM; the golden rows (oracle digests) and the row minima must match, and the planned
-    table's runahead min must equal the golden one."""
+def test_full_table_every_row(monkeypatch, cfg):
+    """The whole C3 (9,337 x 9,337) / C4 (50k x 50k, 40 GB) table by one seeded plan in
+    HBM: EVERY row's latency and reliability against the oracle's row digests (C3 9,337
+    rows, C4 50,000 rows), every row minimum, the sampled rows' SHA-256 of
+    rows_digests.json, and the whole latency table's symmetry (undirected graph)."""
     import torch
     from shadow_amd import route
     monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
     monkeypatch.delenv("SHD_ROUTE_KDGRID", raising=False)
     monkeypatch.delenv("SHD_ROUTE_SEED", raising=False)
+    gold = _gold(cfg)
     dig = json.load(open(os.path.join(GOLD, "rows_digests.json")))[cfg]
     g = config(cfg)
     eng = route.RouteEngine(g)
     assert eng.info["kernel"] == 4
     T = g.targets()
+    assert np.array_equal(T, gold["src"])
     plan = eng.plan(T)
-    assert plan.info["seeded"] == 1
+    assert plan.info["seeded"] == 1 and np.array_equal(plan.positions, np.arange(len(T)))
     dev = torch.device("cuda", 0)
     d_tgt = torch.from_numpy(T.astype(np.int32)).to(dev)
     d_lat = torch.empty((len(T), len(T)), dtype=torch.float64, device=dev)
@@ -113,17 +155,19 @@ def test_full_table_planned_matches_golden(monkeypatch, cfg):
     d_min = torch.empty(len(T), dtype=torch.float64, device=dev)
     plan.rows_async(d_tgt, d_lat, d_rel, d_min, dispatch=False)
     eng.sync()
+    assert _check_every_row(d_lat, d_rel, d_min, plan.sources, gold) == len(T)
     row_of = {int(v): i for i, v in enumerate(T)}
     idx = torch.tensor([row_of[r["src"]] for r in dig["rows"]], device=dev)
-    lat = d_lat[idx].cpu().numpy()
-    rel = d_rel[idx].cpu().numpy()
-    mn = d_min[idx].cpu().numpy()
+    lat, rel = d_lat[idx].cpu().numpy(), d_rel[idx].cpu().numpy()
     for k, r in enumerate(dig["rows"]):
         assert _sha(lat[k]) == r["lat_sha"] and _sha(rel[k]) == r["rel_sha"], (cfg, r["src"])
-        assert mn[k] == r["row_min"]
-    # undirected integer latencies: the latency table is symmetric (spot-check a block)
-    blk = d_lat[:512, :512].cpu().numpy()
-    assert np.array_equal(blk, blk.T)
+    # undirected: lat(s,t) == lat(t,s) over the whole table, tile against transposed tile
+    tb = 8192
+    for i0 in range(0, len(T), tb):
+        for j0 in range(i0, len(T), tb):
+            a = d_lat[i0:i0 + tb, j0:j0 + tb]
+            b = d_lat[j0:j0 + tb, i0:i0 + tb]
+            assert torch.equal(a, b.t()), (i0, j0)
     del d_lat, d_rel
     torch.cuda.empty_cache()
 

@@ -218,18 +218,24 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world == 1 and args.gpus > 1:
         raise SystemExit("launch N>1 with torch.distributed.run (one process per GPU)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # (rehearsals of N ranks on a smaller box share its GPUs: SHD_BENCH_BACKEND=gloo)
+    gpu = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("SHD_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     barrier = dist.barrier if world > 1 else None
 
     if args.config == "c5":
         return bench_c5(args, torch, dist, world, rank, dev, barrier)
 
     from shadow_amd.route import RouteEngine
-    from shadow_amd.shard import allgather_inplace, full_table, runahead_min
+    from shadow_amd.shard import runahead_min
 
     weak = args.scaling == "weak"
     g = workload_graph(args.config, rank if weak else 0)
@@ -237,7 +243,7 @@ def main():
     all_sources = targets.copy()
     if args.sources:
         all_sources = all_sources[: args.sources]
-    eng = RouteEngine(g, device=local)
+    eng = RouteEngine(g, device=gpu)
     # the rows of this rank (strong: a contiguous block of the source list) under one
     # seeded plan: rows whose source has an already-computed neighbour start from it
     t_plan = time.perf_counter()
@@ -253,21 +259,27 @@ def main():
     sh = stream.cuda_stream
     d_tgt = torch.from_numpy(np.ascontiguousarray(targets, np.int32)).to(dev)
     gather = world > 1 and not weak
-    proto = torch.empty(0, dtype=torch.float64, device=dev)
+    d_lat = torch.empty((max(ns, 1), nt), dtype=torch.float64, device=dev)
+    d_rel = torch.empty((max(ns, 1), nt), dtype=torch.float64, device=dev)
     if gather:
-        # shards are views into the full tables: rows land in place, the gather is in place.
-        # A rank's block holds its plan rows (the seed forest's subtrees it owns), padded
-        # to the largest block; the gathered table's row order is every rank's
-        # plan.positions in turn
-        blk_t = torch.tensor([ns], dtype=torch.int64, device=dev)
-        dist.all_reduce(blk_t, op=dist.ReduceOp.MAX)
-        blk = int(blk_t.item())
-        f_lat, d_lat = full_table(len(all_sources), nt, world, rank, proto, blk)
-        f_rel, d_rel = full_table(len(all_sources), nt, world, rank, proto, blk)
-        d_lat, d_rel = d_lat[: max(ns, 1)], d_rel[: max(ns, 1)]
-    else:
-        d_lat = torch.empty((max(ns, 1), nt), dtype=torch.float64, device=dev)
-        d_rel = torch.empty((max(ns, 1), nt), dtype=torch.float64, device=dev)
+        # table assembly payload: each rank packs the upper triangles of its rows (the Path
+        # cache holds each unordered pair once, topology.c:1307-1336), latency as u16 where
+        # exact, and all-gathers the packed segments (padded to the largest rank's)
+        from shadow_amd.shard import tri_offsets, allgather_payload, TriangleIndex
+        lat16 = bool(eng.info["integer_weights"]) and 0 < eng.info["dist_bound"] < 0xFFFF
+        pos = np.asarray(plan.positions, np.int64)  # attached positions (sources = the sorted targets)
+        off, tot = tri_offsets(pos, nt)
+        seg_t = torch.tensor([tot], dtype=torch.int64, device=dev)
+        dist.all_reduce(seg_t, op=dist.ReduceOp.MAX)
+        seg = int(seg_t.item())
+        d_pos = torch.from_numpy(pos.astype(np.int32)).to(dev)
+        d_off = torch.from_numpy(off[:-1].copy()).to(dev)
+        p_lat = torch.empty(max(seg, 1), dtype=torch.int16 if lat16 else torch.float64, device=dev)
+        p_rel = torch.empty(max(seg, 1), dtype=torch.float64, device=dev)
+        pos_by_rank = [None] * world
+        dist.all_gather_object(pos_by_rank, pos)
+        tindex = TriangleIndex(pos_by_rank, nt, seg)
+        gathered = {}
     # +inf: a rank with an empty shard contributes nothing to the runahead MIN
     d_rmin = torch.full((max(ns, 1),), float("inf"), dtype=torch.float64, device=dev)
     d_min = torch.full((1,), float("inf"), dtype=torch.float64, device=dev)
@@ -277,8 +289,9 @@ def main():
     k_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
 
     def gather_tables():
-        allgather_inplace(f_lat, dist)
-        allgather_inplace(f_rel, dist)
+        if ns:
+            eng.tri_payload_async(d_lat, d_rel, d_pos, d_off, nt, p_lat, p_rel, lat16=lat16, stream=sh)
+        gathered["lat"], gathered["rel"] = allgather_payload(p_lat[:seg], p_rel[:seg], seg, dist)
 
     def step(t=None):
         if t is not None:
@@ -316,6 +329,22 @@ def main():
             ag_s = timed(gather_tables, args.gather_reps, torch.cuda.synchronize, barrier) / args.gather_reps
         split = torch.tensor([float(np.mean(kms)) / 1e3, ar_s, ag_s or 0.0], dtype=torch.float64, device=dev)
         dist.all_reduce(split, op=dist.ReduceOp.MAX)
+        gathered_ok = None
+        if args.verify and rank == 0 and gathered:
+            # rows computed on the LAST rank, read back out of rank 0's gathered payload
+            from oracle.oracle import OracleGraph, TIE_MINKEY
+            og = OracleGraph(g)
+            mine = np.asarray(pos_by_rank[world - 1])
+            pick = mine[np.linspace(0, len(mine) - 1, num=min(3, len(mine))).astype(int)]
+            gl, gr = gathered["lat"].cpu().numpy(), gathered["rel"].cpu().numpy()
+            if lat16:
+                gl = gl.view(np.uint16)
+            gathered_ok = True
+            for i in pick:
+                olat, orel, _, _ = og.source_row(int(targets[i]), targets, TIE_MINKEY)
+                k = tindex.index(np.full(nt - i, i), np.arange(i, nt))
+                L = gl[k].astype(np.float64)
+                gathered_ok &= bool(np.array_equal(L, olat[i:]) and np.array_equal(gr[k], orel[i:]))
     dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
@@ -404,12 +433,18 @@ def main():
     }
     if split is not None:
         c_s, ar_s, ag_s = (float(x) for x in split.tolist())
-        gb = 16 * len(all_sources) * nt * (world - 1) / world
+        gb = (world - 1) * seg * ((2 if lat16 else 8) + 8)  # received per GPU
+        full_gb = 16 * len(all_sources) * nt * (world - 1) / world
         res["split"] = {"compute_ms": c_s * 1e3, "allreduce_min_ms": ar_s * 1e3,
                         "allgather_lat_rel_ms": (ag_s * 1e3) if ag_s else None,
                         "allgather_in_step": bool(args.allgather),
+                        "allgather_payload": ("upper-triangle rows, lat u16 + rel f64" if lat16
+                                              else "upper-triangle rows, lat f64 + rel f64"),
                         "allgather_bytes_per_gpu": gb,
-                        "allgather_GBps_per_gpu": (gb / ag_s / 1e9) if ag_s else None}
+                        "full_f64_table_bytes_per_gpu": full_gb,
+                        "payload_over_full_table": gb / full_gb,
+                        "allgather_GBps_per_gpu": (gb / ag_s / 1e9) if ag_s else None,
+                        "gathered_rows_verified_vs_oracle": gathered_ok}
     if not args.no_cpu_baseline and world == 1:
         par, faithful = cpu_baseline(g, all_sources, targets, args.cpu_budget)
         res["cpu_baseline"] = par

@@ -1194,7 +1194,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     auto P = std::make_unique<shd_route_plan>();
     P->c = c; P->world = world; P->rank = rank; P->ns_all = ns;
     const auto t_start = std::chrono::steady_clock::now();
-    double t_close = 0, t_land = 0, t_seeds = 0, t_store = 0, t_sched = 0;  // SHD_ROUTE_PLAN_DEBUG stage times
+    double t_close = 0, t_land = 0, t_seeds = 0, t_store = 0, t_sched = 0, t_rk = 0, t_order = 0, t_hop = 0;  // SHD_ROUTE_PLAN_DEBUG stage times
     auto since = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
     const int n = c->n;
     const char* env = getenv("SHD_ROUTE_SEED");
@@ -1206,41 +1206,51 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         const int rc = ensure_close(c);
         if (rc) return rc;
         t_close = since();
-        std::vector<int> ord(n);
+        // (closeness, vertex) pairs sorted in place: no indirection in the comparisons
+        std::vector<std::pair<double, int>> ord(n);
         rk.resize(n);
-        std::iota(ord.begin(), ord.end(), 0);
-        std::sort(ord.begin(), ord.end(), [&](int a, int b) {
-            return c->close[a] != c->close[b] ? c->close[a] < c->close[b] : a < b;
-        });
-        for (int q = 0; q < n; q++) rk[ord[q]] = q;
+        for (int v = 0; v < n; v++) ord[v] = {c->close[v], v};
+        std::sort(ord.begin(), ord.end());
+        for (int q = 0; q < n; q++) rk[ord[q].second] = q;
+        t_rk = since();
     }
-    auto by_rank = [&](std::vector<int>& v) {  // positions by (vertex rank, position)
-        std::sort(v.begin(), v.end(), [&](int a, int b) {
-            return rk[src[a]] != rk[src[b]] ? rk[src[a]] < rk[src[b]] : a < b;
-        });
+    auto by_rank = [&](std::vector<int>& v) {  // positions by (vertex rank, position): counting sort
+        std::vector<int> cnt(n + 1, 0), tmp(v.size());
+        std::vector<int> sv(v);
+        std::sort(sv.begin(), sv.end());
+        for (int p : sv) cnt[rk[src[p]] + 1]++;
+        for (int x = 0; x < n; x++) cnt[x + 1] += cnt[x];
+        for (int p : sv) tmp[cnt[rk[src[p]]]++] = p;
+        v.swap(tmp);
     };
     // the best seeds of position p among the positions marked in `avail` (first[v]: the
-    // available position of vertex v): neighbours of smaller rank by w(s,u) + closeness(u)
-    std::vector<std::pair<double, int>> cand;
+    // available position of vertex v): neighbours of smaller rank by w(s,u) + closeness(u),
+    // then vertex.  One pass keeping the k best in order (what a full sort of the
+    // candidates would list first; a multigraph's repeated u keeps its best arc, the first
+    // arc on a full tie): hubs have thousands of neighbours, k is at most 3.
     double alpha = 1.0;  // seed score w(s,u) + alpha * closeness(u)
     if (const char* e = getenv("SHD_ROUTE_SEEDALPHA")) alpha = atof(e);
-    auto best_seeds = [&](int p, const std::vector<int>& first, int k, int* arc_out) {
+    auto best_seeds = [&](int p, auto avail, int k, int* arc_out) {
         const int s = src[p];
-        cand.clear();
+        double sc[KD_SEEDS];
+        int m = 0;
         for (int a = c->h_row[s]; a < c->h_row[s + 1]; a++) {
             const int u = c->h_col[a];
-            if (u == s || first[u] < 0 || rk[u] >= rk[s]) continue;
-            cand.push_back({c->h_w[a] + alpha * c->close[u], a});
-        }
-        std::sort(cand.begin(), cand.end(), [&](const std::pair<double, int>& x, const std::pair<double, int>& y) {
-            return x.first != y.first ? x.first < y.first : c->h_col[x.second] < c->h_col[y.second];
-        });
-        int m = 0;
-        for (const auto& cd : cand) {
-            if (m == k) break;
-            bool dup = false;  // (a multigraph would list u twice)
-            for (int q = 0; q < m; q++) dup = dup || c->h_col[arc_out[q]] == c->h_col[cd.second];
-            if (!dup) arc_out[m++] = cd.second;
+            if (u == s || !avail(u) || rk[u] >= rk[s]) continue;
+            const double x = c->h_w[a] + alpha * c->close[u];
+            int dq = -1;
+            for (int q = 0; q < m; q++) if (c->h_col[arc_out[q]] == u) dq = q;
+            if (dq >= 0) {
+                if (!(x < sc[dq])) continue;
+                for (int q = dq; q + 1 < m; q++) { sc[q] = sc[q + 1]; arc_out[q] = arc_out[q + 1]; }
+                m--;
+            }
+            auto before = [&](int q) { return x != sc[q] ? x < sc[q] : u < c->h_col[arc_out[q]]; };
+            if (m == k && !before(m - 1)) continue;
+            int q = m < k ? m++ : k - 1;
+            for (; q > 0 && before(q - 1); q--) { sc[q] = sc[q - 1]; arc_out[q] = arc_out[q - 1]; }
+            sc[q] = x;
+            arc_out[q] = a;
         }
         return m;
     };
@@ -1263,7 +1273,10 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         int maxl = 0;
         for (int p : pos) {
             int a;
-            if (best_seeds(p, first, 1, &a)) { fpar[p] = first[c->h_col[a]]; flvl[p] = flvl[fpar[p]] + 1; }
+            if (best_seeds(p, [&](int u) { return first[u] >= 0; }, 1, &a)) {
+                fpar[p] = first[c->h_col[a]];
+                flvl[p] = flvl[fpar[p]] + 1;
+            }
             maxl = std::max(maxl, flvl[p]);
         }
         for (int q = ns - 1; q >= 0; q--) if (fpar[pos[q]] >= 0) sub[fpar[pos[q]]] += sub[pos[q]];
@@ -1302,6 +1315,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // jobs in rank order: a job's seeds (smaller rank) are settled before it
         std::vector<int> order(job_pos);
         by_rank(order);
+        t_order = since();
         std::vector<int> lvl(nj, 0), slot(nj, -1), nsd(nj, 0);
         std::vector<std::array<int, KD_SEEDS>> seedjob(nj), su(nj), wr(nj);
         // options: seeds per row (1..KD_SEEDS), the `roots` most central rows start
@@ -1349,13 +1363,84 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         std::vector<int> fl(n, -1);  // first job of a vertex, once its level is below the cap
         std::vector<std::array<int, KD_SEEDS>> srec(nj);
         struct Hop { double cost; int u, off; uint32_t rec; };
-        std::vector<Hop> hops;
+        // A row's seeds: its best kseeds available neighbour rows, then (if short) its best
+        // two-hop rows (s -> x -> u, x of degree <= 256), each list in the order a full sort
+        // of the candidates would give.  avail(u): u's row is a usable seed.
+        struct Choice { int m, nh; int arcs[KD_SEEDS]; Hop hop[KD_SEEDS]; };
+        auto choose = [&](int p, auto avail, Choice& C) {
+            const int s = src[p];
+            C.m = best_seeds(p, avail, kseeds, C.arcs);
+            C.nh = 0;
+            if (!two_hop || C.m >= kseeds) return;
+            const int need = kseeds - C.m;
+            auto before = [](const Hop& x, const Hop& y) {
+                return x.cost != y.cost ? x.cost < y.cost : x.u != y.u ? x.u < y.u : x.rec < y.rec;
+            };
+            for (int a = c->h_row[s]; a < c->h_row[s + 1]; a++) {
+                const int x = c->h_col[a];
+                if (x == s || c->h_row[x + 1] - c->h_row[x] > 256) continue;
+                for (int b = c->h_row[x]; b < c->h_row[x + 1]; b++) {
+                    const int u = c->h_col[b];
+                    if (u == s || u == x || rk[u] >= rk[s] || !avail(u)) continue;
+                    bool dup = false;
+                    for (int k = 0; k < C.m; k++) dup = dup || c->h_col[C.arcs[k]] == u;
+                    if (dup) continue;
+                    const Hop h{c->h_w[a] + c->h_w[b] + c->close[u], u, (int)(c->h_w[a] + c->h_w[b]),
+                                (uint32_t)x | ((uint32_t)c->h_ridx[b] << 16) | ((uint32_t)c->h_w[b] << 24)};
+                    int dq = -1;
+                    for (int q = 0; q < C.nh; q++) if (C.hop[q].u == u) dq = q;
+                    if (dq >= 0) {
+                        if (!before(h, C.hop[dq])) continue;
+                        for (int q = dq; q + 1 < C.nh; q++) C.hop[q] = C.hop[q + 1];
+                        C.nh--;
+                    }
+                    if (C.nh == need && !before(h, C.hop[C.nh - 1])) continue;
+                    int q = C.nh < need ? C.nh++ : need - 1;
+                    for (; q > 0 && before(h, C.hop[q - 1]); q--) C.hop[q] = C.hop[q - 1];
+                    C.hop[q] = h;
+                }
+            }
+        };
+        // Choices precomputed on host threads against a superset of the usable rows (every
+        // row of an earlier source: the sequential pass below only withholds rows past the
+        // seed-chain depth cap); the sequential pass keeps a precomputed choice when every
+        // row in it is usable -- then it is exactly the choice over the usable rows -- and
+        // recomputes the row otherwise.
+        std::vector<Choice> pre(order.size());
+        {
+            const double th0 = since();
+            const int nq = (int)order.size();
+            std::atomic<int> nextq{nroot_min};
+            auto work = [&]() {
+                for (int q0 = nextq.fetch_add(256); q0 < nq; q0 = nextq.fetch_add(256))
+                    for (int qq = q0; qq < std::min(nq, q0 + 256); qq++)
+                        choose(order[qq], [&](int u) { return first[u] >= 0; }, pre[qq]);
+            };
+            const int nth = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+            std::vector<std::thread> th;
+            for (int t = 1; t < nth; t++) th.emplace_back(work);
+            work();
+            for (auto& t : th) t.join();
+            t_hop = since() - th0;
+        }
         int nlev = 1, q = 0;
         for (int p : order) {
             const int j = jpos_of[p], s = src[p];
             int arcs[KD_SEEDS];
+            const int qi = q;
             const bool seedable = q++ >= nroot_min;
-            int m = seedable ? best_seeds(p, fl, kseeds, arcs) : 0;
+            Choice ch;
+            ch.m = ch.nh = 0;
+            if (seedable) {
+                bool ok = true;
+                const Choice& pc = pre[qi];
+                for (int k = 0; k < pc.m; k++) ok = ok && fl[c->h_col[pc.arcs[k]]] >= 0;
+                for (int k = 0; k < pc.nh; k++) ok = ok && fl[pc.hop[k].u] >= 0;
+                if (ok) ch = pc;
+                else choose(p, [&](int u) { return fl[u] >= 0; }, ch);
+            }
+            int m = ch.m;
+            for (int k = 0; k < m; k++) arcs[k] = ch.arcs[k];
             if (!seedable && nland > 0) {
                 // nearest landmarks by d(s, L) (undirected: d_L(s)), up to kseeds
                 std::vector<std::pair<double, int>> lc;
@@ -1385,32 +1470,8 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 wr[j][k] = (int)c->h_w[a];
                 srec[j][k] = (int)((uint32_t)s | ((uint32_t)c->h_ridx[a] << 16) | ((uint32_t)c->h_w[a] << 24));
             }
-            if (two_hop && seedable && m < kseeds) {
-                hops.clear();
-                for (int a = c->h_row[s]; a < c->h_row[s + 1]; a++) {
-                    const int x = c->h_col[a];
-                    if (x == s || c->h_row[x + 1] - c->h_row[x] > 256) continue;
-                    for (int b = c->h_row[x]; b < c->h_row[x + 1]; b++) {
-                        const int u = c->h_col[b];
-                        if (u == s || u == x || fl[u] < 0 || rk[u] >= rk[s]) continue;
-                        bool dup = false;
-                        for (int k = 0; k < m; k++) dup = dup || su[j][k] == u;
-                        if (dup) continue;
-                        hops.push_back({c->h_w[a] + c->h_w[b] + c->close[u], u, (int)(c->h_w[a] + c->h_w[b]),
-                                        (uint32_t)x | ((uint32_t)c->h_ridx[b] << 16) | ((uint32_t)c->h_w[b] << 24)});
-                    }
-                }
-                std::sort(hops.begin(), hops.end(), [](const Hop& x, const Hop& y) {
-                    return x.cost != y.cost ? x.cost < y.cost : x.u != y.u ? x.u < y.u : x.rec < y.rec;
-                });
-                for (const Hop& h : hops) {
-                    if (m == kseeds) break;
-                    bool dup = false;
-                    for (int k = 0; k < m; k++) dup = dup || su[j][k] == h.u;
-                    if (dup) continue;
-                    su[j][m] = h.u; wr[j][m] = h.off; srec[j][m] = (int)h.rec;
-                    m++;
-                }
+            for (int q2 = 0; q2 < ch.nh; q2++, m++) {
+                su[j][m] = ch.hop[q2].u; wr[j][m] = ch.hop[q2].off; srec[j][m] = (int)ch.hop[q2].rec;
             }
             for (int k = 0; k < m; k++) {
                 const int sj = first[su[j][k]];
@@ -1464,12 +1525,18 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             if (const char* e = getenv("SHD_ROUTE_LMCOST")) lm_cost = std::max(0.1, atof(e));
             if (const char* e = getenv("SHD_ROUTE_ROOTCOST")) root_cost = std::max(0.1, atof(e));
             if (const char* e = getenv("SHD_ROUTE_FLAGAT")) flag_at = std::max(0.0, std::min(1.0, atof(e)));
-            std::vector<std::vector<int>> dep(nj);
-            std::vector<int> left(nj);
-            for (int j = 0; j < nj; j++) {
-                left[j] = 0;
+            // dependants of each job as one CSR (job j's in [dbeg[j], dbeg[j + 1]))
+            std::vector<int> left(nj, 0), dbeg(nj + 1, 0), dep;
+            for (int j = 0; j < nj; j++)
                 for (int k = 0; k < nsd[j]; k++)
-                    if (lmseed[j][k] < 0) { dep[seedjob[j][k]].push_back(j); left[j]++; }
+                    if (lmseed[j][k] < 0) { dbeg[seedjob[j][k] + 1]++; left[j]++; }
+            for (int j = 0; j < nj; j++) dbeg[j + 1] += dbeg[j];
+            dep.resize(dbeg[nj]);
+            {
+                std::vector<int> fill(dbeg.begin(), dbeg.end() - 1);
+                for (int j = 0; j < nj; j++)
+                    for (int k = 0; k < nsd[j]; k++)
+                        if (lmseed[j][k] < 0) dep[fill[seedjob[j][k]]++] = j;
             }
             std::vector<double> ready(nj, 0.0);
             typedef std::pair<double, int> DI;
@@ -1486,7 +1553,8 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 const double start = std::max(f.first, jr.first);
                 free_at.push({start + t, f.second});
                 qorder.push_back(j);
-                for (int d : dep[j]) {
+                for (int e = dbeg[j]; e < dbeg[j + 1]; e++) {
+                    const int d = dep[e];
                     ready[d] = std::max(ready[d], start + flag_at * t);
                     if (--left[d] == 0) cq.push({ready[d], d});
                 }
@@ -1497,8 +1565,10 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 for (int j = 0; j < nj; j++) hist[nsd[j]]++;
                 fprintf(stderr, "plan world %d rank %d: jobs %d levels %d seeds:", world, rank, nj, nlev);
                 for (int k = 0; k <= KD_SEEDS; k++) fprintf(stderr, " %d:%d", k, hist[k]);
-                fprintf(stderr, "  closeness rows %.2f ms, landmark rows %.2f ms, seeds done %.2f, store %.2f, schedule %.2f ms\n",
-                        1e3 * t_close, 1e3 * t_land, 1e3 * t_seeds, 1e3 * t_store, 1e3 * t_sched);
+                fprintf(stderr, "  closeness rows %.2f ms, rank sort done %.2f, order sort done %.2f, landmark rows %.2f ms, "
+                        "seed choices (threads) %.2f ms, seeds done %.2f, store %.2f, schedule %.2f ms\n",
+                        1e3 * t_close, 1e3 * t_rk, 1e3 * t_order, 1e3 * t_land, 1e3 * t_hop, 1e3 * t_seeds, 1e3 * t_store,
+                        1e3 * t_sched);
             }
             jobs.resize(nj);
             int qi = 0;
@@ -1687,12 +1757,18 @@ int shd_route_fw_table_async(shd_route_t* c, void* stream) {
     const int np = c->fw_np, nb = np / FW_T;
     const unsigned blocks = (unsigned)(((size_t)np * np + 255) / 256);
     hipLaunchKernelGGL(fw_init_kernel, dim3(blocks), dim3(256), 0, st, c->d_W, c->n, np, c->d_fwD);
+    // (SHD_ROUTE_FWREST=1: the 64 x 64 rest kernel with 4 x 4 blocks, for A/B runs)
+    static const int rest1 = getenv("SHD_ROUTE_FWREST") && atoi(getenv("SHD_ROUTE_FWREST")) == 1;
+    const int nr = (nb + 1) / 2;
     for (int kb = 0; kb < nb; kb++) {
         // pivot tiles after the first are closed inside the previous fw_rest launch
         if (kb == 0) hipLaunchKernelGGL(fw_diag_kernel<FW_T>, dim3(1), dim3(256), 0, st, c->d_fwD, np, kb);
         if (nb > 1) {
             hipLaunchKernelGGL(fw_panel_kernel<FW_T>, dim3(nb - 1, 2), dim3(256), 0, st, c->d_fwD, np, kb);
-            hipLaunchKernelGGL(fw_rest_kernel<FW_T>, dim3(nb - 1, nb - 1), dim3(256), 0, st, c->d_fwD, np, kb);
+            if (rest1)
+                hipLaunchKernelGGL(fw_rest_kernel<FW_T>, dim3(nb - 1, nb - 1), dim3(256), 0, st, c->d_fwD, np, kb);
+            else
+                hipLaunchKernelGGL(fw_rest2_kernel, dim3(nr * nr), dim3(256), 0, st, c->d_fwD, np, kb);
         }
     }
     c->fw_ready = 1;

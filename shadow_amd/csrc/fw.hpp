@@ -89,26 +89,33 @@ __device__ inline void fw_st(uint16_t* p, const uint32_t (&v)[H]) {
 template <int T>
 __device__ inline void fw_tile_product(const uint16_t* At, const uint16_t* Bt, uint32_t (&acc)[T / 16][T / 32], int r, int c) {
     constexpr int R = T / 16, H = R / 2;
+    // software-pipelined LDS reads (step k + 1's in flight while step k computes), and per
+    // row the adds into temporaries before the mins (an op_sel'd add followed directly by
+    // its dependent min costs an s_nop)
+    uint32_t av[H], bv[H];
+    fw_ld<H>(At + R * r, av);
+    fw_ld<H>(Bt + R * c, bv);
 #pragma unroll 4
     for (int k = 0; k < T; k++) {
-        uint32_t av[H], bv[H];
-        fw_ld<H>(At + k * T + R * r, av);
-        fw_ld<H>(Bt + k * T + R * c, bv);
+        const int kn = k + 1 < T ? k + 1 : k;
+        uint32_t an[H], bn[H];
+        fw_ld<H>(At + kn * T + R * r, an);
+        fw_ld<H>(Bt + kn * T + R * c, bn);
         // a row value broadcast to both halves is a shuffle the packed add takes as an
         // op_sel modifier: no instruction of its own
-        fw_us2 a2[R];
 #pragma unroll
-        for (int h = 0; h < H; h++) {
-            const fw_us2 x = __builtin_bit_cast(fw_us2, av[h]);
-            a2[2 * h] = __builtin_shufflevector(x, x, 0, 0);
-            a2[2 * h + 1] = __builtin_shufflevector(x, x, 1, 1);
-        }
-#pragma unroll
-        for (int i = 0; i < R; i++)
+        for (int i = 0; i < R; i++) {
+            const fw_us2 x = __builtin_bit_cast(fw_us2, av[i >> 1]);
+            const fw_us2 a2 = (i & 1) ? __builtin_shufflevector(x, x, 1, 1) : __builtin_shufflevector(x, x, 0, 0);
+            uint32_t t[H];
 #pragma unroll
             for (int h = 0; h < H; h++)
-                acc[i][h] = fw_pkmin(acc[i][h], __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(
-                                                                                a2[i], __builtin_bit_cast(fw_us2, bv[h]))));
+                t[h] = __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(a2, __builtin_bit_cast(fw_us2, bv[h])));
+#pragma unroll
+            for (int h = 0; h < H; h++) acc[i][h] = fw_pkmin(acc[i][h], t[h]);
+        }
+#pragma unroll
+        for (int h = 0; h < H; h++) { av[h] = an[h]; bv[h] = bn[h]; }
     }
 }
 
@@ -252,6 +259,126 @@ __global__ __launch_bounds__(256) void fw_rest_kernel(uint16_t* __restrict__ D, 
         fw_close<T>(At, acc, r, c);
     }
     fw_store_block<T>(D, np, ti, tj, r, c, acc);
+}
+
+// The rest update of pivot kb over 128 x 128 regions (2 x 2 tiles of 64) with 8 x 8
+// register blocks: 256 threads as 16 x 16, thread (r, c) holds rows 8r.. and columns 8c..
+// of the region.  Per k step one 16-byte LDS read of the column panel (transposed: the
+// thread's 8 rows) and one of the row panel (its 8 columns) feed 64 relaxations (32
+// v_pk_add_u16 + 32 v_pk_min_u16): half the LDS bytes per relaxation of the 4 x 4 form,
+// which shared the LDS and VALU evenly and ran at 0.27 of the packed-u16 VALU rate.
+// Regions are fixed in absolute tile coordinates and the 1-D grid maps region w to
+// workgroup w every pivot, so a region stays on XCD w % 8 and its tiles in that XCD's L2
+// across pivots.  Tiles in pivot row or column kb (the panels), or past the matrix, are
+// not written.  The region holding the next pivot tile (kb + 1, kb + 1) is dispatched
+// first (its workgroup id swapped with 0) and closes that tile after its product, as the
+// 64 x 64 kernel did.
+constexpr int FW_RG = 2 * FW_T;  // region edge
+__global__ __launch_bounds__(256) void fw_rest2_kernel(uint16_t* __restrict__ D, int np, int kb) {
+    static_assert(FW_T == 64, "regions of 2 x 2 tiles of 64");
+    __shared__ __attribute__((aligned(16))) uint16_t At[FW_T * FW_RG];  // [k][i], i < 128
+    __shared__ __attribute__((aligned(16))) uint16_t Bt[FW_T * FW_RG];  // [k][j], j < 128
+    const int nb = np / FW_T, nr = (nb + 1) / 2;
+    const int pn = kb + 1;
+    int w = blockIdx.x;
+    if (pn < nb) {
+        const int wp = (pn / 2) * nr + pn / 2;
+        if (w == 0) w = wp;
+        else if (w == wp) w = 0;
+    }
+    const int I = w / nr, J = w % nr;
+    if (I >= nr) return;
+    const int tid = threadIdx.x, r = tid >> 4, c = tid & 15;
+    // valid tile rows / columns of the region (not the pivot's, not past the matrix)
+    const bool row_ok[2] = {2 * I < nb && 2 * I != kb, 2 * I + 1 < nb && 2 * I + 1 != kb};
+    const bool col_ok[2] = {2 * J < nb && 2 * J != kb, 2 * J + 1 < nb && 2 * J + 1 != kb};
+    if (!((row_ok[0] || row_ok[1]) && (col_ok[0] || col_ok[1]))) return;  // (uniform)
+    const int ti = 2 * I + (r >> 3), tj = 2 * J + (c >> 3);
+    const bool mine = row_ok[r >> 3] && col_ok[c >> 3];
+    const long long row0 = (long long)ti * FW_T + 8 * (r & 7);
+    const int col0 = tj * FW_T + 8 * (c & 7);
+    // C first: its loads overlap the panel staging
+    uint32_t acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        if (mine) {
+            const uint4 x = *reinterpret_cast<const uint4*>(D + (row0 + i) * np + col0);
+            acc[i][0] = x.x; acc[i][1] = x.y; acc[i][2] = x.z; acc[i][3] = x.w;
+        } else {
+            acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0xFFFFFFFFu;
+        }
+    }
+    // column panel D[region rows][kb cols] transposed into At: a wave's lanes take 64
+    // consecutive rows of one 4-column strip (consecutive 2-byte LDS writes); rows of a
+    // tile past the matrix read as "no path"
+    for (int q = tid; q < FW_RG * FW_T / 4; q += 256) {
+        const int row = q % FW_RG, c4 = (q / FW_RG) * 4;
+        const int gt = 2 * I + (row >> 6);
+        uint2 v = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (gt < nb) v = *reinterpret_cast<const uint2*>(D + ((long long)2 * I * FW_T + row) * np + kb * FW_T + c4);
+        At[(c4 + 0) * FW_RG + row] = (uint16_t)(v.x & 0xFFFFu);
+        At[(c4 + 1) * FW_RG + row] = (uint16_t)(v.x >> 16);
+        At[(c4 + 2) * FW_RG + row] = (uint16_t)(v.y & 0xFFFFu);
+        At[(c4 + 3) * FW_RG + row] = (uint16_t)(v.y >> 16);
+    }
+    // row panel D[kb rows][region cols] into Bt as is
+    for (int q = tid; q < FW_T * FW_RG / 8; q += 256) {
+        const int k = q / (FW_RG / 8), c8 = (q % (FW_RG / 8)) * 8;
+        const int gt = 2 * J + (c8 >> 6);
+        uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (gt < nb) v = *reinterpret_cast<const uint4*>(D + ((long long)kb * FW_T + k) * np + 2 * J * FW_T + c8);
+        *reinterpret_cast<uint4*>(Bt + k * FW_RG + c8) = v;
+    }
+    __syncthreads();
+    // software-pipelined: step k + 1's two LDS reads are in flight while step k computes;
+    // per row the four packed adds go to their own temporaries before the four mins, so
+    // no add is followed directly by its dependent min (which costs an s_nop after an
+    // op_sel'd add)
+    uint4 av = *reinterpret_cast<const uint4*>(At + 8 * r);
+    uint4 bv = *reinterpret_cast<const uint4*>(Bt + 8 * c);
+#pragma unroll 2
+    for (int k = 0; k < FW_T; k++) {
+        const int kn = k + 1 < FW_T ? k + 1 : k;
+        const uint4 an = *reinterpret_cast<const uint4*>(At + kn * FW_RG + 8 * r);
+        const uint4 bn = *reinterpret_cast<const uint4*>(Bt + kn * FW_RG + 8 * c);
+        const uint32_t aw[4] = {av.x, av.y, av.z, av.w}, bw[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const fw_us2 x = __builtin_bit_cast(fw_us2, aw[i >> 1]);
+            const fw_us2 a2 = (i & 1) ? __builtin_shufflevector(x, x, 1, 1) : __builtin_shufflevector(x, x, 0, 0);
+            uint32_t t[4];
+#pragma unroll
+            for (int h = 0; h < 4; h++)
+                t[h] = __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(a2, __builtin_bit_cast(fw_us2, bw[h])));
+#pragma unroll
+            for (int h = 0; h < 4; h++) acc[i][h] = fw_pkmin(acc[i][h], t[h]);
+        }
+        av = an;
+        bv = bn;
+    }
+    const bool pivot_region = pn < nb && (pn >> 1) == I && (pn >> 1) == J;
+    const bool pivot_mine = pivot_region && ti == pn && tj == pn;
+    if (pivot_region) {
+        // the next pivot tile: its 64 owner threads hand it over in LDS, the whole
+        // workgroup closes it in the 4 x 4 layout, and stores it
+        __syncthreads();  // every thread's product is done with At
+        if (pivot_mine)
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                *reinterpret_cast<uint4*>(At + (8 * (r & 7) + i) * FW_T + 8 * (c & 7)) =
+                    make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+        __syncthreads();
+        const int r4 = tid / 16, c4 = tid % 16;
+        uint32_t x[4][2];
+#pragma unroll
+        for (int i = 0; i < 4; i++) fw_ld<2>(At + (4 * r4 + i) * FW_T + 4 * c4, x[i]);
+        fw_close<FW_T>(At, x, r4, c4);
+        fw_store_block<FW_T>(D, np, pn, pn, r4, c4, x);
+    }
+    if (mine && !pivot_mine)
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+            *reinterpret_cast<uint4*>(D + (row0 + i) * np + col0) = make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
 }
 
 // In-arc lists for the parent search, built once per graph: row v holds the keys

@@ -135,6 +135,8 @@ def allgather_payload(lat_seg, rel_seg, seg: int, dist, group=None):
         return y
     out_l = torch.empty(world * seg, dtype=lat_seg.dtype, device=lat_seg.device)
     out_r = torch.empty(world * seg, dtype=rel_seg.dtype, device=rel_seg.device)
-    dist.all_gather_into_tensor(out_l, pad(lat_seg), group=group)
+    # u16 latencies travel as bytes (gloo has no 16-bit integer type)
+    byt = lambda t: t.view(torch.uint8) if t.element_size() == 2 else t
+    dist.all_gather_into_tensor(byt(out_l), byt(pad(lat_seg)), group=group)
     dist.all_gather_into_tensor(out_r, pad(rel_seg), group=group)
     return out_l, out_r

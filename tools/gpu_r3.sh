@@ -18,3 +18,8 @@ if [ "${C5:-1}" = 1 ]; then
 timeout -k 10 300 python -u bench.py --config c5 --steps 20 --warmup 5 > gpurun_out/bench_${tag}_c5.json 2> gpurun_out/bench_${tag}_c5.err || { echo BENCH C5 FAILED; tail gpurun_out/bench_${tag}_c5.err; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/bench_${tag}_c5.json'));print('C5', round(d['value']), 'ms/step', round(d['ms_per_step'],4), 'fw', round(d['k4']['fw_table_ms'],3), 'cpu', d['cpu_baseline'] and round(d['cpu_baseline']['value'],1), d['cpu_baseline_fw'] and d['cpu_baseline_fw']['sample'])"
 fi
+if [ "${REHEARSE:-0}" = 1 ]; then
+# two ranks sharing this box's GPU over gloo: the strong-split path with the triangle payload
+SHD_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --config ${RCFG:-c3} --steps 5 --warmup 1 --gather-reps 1 > gpurun_out/bench_${tag}_rehearse.json 2> gpurun_out/bench_${tag}_rehearse.err || { echo REHEARSAL FAILED; tail -20 gpurun_out/bench_${tag}_rehearse.err; exit 1; }
+python -c "import json;d=json.loads(open('gpurun_out/bench_${tag}_rehearse.json').read().strip().splitlines()[-1]);print('rehearse', json.dumps(d['split']))"
+fi

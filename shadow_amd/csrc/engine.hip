@@ -457,8 +457,13 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 c->allocs.push_back(c->d_kd_ws);
                 if (hipMalloc((void**)&c->d_kd_next, sizeof(int)) != hipSuccess) return SHD_ROUTE_ENOMEM;
                 c->allocs.push_back(c->d_kd_next);
-                const void* fn = kd_dispatch(blk, [&](auto B) { return (const void*)sssp_delta_kernel<decltype(B)::value>; });
-                rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                for (int pk = 0; pk < 2 && !rc; pk++) {
+                    const void* fn = kd_dispatch(blk, [&](auto B) {
+                        return pk ? (const void*)kd_plan_rows_kernel<decltype(B)::value>
+                                  : (const void*)sssp_delta_kernel<decltype(B)::value>;
+                    });
+                    rc = hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                }
                 if (rc) return rc;
                 c->kd = 1; c->kd_block = blk; c->kd_lds = lds; c->kd_delta = delta; c->kd_qcap = qcap;
                 c->kd_walk = kd_dispatch(blk, [&](auto B) { return kd_walk_fits<decltype(B)::value>(n, qcap, c->kd_nrtab); }) ? 1 : 0;
@@ -598,14 +603,18 @@ DevDelta kd_args(const shd_route* c) {
 
 // one KD launch of ns sources (k.jobs: planned jobs, else d_src); `next` is zeroed
 int kd_launch(shd_route* c, DevDelta k, int* next, const int32_t* d_src, int ns, const int32_t* d_tgt, int nt,
-              int64_t ld, double* d_lat, double* d_rel, double* d_row_min, hipStream_t st) {
+              int64_t ld, double* d_lat, double* d_rel, double* d_row_min, hipStream_t st, bool planner = false) {
     if (ns <= 0) return SHD_ROUTE_OK;
     k.next = next;
     const int grid = std::min(ns, c->kd_slots);
     kd_dispatch(c->kd_block, [&](auto B) {
         constexpr int b = decltype(B)::value;
-        hipLaunchKernelGGL(sssp_delta_kernel<b>, dim3(grid), dim3(b), c->kd_lds, st, k, d_src, ns, d_tgt,
-                           nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kd_ws, c->kd_stride);
+        if (planner)
+            hipLaunchKernelGGL(kd_plan_rows_kernel<b>, dim3(grid), dim3(b), c->kd_lds, st, k, d_src, ns, d_tgt,
+                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kd_ws, c->kd_stride);
+        else
+            hipLaunchKernelGGL(sssp_delta_kernel<b>, dim3(grid), dim3(b), c->kd_lds, st, k, d_src, ns, d_tgt,
+                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kd_ws, c->kd_stride);
         return 0;
     });
     return hip_check(hipGetLastError());
@@ -1104,7 +1113,7 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, std::vector<s
     g.jobs = (const KDJob*)dj.p;
     g.drow = (const uint16_t*)dd.p; g.drow_out = (uint16_t*)dd.p; g.prow = (uint32_t*)dp.p; g.rstride = rs;
     g.done = (int*)dn.p + 1;
-    if ((rc = kd_launch(c, g, (int*)dn.p, nullptr, k, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr)))
+    if ((rc = kd_launch(c, g, (int*)dn.p, nullptr, k, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, true)))
         return rc;
     if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
     if ((rc = take_err(c))) return rc;
@@ -1757,8 +1766,9 @@ int shd_route_fw_table_async(shd_route_t* c, void* stream) {
     const int np = c->fw_np, nb = np / FW_T;
     const unsigned blocks = (unsigned)(((size_t)np * np + 255) / 256);
     hipLaunchKernelGGL(fw_init_kernel, dim3(blocks), dim3(256), 0, st, c->d_W, c->n, np, c->d_fwD);
-    // (SHD_ROUTE_FWREST=1: the 64 x 64 rest kernel with 4 x 4 blocks, for A/B runs)
-    static const int rest1 = getenv("SHD_ROUTE_FWREST") && atoi(getenv("SHD_ROUTE_FWREST")) == 1;
+    // rest kernel: 64 x 64 tiles with 4 x 4 register blocks (default); SHD_ROUTE_FWREST=2 selects
+    // the 128 x 128-region kernel with 8 x 8 blocks (C5 FW table 3.28 ms against 3.06, rocprof A/B)
+    static const int rest1 = !(getenv("SHD_ROUTE_FWREST") && atoi(getenv("SHD_ROUTE_FWREST")) == 2);
     const int nr = (nb + 1) / 2;
     for (int kb = 0; kb < nb; kb++) {
         // pivot tiles after the first are closed inside the previous fw_rest launch

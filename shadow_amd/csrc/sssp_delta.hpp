@@ -845,12 +845,12 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
     }
 }
 
+#define KD_KERNEL_PARAMS                                                                                   \
+    DevDelta g, const int* __restrict__ src, int ns, const int* __restrict__ tgt, int nt, long long ld,     \
+        double* __restrict__ lat_out, double* __restrict__ rel_out, double* __restrict__ row_min,          \
+        int* __restrict__ err, char* __restrict__ ws, size_t ws_stride
 template <int B>
-__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sssp_delta_kernel(DevDelta g, const int* __restrict__ src, int ns,
-                                                       const int* __restrict__ tgt, int nt, long long ld,
-                                                       double* __restrict__ lat_out, double* __restrict__ rel_out,
-                                                       double* __restrict__ row_min, int* __restrict__ err,
-                                                       char* __restrict__ ws, size_t ws_stride) {
+__device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PARAMS) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int n = g.n, nw = g.nw;
     constexpr int RR = kd_rr<B>();
@@ -1669,6 +1669,19 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         KD_STAMP(4);
         KD_FLUSH();
     }
+}
+
+// The table's rows (every planned or plain rows launch) ...
+template <int B>
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sssp_delta_kernel(KD_KERNEL_PARAMS) {
+    kd_rows_body<B>(g, src, ns, tgt, nt, ld, lat_out, rel_out, row_min, err, ws, ws_stride);
+}
+// ... and the planner's own rows (closeness and landmark rows, kept in a store, no output):
+// the same code under its own name, so kernel statistics of a rows launch are not averaged
+// with the planner's small launches
+template <int B>
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void kd_plan_rows_kernel(KD_KERNEL_PARAMS) {
+    kd_rows_body<B>(g, src, ns, tgt, nt, ld, lat_out, rel_out, row_min, err, ws, ws_stride);
 }
 
 template <int B>

@@ -9,22 +9,30 @@ import json
 import os
 import sys
 
-HOT = ("sssp_batch_kernel", "sssp_batch_rows_kernel", "path_attr_kernel", "sssp_k32_kernel", "sssp_rows_kernel", "sssp_k16", "sssp_delta_kernel")
+HOT = ("sssp_batch_kernel", "sssp_batch_rows_kernel", "path_attr_kernel", "sssp_k32_kernel", "sssp_rows_kernel", "sssp_k16", "sssp_delta_kernel",
+       "direct_rows_kernel", "fw_rest", "fw_diag", "fw_panel", "fw_parent", "fw_rows", "fw_inlist")
 
 
 def load(path):
+    """counter values per kernel name, from that kernel's dispatches of the largest grid only
+    (a smaller launch of the same kernel, e.g. the planner's rows before r03, is not a step)"""
+    rows = list(csv.DictReader(open(path)))
+    big = collections.defaultdict(int)
+    for r in rows:
+        big[r["Kernel_Name"]] = max(big[r["Kernel_Name"]], int(r["Grid_Size"]))
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
-    for r in csv.DictReader(open(path)):
-        agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for r in rows:
+        if int(r["Grid_Size"]) == big[r["Kernel_Name"]]:
+            agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return agg
 
 
-def main(src_dir, out, cfg, sources):
+def main(src_dir, out, cfg, sources, only=None):
     fetch = load(os.path.join(src_dir, "fetch_counter_collection.csv"))
     write = load(os.path.join(src_dir, "write_counter_collection.csv"))
     per = {}
     for k in set(fetch) | set(write):
-        if not any(h in k for h in HOT):
+        if not any(h in k for h in HOT) or (only and only not in k):
             continue
         f = fetch.get(k, {}).get("FETCH_SIZE", [0.0])
         w = write.get(k, {}).get("WRITE_SIZE", [0.0])
@@ -39,4 +47,4 @@ def main(src_dir, out, cfg, sources):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]))
+    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5] if len(sys.argv) > 5 else None)

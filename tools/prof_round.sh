@@ -32,4 +32,6 @@ pmc c4 FETCH_SIZE --config c4 --steps 2 --warmup 1
 pmc c4 WRITE_SIZE --config c4 --steps 2 --warmup 1
 pmc c3 FETCH_SIZE --config c3 --steps 2 --warmup 1
 pmc c3 WRITE_SIZE --config c3 --steps 2 --warmup 1
+pmc c5 FETCH_SIZE --config c5 --steps 3 --warmup 1
+pmc c5 WRITE_SIZE --config c5 --steps 3 --warmup 1
 echo prof done

@@ -556,7 +556,12 @@ def bench_c5(args, torch, dist, world, rank, dev, barrier):
     if rank != 0:
         return
     relax = float(n) ** 3
-    peak_relax = 256 * 4 * 32 * 2 * 2.4e9 / 2  # packed u16: 2 pairs per lane-op, add + min
+    # packed u16 min-plus: one v_pk_add_u16 + one v_pk_min_u16 per 2 relaxations, i.e. one packed
+    # instruction per relaxation.  Nominal: 32 lanes/cycle/SIMD at 2.4 GHz; measured on MI355X
+    # (tools/micro/pk_rate.hip, 8 waves/SIMD, independent chains: profiles/r03_pk_rate.txt):
+    # 35.8 T packed instructions/s (u32 adds 50.0 T/s), the roof the kernel can reach
+    peak_nominal = 256 * 4 * 32 * 2.4e9
+    peak_relax = 35.8e12
     res = {
         "metric": "source-paths/sec", "value": n * args.steps / dt, "unit": "source-paths/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
@@ -572,6 +577,8 @@ def bench_c5(args, torch, dist, world, rank, dev, barrier):
                      "model": "SURVEY 8(d) K3: read lat + r (16 B) and write lat + rel (16 B) per pair"},
         "k4": {"fw_table_ms": fw_s * 1e3, "grelax_per_s": relax / fw_s / 1e9,
                "peak_grelax_per_s": peak_relax / 1e9, "frac": relax / fw_s / peak_relax,
+               "peak_source": "measured packed-u16 VALU rate (tools/micro/pk_rate.hip, profiles/r03_pk_rate.txt)",
+               "nominal_peak_grelax_per_s": peak_nominal / 1e9, "frac_of_nominal": relax / fw_s / peak_nominal,
                "bound": "valu (packed u16 min-plus: v_pk_add_u16 + v_pk_min_u16 per 2 relaxations)",
                "fp64_equivalent_peak_grelax_per_s": 39.3e12 / 1e9,
                "fw_rows_ms": fwr_s * 1e3, "rows_verified_vs_oracle": fw_ok,

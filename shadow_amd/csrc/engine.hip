@@ -75,6 +75,7 @@ struct shd_route {
     double* d_kd_rtab = nullptr;    // distinct reliabilities
     int kd_nlight = 0, kd_nrtab = 1, kd_walk = 0, kd_packed = 0, kd_fused = 0;
     int has_vf = 0;  // some vertex has a packet-loss factor (else f_v is absent everywhere)
+    int vf_lossy = 0;  // some vertex factor is not exactly 1.0 (else every present f_v is a no-op)
     int kd_rone = -1;  // rtab index of exactly 1.0 (-1: none)
     char* d_kd_ws = nullptr;
     int* d_kd_next = nullptr;  // KD source queue counter
@@ -589,7 +590,9 @@ DevDelta kd_args(const shd_route* c) {
     k.row = c->d_row; k.orec = c->d_kd_orec; k.oridx = c->d_kd_oridx;
     k.nnz = c->nnz; k.lrow = c->d_kd_lstart; k.lrec = reinterpret_cast<const uint2*>(c->d_kd_lrec); k.nlight = c->kd_nlight;
     k.rtab = c->d_kd_rtab; k.nrtab = c->kd_nrtab; k.rone = c->kd_rone; k.walk = c->kd_walk; k.packed = c->kd_packed;
-    k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg; k.has_vf = c->has_vf; k.dflags = 0;
+    k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg; k.dflags = 0;
+    // a factor of exactly 1.0 multiplies as a no-op: KD reads vf only where one is not
+    k.has_vf = c->vf_lossy;
 #ifdef SHD_STAMPS
     if (const char* e = getenv("SHD_ROUTE_DFLAGS")) k.dflags = atoi(e);
 #endif
@@ -730,7 +733,11 @@ int shd_route_create(shd_route_t** out, const shd_graph_t* g, int device) {
     std::vector<double> vf(n, NAN);
     if (g->vertex_packetloss)
         for (int v = 0; v < n; v++)
-            if (!std::isnan(g->vertex_packetloss[v])) { vf[v] = (1.0f - g->vertex_packetloss[v]); c->has_vf = 1; }
+            if (!std::isnan(g->vertex_packetloss[v])) {
+                vf[v] = (1.0f - g->vertex_packetloss[v]);
+                c->has_vf = 1;
+                if (vf[v] != 1.0) c->vf_lossy = 1;
+            }
 
     int rc = SHD_ROUTE_OK;
     if (!rc) rc = upload(c, &c->d_row, row);
@@ -1203,7 +1210,8 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     auto P = std::make_unique<shd_route_plan>();
     P->c = c; P->world = world; P->rank = rank; P->ns_all = ns;
     const auto t_start = std::chrono::steady_clock::now();
-    double t_close = 0, t_land = 0, t_seeds = 0, t_store = 0, t_sched = 0, t_rk = 0, t_order = 0, t_hop = 0;  // SHD_ROUTE_PLAN_DEBUG stage times
+    double t_close = 0, t_land = 0, t_seeds = 0, t_store = 0, t_sched = 0, t_rk = 0, t_order = 0, t_hop = 0, t_loop0 = 0, t_alloc = 0, t_deps = 0;
+    int n_recomp = 0;  // SHD_ROUTE_PLAN_DEBUG stage times
     auto since = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
     const int n = c->n;
     const char* env = getenv("SHD_ROUTE_SEED");
@@ -1215,18 +1223,35 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         const int rc = ensure_close(c);
         if (rc) return rc;
         t_close = since();
-        // (closeness, vertex) pairs sorted in place: no indirection in the comparisons
-        std::vector<std::pair<double, int>> ord(n);
+        // rank by (closeness, vertex).  closeness is a mean of L integer distances, so L times
+        // it is an exact integer sum: a counting sort over the sums, vertices ascending within
+        // one (an std::sort of (double, int) pairs took ~3 ms at C4)
         rk.resize(n);
-        for (int v = 0; v < n; v++) ord[v] = {c->close[v], v};
-        std::sort(ord.begin(), ord.end());
-        for (int q = 0; q < n; q++) rk[ord[q].second] = q;
+        const double L = (double)std::min(n, 16);
+        bool integral = true;
+        long long smax = 0;
+        for (int v = 0; v < n && integral; v++) {
+            const double x = c->close[v] * L;
+            integral = x >= 0 && x < 1e8 && x == std::floor(x);
+            if (integral) smax = std::max(smax, (long long)x);
+        }
+        if (integral) {
+            std::vector<int> cnt((size_t)smax + 2, 0);
+            for (int v = 0; v < n; v++) cnt[(size_t)(c->close[v] * L) + 1]++;
+            for (long long x = 0; x <= smax; x++) cnt[x + 1] += cnt[x];
+            for (int v = 0; v < n; v++) rk[v] = cnt[(size_t)(c->close[v] * L)]++;
+        } else {
+            std::vector<std::pair<double, int>> ord(n);
+            for (int v = 0; v < n; v++) ord[v] = {c->close[v], v};
+            std::sort(ord.begin(), ord.end());
+            for (int q = 0; q < n; q++) rk[ord[q].second] = q;
+        }
         t_rk = since();
     }
     auto by_rank = [&](std::vector<int>& v) {  // positions by (vertex rank, position): counting sort
         std::vector<int> cnt(n + 1, 0), tmp(v.size());
         std::vector<int> sv(v);
-        std::sort(sv.begin(), sv.end());
+        if (!std::is_sorted(sv.begin(), sv.end())) std::sort(sv.begin(), sv.end());
         for (int p : sv) cnt[rk[src[p]] + 1]++;
         for (int x = 0; x < n; x++) cnt[x + 1] += cnt[x];
         for (int p : sv) tmp[cnt[rk[src[p]]]++] = p;
@@ -1317,13 +1342,21 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     const int nj = (int)job_pos.size(), nr = (int)P->row_pos.size();
     std::vector<KDJob> jobs;
     if (want && nj >= 2) {
+        // jobs renumbered in rank order (a job's seeds, of smaller rank, are settled before
+        // it), so that the passes below walk every per-job array in sequence
+        {
+            std::vector<int> jpos_of(ns, -1);
+            for (int j = 0; j < nj; j++) jpos_of[job_pos[j]] = j;
+            std::vector<int> order(job_pos);
+            by_rank(order);
+            std::vector<int> jr(nj);
+            for (int q = 0; q < nj; q++) jr[q] = job_row[jpos_of[order[q]]];
+            job_pos.swap(order);
+            job_row.swap(jr);
+        }
         std::vector<int> first(n, -1);  // first job of each source vertex
         for (int j = 0; j < nj; j++) if (first[src[job_pos[j]]] < 0) first[src[job_pos[j]]] = j;
-        std::vector<int> jpos_of(ns, -1);
-        for (int j = 0; j < nj; j++) if (jpos_of[job_pos[j]] < 0) jpos_of[job_pos[j]] = j;
-        // jobs in rank order: a job's seeds (smaller rank) are settled before it
-        std::vector<int> order(job_pos);
-        by_rank(order);
+        const std::vector<int>& order = job_pos;
         t_order = since();
         std::vector<int> lvl(nj, 0), slot(nj, -1), nsd(nj, 0);
         std::vector<std::array<int, KD_SEEDS>> seedjob(nj), su(nj), wr(nj);
@@ -1375,10 +1408,18 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // A row's seeds: its best kseeds available neighbour rows, then (if short) its best
         // two-hop rows (s -> x -> u, x of degree <= 256), each list in the order a full sort
         // of the candidates would give.  avail(u): u's row is a usable seed.
-        struct Choice { int m, nh; int arcs[KD_SEEDS]; Hop hop[KD_SEEDS]; };
+        // (the chosen arcs' head, weight and record are kept in the choice: the sequential
+        // pass below then reads no CSR array, whose random reads cost ~5 ms at C4)
+        struct Choice { int m, nh; int arcs[KD_SEEDS]; int u[KD_SEEDS], w[KD_SEEDS]; uint32_t rec[KD_SEEDS]; Hop hop[KD_SEEDS]; };
         auto choose = [&](int p, auto avail, Choice& C) {
             const int s = src[p];
             C.m = best_seeds(p, avail, kseeds, C.arcs);
+            for (int k = 0; k < C.m; k++) {
+                const int a = C.arcs[k];
+                C.u[k] = c->h_col[a];
+                C.w[k] = (int)c->h_w[a];
+                C.rec[k] = (uint32_t)s | ((uint32_t)c->h_ridx[a] << 16) | ((uint32_t)c->h_w[a] << 24);
+            }
             C.nh = 0;
             if (!two_hop || C.m >= kseeds) return;
             const int need = kseeds - C.m;
@@ -1392,7 +1433,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                     const int u = c->h_col[b];
                     if (u == s || u == x || rk[u] >= rk[s] || !avail(u)) continue;
                     bool dup = false;
-                    for (int k = 0; k < C.m; k++) dup = dup || c->h_col[C.arcs[k]] == u;
+                    for (int k = 0; k < C.m; k++) dup = dup || C.u[k] == u;
                     if (dup) continue;
                     const Hop h{c->h_w[a] + c->h_w[b] + c->close[u], u, (int)(c->h_w[a] + c->h_w[b]),
                                 (uint32_t)x | ((uint32_t)c->h_ridx[b] << 16) | ((uint32_t)c->h_w[b] << 24)};
@@ -1433,9 +1474,9 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             t_hop = since() - th0;
         }
         int nlev = 1, q = 0;
-        for (int p : order) {
-            const int j = jpos_of[p], s = src[p];
-            int arcs[KD_SEEDS];
+        t_loop0 = since();
+        for (int j = 0; j < nj; j++) {
+            const int p = job_pos[j], s = src[p];
             const int qi = q;
             const bool seedable = q++ >= nroot_min;
             Choice ch;
@@ -1443,13 +1484,12 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             if (seedable) {
                 bool ok = true;
                 const Choice& pc = pre[qi];
-                for (int k = 0; k < pc.m; k++) ok = ok && fl[c->h_col[pc.arcs[k]]] >= 0;
+                for (int k = 0; k < pc.m; k++) ok = ok && fl[pc.u[k]] >= 0;
                 for (int k = 0; k < pc.nh; k++) ok = ok && fl[pc.hop[k].u] >= 0;
                 if (ok) ch = pc;
-                else choose(p, [&](int u) { return fl[u] >= 0; }, ch);
+                else { choose(p, [&](int u) { return fl[u] >= 0; }, ch); n_recomp++; }
             }
             int m = ch.m;
-            for (int k = 0; k < m; k++) arcs[k] = ch.arcs[k];
             if (!seedable && nland > 0) {
                 // nearest landmarks by d(s, L) (undirected: d_L(s)), up to kseeds
                 std::vector<std::pair<double, int>> lc;
@@ -1473,12 +1513,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 }
                 nsd[j] = mk;
             }
-            for (int k = 0; k < m; k++) {
-                const int a = arcs[k], u = c->h_col[a];
-                su[j][k] = u;
-                wr[j][k] = (int)c->h_w[a];
-                srec[j][k] = (int)((uint32_t)s | ((uint32_t)c->h_ridx[a] << 16) | ((uint32_t)c->h_w[a] << 24));
-            }
+            for (int k = 0; k < m; k++) { su[j][k] = ch.u[k]; wr[j][k] = ch.w[k]; srec[j][k] = (int)ch.rec[k]; }
             for (int q2 = 0; q2 < ch.nh; q2++, m++) {
                 su[j][m] = ch.hop[q2].u; wr[j][m] = ch.hop[q2].off; srec[j][m] = (int)ch.hop[q2].rec;
             }
@@ -1503,6 +1538,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         bool ok = ntot > 0 &&
                   hipMalloc((void**)&P->d_drow, sizeof(uint16_t) * (size_t)rs * ntot) == hipSuccess &&
                   hipMalloc((void**)&P->d_prow, sizeof(uint32_t) * (size_t)rs * ntot) == hipSuccess;
+        t_alloc = since();
         if (ok && P->nland) {
             // landmark rows into the slots after the kept rows' (pads: unreached, no record)
             std::vector<uint16_t> hd((size_t)rs * P->nland, 0xFFFFu);
@@ -1547,25 +1583,46 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                     for (int k = 0; k < nsd[j]; k++)
                         if (lmseed[j][k] < 0) dep[fill[seedjob[j][k]]++] = j;
             }
-            std::vector<double> ready(nj, 0.0);
-            typedef std::pair<double, int> DI;
-            std::priority_queue<DI, std::vector<DI>, std::greater<DI>> cq, free_at;
-            for (int j = 0; j < nj; j++) if (!left[j]) cq.push({0.0, j});
-            for (int w = 0; w < W; w++) free_at.push({0.0, w});
+            t_deps = since();
+            // times in integer ticks of 1/100 row: the ready queue is a bucket queue (a row
+            // becomes ready strictly after the start of the row that releases it, so the
+            // queue's minimum only grows and every bucket is complete when it is reached;
+            // within a bucket, rows in job order).  A binary heap of (double, job) pairs took
+            // ~6 ms at C4.
+            auto tk = [](double x) { return (long long)std::llround(x * 100.0); };
+            const long long t_root = tk(root_cost), t_lm = tk(lm_cost), t_one = 100;
+            std::vector<long long> ready(nj, 0);
+            std::vector<std::vector<int>> bq(1);
+            size_t bq_n = 0;  // rows queued
+            for (int j = 0; j < nj; j++) if (!left[j]) { bq[0].push_back(j); bq_n++; }
+            typedef std::pair<long long, int> LI;
+            std::priority_queue<LI, std::vector<LI>, std::greater<LI>> free_at;
+            for (int w = 0; w < W; w++) free_at.push({0, w});
             std::vector<int> qorder;
             qorder.reserve(nj);
-            while (!cq.empty()) {
-                const DI f = free_at.top(); free_at.pop();
-                const DI jr = cq.top(); cq.pop();
-                const int j = jr.second;
-                const double t = !nsd[j] ? root_cost : lmseed[j][0] >= 0 ? lm_cost : 1.0;
-                const double start = std::max(f.first, jr.first);
+            size_t cur = 0, pos = 0;  // current bucket and the next row in it
+            while (bq_n) {
+                while (pos >= bq[cur].size()) {
+                    std::vector<int>().swap(bq[cur]);
+                    cur++; pos = 0;
+                    if (cur < bq.size() && bq[cur].size() > 1) std::sort(bq[cur].begin(), bq[cur].end());
+                }
+                const int j = bq[cur][pos++];
+                bq_n--;
+                const LI f = free_at.top(); free_at.pop();
+                const long long t = !nsd[j] ? t_root : lmseed[j][0] >= 0 ? t_lm : t_one;
+                const long long start = std::max(f.first, (long long)cur);
                 free_at.push({start + t, f.second});
                 qorder.push_back(j);
+                const long long rel = start + std::max(1ll, tk(flag_at * (double)t / 100.0));
                 for (int e = dbeg[j]; e < dbeg[j + 1]; e++) {
                     const int d = dep[e];
-                    ready[d] = std::max(ready[d], start + flag_at * t);
-                    if (--left[d] == 0) cq.push({ready[d], d});
+                    ready[d] = std::max(ready[d], rel);
+                    if (--left[d] == 0) {
+                        if ((size_t)ready[d] >= bq.size()) bq.resize((size_t)ready[d] + 1);
+                        bq[ready[d]].push_back(d);
+                        bq_n++;
+                    }
                 }
             }
             t_sched = since();
@@ -1578,6 +1635,8 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                         "seed choices (threads) %.2f ms, seeds done %.2f, store %.2f, schedule %.2f ms\n",
                         1e3 * t_close, 1e3 * t_rk, 1e3 * t_order, 1e3 * t_land, 1e3 * t_hop, 1e3 * t_seeds, 1e3 * t_store,
                         1e3 * t_sched);
+                fprintf(stderr, "  seq loop start %.2f (recomputed %d), alloc done %.2f, deps done %.2f\n", 1e3 * t_loop0, n_recomp,
+                        1e3 * t_alloc, 1e3 * t_deps);
             }
             jobs.resize(nj);
             int qi = 0;

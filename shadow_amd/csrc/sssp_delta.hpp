@@ -107,6 +107,7 @@ constexpr uint32_t KD_EVTAG = 0xFFFF0000u;  // ring record y of a tie event: v |
 typedef unsigned short kd_us2 __attribute__((ext_vector_type(2)));
 typedef double kd_d2 __attribute__((ext_vector_type(2)));
 typedef unsigned kd_u4 __attribute__((ext_vector_type(4)));
+typedef unsigned kd_u2 __attribute__((ext_vector_type(2)));
 
 struct DevDelta {
     int* next;                          // source queue counter (zeroed before each launch)
@@ -138,13 +139,16 @@ struct DevDelta {
     const double* __restrict__ vf;
     const double* __restrict__ self_w;
     const double* __restrict__ self_r;
-    int has_vf;                         // some vertex factor present (else vf is all NaN: not read)
+    int has_vf;                         // some vertex factor other than 1.0 (else every f_v is 1.0 or
+                                        // absent, a no-op in every product: vf is not read)
     int dflags;                         // diagnostic builds: 1 = skip the output-row stores
-    unsigned long long* dbg;            // SHD_STAMPS builds: 32 words per source
+    unsigned long long* dbg;            // SHD_STAMPS builds: KD_NACC words per source
 };
 
+constexpr int KD_NACC = 40;
 #ifdef SHD_STAMPS
-// 32 words per source: 0-4 phase stamps, 5 sweeps, 6 queued, 7 arcs, 8-11 summed sweep
+// KD_NACC words per source (32-35: pre-init: walk cycles of wave 0, barrier wait, pre-init
+// cycles of its first wave, rows pre-initialised): 0-4 phase stamps, 5 sweeps, 6 queued, 7 arcs, 8-11 summed sweep
 // parts, 12-15 phase C (sweeps, compute, store drain, barriers), 16-19 phase B parts
 // accumulated in LDS (sm->acc) and written out once per source: a global read-modify-
 // write inside the timed regions would drain the wave's vmcnt and distort them
@@ -155,7 +159,7 @@ struct DevDelta {
 #define KD_COUNT(slot, x) do { if (lane == 0 && (x)) atomicAdd(&sm->acc[slot], (unsigned long long)(x)); } while (0)
 #define KD_MARK() do { if (tid == 0) kd_t = __builtin_amdgcn_s_memtime(); } while (0)
 #define KD_ACC(slot) do { if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[slot] += t_ - kd_t; kd_t = t_; } } while (0)
-#define KD_FLUSH() do { lds_barrier(); if (g.dbg && i >= 0) for (int q_ = tid; q_ < 32; q_ += B) g.dbg[(size_t)i * 32 + q_] = sm->acc[q_]; lds_barrier(); if (tid < 32) sm->acc[tid] = 0; lds_barrier(); } while (0)
+#define KD_FLUSH() do { lds_barrier(); if (g.dbg && i >= 0) for (int q_ = tid; q_ < KD_NACC; q_ += B) g.dbg[(size_t)i * KD_NACC + q_] = sm->acc[q_]; lds_barrier(); if (tid < KD_NACC) sm->acc[tid] = 0; lds_barrier(); } while (0)
 #else
 #define KD_ACCP nullptr
 #define KD_OUT true
@@ -184,8 +188,25 @@ struct KDSmall {
     int jflag[3];       // phase C pointer jumping: "some pointer moved" per round (mod 3)
     KDJob job;          // the current job (kept in LDS: read where needed, not held in
                         // registers across phase A, whose expansion needs all of them)
+    // Pre-init (planned launches, B >= 1024): the next job is taken at the start of this
+    // row's output phases, and while most waves walk this row's paths the last KD_PREW
+    // waves stream the next row's seeds (HBM) into its parent records and a staged D0
+    KDJob njob;         // the next job (valid when njb >= 0)
+    int njb;            // its queue index (-1: not taken; the loop takes one as usual)
+    int npre;           // the next row's records and staged D0 are written (set after phase C)
+    int npre_ok;        // pre-init waves that completed
+    int wpar;           // which of the two per-workgroup record slices the current row uses
+    const KDJob* jobs;  // (the launch's job list, queue counter, row store and flags, for the
+    int* qnext;         //  non-inlined output phases)
+    const uint16_t* drow;
+    uint32_t* prow;
+    long long rstride;
+    int* done;
+    uint32_t* wsl[2];   // the two record slices of this workgroup
+    uint16_t* dstage;   // staged D0 of the next row (u16 x (n + 8))
+    int ns;
 #ifdef SHD_STAMPS
-    unsigned long long acc[32];
+    unsigned long long acc[KD_NACC];
 #endif
 };
 
@@ -230,6 +251,10 @@ struct KDLayout {
     }
 };
 constexpr int KD_MAXD = 32;           // phase C path walk: arcs held in registers
+#ifndef KD_PREW
+#define KD_PREW 0                     // waves pre-initialising the next row during the walk (0: off)
+#endif
+constexpr int KD_PRESPIN = 32;        // pre-init: polls of a seed's flag (s_sleep 8 each) before giving up
 constexpr int KD_WQ = 4;              // phase C path walk: targets per thread
 constexpr int KD_ONE = 254;           // phase C: rtab slot holding 1.0 (the source's own step)
 constexpr int KD_NAN = 255;           // phase C: rtab slot holding NaN (unreachable vertices)
@@ -240,10 +265,18 @@ constexpr int kd_rr() { return B >= 1024 ? KD_RR : 256; }
 // per-workgroup HBM slice: relv f64[n] | wpr u32[n + 8], the parent record of every vertex:
 // parent | ridx << 16 (| w << 24, packed arcs) of the parent arc (KD_SRC_MARK for the source)
 // | tie events
-// {p | ridx << 16 | w << 24, v} x n (seeded rows).  Seeded rows use relv as u32 keys.
+// {p | ridx << 16 | w << 24, v} x n (seeded rows) | a second record slice u32[n + 8] (rows
+// alternate between the two, so the next row's pre-init never writes the records the current
+// row may still read) | staged D0 u16[n + 8].  Seeded rows use relv as u32 keys.
 __host__ __device__ inline size_t kd_ws_stride(int n) {
+    return a16(sizeof(double) * n) + a16(sizeof(uint32_t) * (n + 8)) + a16(8 * (size_t)n) + 256 +
+           a16(sizeof(uint32_t) * (n + 8)) + a16(sizeof(uint16_t) * (n + 8));
+}
+// the second record slice and the staged D0 (pre-init), after relv | wpr | events
+__host__ __device__ inline size_t kd_ws_wpr1(int n) {
     return a16(sizeof(double) * n) + a16(sizeof(uint32_t) * (n + 8)) + a16(8 * (size_t)n) + 256;
 }
+__host__ __device__ inline size_t kd_ws_dstage(int n) { return kd_ws_wpr1(n) + a16(sizeof(uint32_t) * (n + 8)); }
 __host__ __device__ inline long long kd_row_stride(int n) { return ((long long)n + 2 + 7) & ~7ll; }
 
 // LDS-only workgroup barrier: outstanding global stores (output rows) stay in flight.
@@ -412,6 +445,108 @@ __device__ inline int kd_next_source(int* ctr, int* slot, int tid, bool all_queu
     return i;
 }
 
+// Pre-init of the next job (sm->njob), by the threads pt = 0 .. PT-1 of the last KD_PREW waves
+// while the other waves walk the current row's paths (LDS-bound; this is HBM-bound): the
+// seeded init's stream (the seeded branch of kd_rows_body) with D0 written to the staged
+// array instead of LDS, the parent records to the next row's own record array (its store
+// slot, or the record slice the current row does not use).  All or nothing: a wave whose
+// seeds are not ready after a short poll leaves it to the next row's own init.
+template <int B>
+__device__ inline void kd_preinit(const int n, const int pt, const int PT, int* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    KDSmall* sm = reinterpret_cast<KDSmall*>(smem);
+    const int lane = threadIdx.x & 63;
+    const int nseed = __builtin_amdgcn_readfirstlane(sm->njob.nseed);
+    const int s = __builtin_amdgcn_readfirstlane(sm->njob.s);
+    int* const done = sm->done;
+    int ok = 1;
+    if (lane == 0) {
+        for (int q = 0; q < nseed && ok; q++) {
+            const int sl = sm->njob.seed[q];
+            int spin = 0;
+            while (__hip_atomic_load(&done[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && spin < KD_PRESPIN) {
+                __builtin_amdgcn_s_sleep(8);
+                spin++;
+            }
+            ok = spin < KD_PRESPIN;
+        }
+        if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!__builtin_amdgcn_readfirstlane(ok)) return;
+    const int st = __builtin_amdgcn_readfirstlane(sm->njob.store);
+    uint32_t* const wpr = st >= 0 ? sm->prow + (size_t)st * sm->rstride : sm->wsl[sm->wpar ^ 1];
+    uint16_t* const dstg = sm->dstage;
+    int su[KD_SEEDS];
+    unsigned wsu[KD_SEEDS], rsu[KD_SEEDS];
+    const uint16_t* sdrow[KD_SEEDS];
+    const uint32_t* sprow[KD_SEEDS];
+#pragma unroll
+    for (int q = 0; q < KD_SEEDS; q++) {
+        const int sl = __builtin_amdgcn_readfirstlane(q < nseed ? sm->njob.seed[q] : 0);
+        wsu[q] = (unsigned)__builtin_amdgcn_readfirstlane(q < nseed ? sm->njob.wr[q] : 0) & 0xFFFFu;
+        su[q] = __builtin_amdgcn_readfirstlane(q < nseed ? sm->njob.u[q] : -1);
+        rsu[q] = (unsigned)__builtin_amdgcn_readfirstlane(q < nseed ? sm->njob.rec[q] : 0);
+        sdrow[q] = sm->drow + (size_t)sl * sm->rstride;
+        sprow[q] = sm->prow + (size_t)sl * sm->rstride;
+    }
+    // two groups of 4 vertices per lane and trip, all 4 * KD_SEEDS loads issued first (four
+    // waves alone must keep enough bytes in flight to finish within the walk)
+    auto load = [&](int v0, uint2 (&dq)[KD_SEEDS], uint4 (&pq)[KD_SEEDS]) __attribute__((always_inline)) {
+        const int vl = min(v0, n & ~3);
+#pragma unroll
+        for (int q = 0; q < KD_SEEDS; q++) {
+            if (q < nseed) {
+                const kd_u2 d2 = *(const KD_GLOBAL kd_u2*)(sdrow[q] + vl);
+                const kd_u4 p4 = *(const KD_GLOBAL kd_u4*)(sprow[q] + vl);
+                dq[q] = make_uint2(d2.x, d2.y);
+                pq[q] = make_uint4(p4.x, p4.y, p4.z, p4.w);
+            } else {
+                dq[q] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+                pq[q] = make_uint4(KD_NONE, KD_NONE, KD_NONE, KD_NONE);
+            }
+        }
+    };
+    auto comb = [&](int v0, const uint2 (&dq)[KD_SEEDS], const uint4 (&pq)[KD_SEEDS]) __attribute__((always_inline)) {
+        uint32_t dw[2], rw[4];
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            const int v = v0 + h;
+            unsigned dbest = 0xFFFFu, kbest = 0xFFFFFFFFu;
+            uint32_t rbest = KD_NONE;
+#pragma unroll
+            for (int q = 0; q < KD_SEEDS; q++) {
+                const uint32_t d2 = (h < 2) ? dq[q].x : dq[q].y;
+                const unsigned d = (h & 1) ? (d2 >> 16) : (d2 & 0xFFFFu);
+                const unsigned c = q < nseed ? min(0xFFFFu, wsu[q] + d) : 0xFFFFFu;
+                const uint32_t p = kd_comp(pq[q], h);
+                const uint32_t r = v == su[q] ? rsu[q] : p;
+                const uint32_t k = __builtin_amdgcn_perm(~r, r, 0x07010002u);  // (255-w) | p | ridx
+                if (c < dbest || (c == dbest && k < kbest)) { dbest = c; kbest = k; rbest = r; }
+            }
+            if (v >= n) dbest = 0xFFFFu;
+            if (v == s) rbest = KD_SRC_MARK;
+            if (h & 1) dw[h >> 1] |= dbest << 16;
+            else dw[h >> 1] = dbest;
+            rw[h] = rbest;
+        }
+        *(KD_GLOBAL kd_u2*)(dstg + v0) = kd_u2{dw[0], dw[1]};
+        *(KD_GLOBAL kd_u4*)(wpr + v0) = kd_u4{rw[0], rw[1], rw[2], rw[3]};
+    };
+    for (int v0 = 4 * pt; v0 <= n; v0 += 8 * PT) {
+        const int v1 = v0 + 4 * PT;
+        uint2 da[KD_SEEDS], db[KD_SEEDS];
+        uint4 pa[KD_SEEDS], pb[KD_SEEDS];
+        load(v0, da, pa);
+        load(v1, db, pb);
+        comb(v0, da, pa);
+        if (v1 <= n) comb(v1, db, pb);
+    }
+    wait_stores();
+    if (lane == 0) atomicAdd(&sm->npre_ok, 1);
+    (void)err;
+}
+
 // Phases C/D of one row (lat row, parent copy, reliability by walks or level sweeps, rel
 // row, row min), called once per row.  Not inlined, on purpose: see the call site.
 template <int B>
@@ -480,8 +615,19 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
         }
     }
     wait_stores();  // wpr of phase B visible to the whole workgroup
-    if (tid == 0) { sm->deep = 0; sm->rmin = kInfBits; }
+    // planned launches: the next job is taken here (queue order is unchanged: a job is still
+    // taken after every job it seeds from), so the pre-init waves below can stream its seeds
+    const bool queued = sm->jobs != nullptr;
+    if (tid == 0) {
+        sm->deep = 0; sm->rmin = kInfBits;
+        if (queued) sm->njb = atomicAdd(sm->qnext, 1);
+    }
     __syncthreads();
+    const int njb = queued ? __builtin_amdgcn_readfirstlane(sm->njb) : -1;
+    if (tid < 16 && njb >= 0) {
+        const int x = njb < sm->ns ? ((const KD_GLOBAL int*)(sm->jobs + njb))[tid] : (tid == 3 ? 0 : -1);
+        reinterpret_cast<int*>(&sm->njob)[tid] = x;  // (past the end: nseed = 0, no pre-init)
+    }
 
     KD_ACC(18);
     // dist is dead: its LDS becomes the parent array
@@ -599,7 +745,11 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
         // global load behind the previous group's stores); else over the target list
         const int lim = tsorted ? n : nt;
         const int rpar = (int)(((uintptr_t)rrow >> 3) & 1);
-        for (int j0 = tid; j0 < lim; j0 += KD_WQ * B) {
+        // with a seeded next job, the last KD_PREW waves pre-init it (below) and BW threads walk
+        const bool pre = KD_PREW > 0 && B >= 1024 && njb >= 0 && __builtin_amdgcn_readfirstlane(sm->njob.nseed) > 0;
+        const int BW = pre ? B - 64 * KD_PREW : B;
+        if (tid < BW) {
+        for (int j0 = tid; j0 < lim; j0 += KD_WQ * BW) {
             // KD_WQ targets per thread: independent parent chains in flight.  A chain that
             // reaches the source stays there (parv[s] = s, factor 1.0), so a step is two LDS
             // reads and a byte insert, and the wave stops when every chain is parked.
@@ -607,10 +757,10 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
             uint32_t pk[KD_WQ][KD_MAXD / 4];
 #pragma unroll
             for (int q = 0; q < KD_WQ; q++) {
-                const int j = j0 + q * B;
+                const int j = j0 + q * BW;
                 if (tsorted) {
                     // chains (0, 1) and (2, 3) are adjacent vertices: paired 16-B stores
-                    const int v = (j0 - tid) + (q >> 1) * 2 * B + 2 * tid + (q & 1);
+                    const int v = (j0 - tid) + (q >> 1) * 2 * BW + 2 * tid + (q & 1);
                     jq[q] = v < n ? tpos(v) : -1;
                     t2[q] = jq[q] >= 0 ? v : -1;
                 } else {
@@ -698,7 +848,23 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                 }
             }
         }
+#ifdef SHD_STAMPS
+        if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[32] += t_ - kd_t; kd_t = t_; }
+#endif
+        } else if (pre) {
+#ifdef SHD_STAMPS
+            const unsigned long long p0 = __builtin_amdgcn_s_memtime();
+#endif
+            kd_preinit<B>(n, tid - BW, 64 * KD_PREW, err);
+#ifdef SHD_STAMPS
+            if (tid == BW) sm->acc[34] += __builtin_amdgcn_s_memtime() - p0;
+#endif
+        }
         __syncthreads();
+#ifdef SHD_STAMPS
+        if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[33] += t_ - kd_t; kd_t = t_; }
+#endif
+        if (tid == 0 && pre) { sm->npre = sm->npre_ok == KD_PREW; sm->npre_ok = 0; }
         KD_ACC(13);
         KD_STAMP(3);
     }
@@ -886,7 +1052,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
     uint2* const evl = reinterpret_cast<uint2*>(ws + (size_t)blockIdx.x * ws_stride + a16(sizeof(double) * n) +
                                                 a16(sizeof(uint32_t) * (n + 8)));
 #ifdef SHD_STAMPS
-    if (tid < 32) sm->acc[tid] = 0;
+    if (tid < KD_NACC) sm->acc[tid] = 0;
     __syncthreads();
 #endif
     const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
@@ -922,29 +1088,42 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
     // sources take more and the launch ends within about one source of the mean
     // (a static stride ended with the workgroups holding ceil(ns / grid) sources)
     const bool queued = g.jobs != nullptr;
+    if (tid == 0) {
+        sm->njb = -1; sm->npre = 0; sm->npre_ok = 0; sm->wpar = 0;
+        sm->jobs = g.jobs; sm->qnext = g.next; sm->drow = g.drow; sm->prow = g.prow; sm->rstride = g.rstride;
+        sm->done = g.done; sm->ns = ns;
+        sm->wsl[0] = wslice;
+        sm->wsl[1] = reinterpret_cast<uint32_t*>(ws + (size_t)blockIdx.x * ws_stride + kd_ws_wpr1(n));
+        sm->dstage = reinterpret_cast<uint16_t*>(ws + (size_t)blockIdx.x * ws_stride + kd_ws_dstage(n));
+    }
+    // (the barriers of kd_next_source publish these)
+    // the next job: taken in the previous row's output phases (planned launches), else here
     for (int jb = queued ? kd_next_source(g.next, &sm->next, tid, true) : (int)blockIdx.x; jb < ns;
-         jb = kd_next_source(g.next, &sm->next, tid, queued)) {
+         jb = sm->njb >= 0 ? sm->njb : kd_next_source(g.next, &sm->next, tid, queued)) {
         if (tid < 16) {
             int x;
-            if (g.jobs) x = reinterpret_cast<const int*>(g.jobs + jb)[tid];
+            if (sm->njb >= 0) x = reinterpret_cast<const int*>(&sm->njob)[tid];
+            else if (g.jobs) x = reinterpret_cast<const int*>(g.jobs + jb)[tid];
             else x = tid == 0 ? jb : tid == 1 ? src[jb] : tid == 2 ? -1 : 0;  // row, s, store = -1, nseed = 0
             reinterpret_cast<int*>(&sm->job)[tid] = x;
         }
+        if (tid == 0) sm->wpar ^= 1;  // rows alternate between the two record slices
         __syncthreads();
+        if (tid == 0) sm->njb = -1;   // (every thread has read it: the increment above)
         const int i = sm->job.row, s = sm->job.s;
         {
             bool bad = s < 0 || s >= n || sm->job.nseed < 0 || sm->job.nseed > KD_SEEDS;
             for (int q = 0; q < KD_SEEDS; q++)
                 if (q < sm->job.nseed) bad = bad || sm->job.u[q] < 0 || sm->job.u[q] >= n || sm->job.seed[q] < 0;
             if (bad) {
-                if (tid == 0) raise_err(err, SHD_ROUTE_EINVAL);
+                if (tid == 0) { raise_err(err, SHD_ROUTE_EINVAL); sm->npre = 0; }
                 continue;
             }
         }
         // parent records: the row kept for later seeds is this source's own array
         auto wpr_of = [&]() __attribute__((always_inline)) {
             const int st = __builtin_amdgcn_readfirstlane(sm->job.store);
-            return st >= 0 ? g.prow + (size_t)st * g.rstride : wslice;
+            return st >= 0 ? g.prow + (size_t)st * g.rstride : sm->wsl[__builtin_amdgcn_readfirstlane(sm->wpar)];
         };
         const double fs = g.vf[s];
         const double cs = isnan(fs) ? 1.0 : 1.0 * fs;
@@ -960,7 +1139,16 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
         KD_ACC(9);
 #endif
         const bool seeded = __builtin_amdgcn_readfirstlane(sm->job.nseed) > 0;
-        if (seeded) {
+        if (seeded && __builtin_amdgcn_readfirstlane(sm->npre)) {
+#ifdef SHD_STAMPS
+            if (tid == 0) sm->acc[35] += 1;
+#endif
+            // pre-initialised during the previous row (kd_preinit): the parent records are in
+            // place, D0 comes from the staged array
+            const uint16_t* const dstg = sm->dstage;
+            for (int v0 = 8 * tid; v0 <= n; v0 += 8 * B)
+                *reinterpret_cast<uint4*>(dist + v0) = *reinterpret_cast<const uint4*>(dstg + v0);
+        } else if (seeded) {
             uint32_t* const wpr = wpr_of();
             SEED_VIEW();
             // the seeds' rows are ready: one relaxed poll of each flag, one agent-scope
@@ -1051,6 +1239,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
             dist[s] = 0;
             pend[s >> 6] = 1ull << (s & 63);
             wmin[s >> 6] = 0;
+            sm->npre = 0;  // (consumed: every thread read it before the barrier above)
         }
         lds_barrier();
 

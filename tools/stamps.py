@@ -35,7 +35,7 @@ lat = torch.empty((len(S), len(T)), dtype=torch.float64, device=dev)
 rel = torch.empty_like(lat)
 mn = torch.empty(len(S), dtype=torch.float64, device=dev)
 nwg = (len(S) + 7) // 8
-dbg = torch.zeros((len(S) + nwg) * 32, dtype=torch.int64, device=dev)
+dbg = torch.zeros((len(S) + nwg) * 40, dtype=torch.int64, device=dev)
 L.shd_route_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
 L.shd_route_debug_buffer(eng._h, C.c_void_p(dbg.data_ptr()))
 plan = eng.plan(S, a.world, a.rank) if a.plan else None
@@ -58,7 +58,7 @@ for rep in range(3):
 print(f"launch time (diag build, last rep): {e0.elapsed_time(e1):.3f} ms")
 if plan is not None:
     print("plan", plan.info)
-d_all = dbg.cpu().numpy().astype(np.int64).reshape(-1, 32 if eng.info["kernel"] == 4 else 8)
+d_all = dbg.cpu().numpy().astype(np.int64).reshape(-1, 40 if eng.info["kernel"] == 4 else 8)
 d = d_all[: len(S)]
 if eng.info["kernel"] == 2:
     flat = dbg.cpu().numpy().astype(np.int64)
@@ -91,6 +91,10 @@ if eng.info["kernel"] == 4:
         print(f"  {nm:14s} mean {ph[:, k].mean():10.0f} cyc  p50 {np.median(ph[:, k]):10.0f}  max {ph[:, k].max():10.0f}")
     tot = d[:, 4] - d[:, 0]
     print(f"  total          mean {tot.mean():10.0f} cyc")
+    pa = ph[:, 0]
+    q = np.percentile(pa, [50, 90, 99, 99.9])
+    print(f"  A percentiles p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} p99.9 {q[3]:.0f}; rows > 1M cyc: {(pa > 1e6).sum()}, "
+          f"their share of A cycles {pa[pa > 1e6].sum() / max(pa.sum(), 1):.3f}; top rows {np.argsort(pa)[-8:][::-1].tolist()}")
     print(f"  sweeps mean/max        {d[:, 5].mean():.1f} / {d[:, 5].max()}   C sweeps {d[:, 12].mean():.1f}")
     print(f"  queued vertices / n    {d[:, 6].mean() / g.n:.3f}")
     print(f"  arcs expanded / nnz    {d[:, 7].mean() / g.nnz:.3f}")
@@ -105,6 +109,8 @@ if eng.info["kernel"] == 4:
     for k, nm in [(11, "minreduce"), (8, "gather"), (9, "prep"), (10, "expand"), (16, "B.short"), (17, "B.long"),
                   (18, "lat row+drain"), (19, "par copy"), (13, "C.compute")]:
         print(f"  A.{nm:10s} mean {d[:, k].mean():10.0f} cyc  ({d[:, k].mean() / max(d[:, 5].mean(), 1):.0f}/sweep)")
+    print(f"  pre-init: walk (wave 0) {d[:, 32].mean():.0f}  barrier wait {d[:, 33].mean():.0f}  pre-init wave {d[:, 34].mean():.0f} cyc/row; "
+          f"rows started pre-initialised {d[:, 35].sum():.0f} of {len(d)}")
     t0 = d[:, 0] - d[:, 0].min()
     print(f"  start spread (cyc): p50 {np.median(t0):.0f} max {t0.max()}  end max {(d[:, 4] - d[:, 0].min()).max()}")
     sys.exit(0)

@@ -90,6 +90,8 @@ struct shd_route {
     std::vector<int> lm_v;
     std::vector<std::vector<double>> lm_d;
     std::vector<std::vector<uint32_t>> lm_p;
+    uint16_t* d_lm_drow = nullptr;  // the landmark rows in the row-store format (device)
+    uint32_t* d_lm_prow = nullptr;
     int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD
     // K4 (fw.hpp): u16 all-pairs table + dense u16 weights, Np x Np (Np = n rounded to 64)
     uint16_t* d_fwD = nullptr;
@@ -785,6 +787,8 @@ void shd_route_destroy(shd_route_t* c) {
     (void)hipSetDevice(c->device);
     if (c->d_keys) (void)hipFree(c->d_keys);
     if (c->d_fwkey) (void)hipFree(c->d_fwkey);
+    if (c->d_lm_drow) (void)hipFree(c->d_lm_drow);
+    if (c->d_lm_prow) (void)hipFree(c->d_lm_prow);
     for (void* p : c->allocs) (void)hipFree(p);
     delete c;
 }
@@ -1093,10 +1097,11 @@ namespace {
 // Exact rows of `verts` on the device for the planner: one unplanned KD launch whose jobs
 // write no output row (row -1) but keep their row in store slot k, the format seeded rows
 // read (u16 distances, 0xFFFF = unreached, and the engine tie-rule parent record
-// `parent | ridx << 16 | w << 24` of every vertex).  Copied back into d_out / p_out
-// (p_out nullable).  Blocks: the planner runs once per context, before any planned launch.
-int device_store_rows(shd_route* c, const std::vector<int>& verts, std::vector<std::vector<double>>& d_out,
-                      std::vector<std::vector<uint32_t>>* p_out) {
+// `parent | ridx << 16 | w << 24` of every vertex).  The store stays in dd / dp (device) and
+// is copied back into d_out / p_out.  Blocks: the planner runs once per context, before any
+// planned launch.
+int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, DevBuf& dp,
+                      std::vector<std::vector<double>>& d_out, std::vector<std::vector<uint32_t>>& p_out) {
     const int k = (int)verts.size(), n = c->n;
     if (k == 0) return SHD_ROUTE_OK;
     const long long rs = kd_row_stride(n);
@@ -1105,7 +1110,7 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, std::vector<s
         std::memset(&jobs[q], 0, sizeof(KDJob));
         jobs[q].row = -1; jobs[q].s = verts[q]; jobs[q].store = q; jobs[q].nseed = 0;
     }
-    DevBuf dj, dd, dp, dn;
+    DevBuf dj, dn;
     if (dj.alloc(sizeof(KDJob) * k) || dd.alloc(sizeof(uint16_t) * (size_t)rs * k) ||
         dp.alloc(sizeof(uint32_t) * (size_t)rs * k) || dn.alloc(sizeof(int) * (1 + (size_t)k)))
         return SHD_ROUTE_ENOMEM;
@@ -1125,77 +1130,63 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, std::vector<s
     if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
     if ((rc = take_err(c))) return rc;
     std::vector<uint16_t> hd((size_t)rs * k);
-    if (hipMemcpy(hd.data(), dd.p, sizeof(uint16_t) * hd.size(), hipMemcpyDeviceToHost) != hipSuccess)
+    std::vector<uint32_t> hp((size_t)rs * k);
+    if (hipMemcpy(hd.data(), dd.p, sizeof(uint16_t) * hd.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(hp.data(), dp.p, sizeof(uint32_t) * hp.size(), hipMemcpyDeviceToHost) != hipSuccess)
         return SHD_ROUTE_EDEVICE;
     d_out.assign(k, {});
+    p_out.assign(k, {});
     for (int q = 0; q < k; q++) {
         d_out[q].resize(n);
         for (int v = 0; v < n; v++) {
             const uint16_t x = hd[(size_t)q * rs + v];
             d_out[q][v] = x == 0xFFFFu ? INFINITY : (double)x;
         }
-    }
-    if (p_out) {
-        std::vector<uint32_t> hp((size_t)rs * k);
-        if (hipMemcpy(hp.data(), dp.p, sizeof(uint32_t) * hp.size(), hipMemcpyDeviceToHost) != hipSuccess)
-            return SHD_ROUTE_EDEVICE;
-        p_out->assign(k, {});
-        for (int q = 0; q < k; q++) (*p_out)[q].assign(hp.begin() + (size_t)q * rs, hp.begin() + (size_t)q * rs + n);
+        p_out[q].assign(hp.begin() + (size_t)q * rs, hp.begin() + (size_t)q * rs + n);
     }
     return SHD_ROUTE_OK;
 }
 
-// closeness estimate: mean distance from 16 pseudo-random landmarks (deterministic), their
-// rows computed on the device
-int ensure_close(shd_route* c) {
-    if (!c->close.empty()) return SHD_ROUTE_OK;
-    const int n = c->n, L = std::min(n, 16);
-    std::vector<int> lm;
-    uint64_t x = 0x243F6A8885A308D3ull;
-    while ((int)lm.size() < L) {
-        x += 0x9E3779B97F4A7C15ull;
-        uint64_t z = x;
-        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-        z ^= z >> 31;
-        const int v = (int)(z % (uint64_t)n);
-        if (std::find(lm.begin(), lm.end(), v) == lm.end()) lm.push_back(v);
-    }
-    std::vector<std::vector<double>> D;
-    const int rc = device_store_rows(c, lm, D, nullptr);
-    if (rc) return rc;
-    c->close.assign(n, 0.0);
-    for (int v = 0; v < n; v++) {
-        double sum = 0;
-        for (int k = 0; k < L; k++) sum += D[k][v];
-        c->close[v] = sum / L;
-    }
-    return SHD_ROUTE_OK;
-}
-
-// Landmark rows: the k most central vertices (closeness order), each row exactly as the
-// KD kernel computes it -- exact integer distances (u16) and the engine tie-rule parent
-// record of every vertex -- so that a row seeded from one is bit-identical to a row seeded
-// from any other device row.  One device launch, once per context.
-int ensure_landmarks(shd_route* c, int k) {
-    if ((int)c->lm_v.size() >= k) return SHD_ROUTE_OK;
-    int rc = ensure_close(c);
-    if (rc) return rc;
+// The planner's device rows, once per context, in one launch: the rows of the k highest-degree
+// vertices (the hubs of a BA-like topology; ties by id).  The first 16 give every vertex's
+// closeness estimate (its mean distance to them); all k are the landmark rows that seed the
+// plans' roots, kept on the device in the row-store format (a plan copies them device to
+// device).  (Before round 3: 16 pseudo-random closeness rows, then the 16 (64) most central
+// vertices' rows in a second launch.)
+int ensure_hub_rows(shd_route* c, int k) {
     const int n = c->n;
+    k = std::min(n, std::max(k, 16));
+    if ((int)c->lm_v.size() >= k) return SHD_ROUTE_OK;
     std::vector<int> ord(n);
     std::iota(ord.begin(), ord.end(), 0);
+    auto deg = [&](int v) { return c->h_row.empty() ? 0 : c->h_row[v + 1] - c->h_row[v]; };
     std::partial_sort(ord.begin(), ord.begin() + k, ord.end(), [&](int a, int b) {
-        return c->close[a] != c->close[b] ? c->close[a] < c->close[b] : a < b;
+        return deg(a) != deg(b) ? deg(a) > deg(b) : a < b;
     });
     std::vector<int> lv(ord.begin(), ord.begin() + k);
     std::vector<std::vector<double>> D;
     std::vector<std::vector<uint32_t>> Pr;
-    if ((rc = device_store_rows(c, lv, D, &Pr))) return rc;
+    DevBuf dd, dp;
+    int rc = device_store_rows(c, lv, dd, dp, D, Pr);
+    if (rc) return rc;
+    const int L = std::min(k, 16);
+    c->close.assign(n, 0.0);
+    for (int v = 0; v < n; v++) {
+        double sum = 0;
+        for (int q = 0; q < L; q++) sum += D[q][v];
+        c->close[v] = sum / L;
+    }
+    if (c->d_lm_drow) (void)hipFree(c->d_lm_drow);
+    if (c->d_lm_prow) (void)hipFree(c->d_lm_prow);
+    c->d_lm_drow = (uint16_t*)dd.p; dd.p = nullptr;
+    c->d_lm_prow = (uint32_t*)dp.p; dp.p = nullptr;
     c->lm_v = lv;
     c->lm_d = std::move(D);
     c->lm_p = std::move(Pr);
     return SHD_ROUTE_OK;
 }
+int ensure_close(shd_route* c) { return c->close.empty() ? ensure_hub_rows(c, 16) : SHD_ROUTE_OK; }
+int ensure_landmarks(shd_route* c, int k) { return ensure_hub_rows(c, k); }
 
 }  // namespace
 
@@ -1219,8 +1210,12 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                       ns >= 2 && !c->h_row.empty();
     // closeness rank of every vertex: a row may only be seeded by rows of smaller rank
     std::vector<int> rk;
+    // landmark rows (below): 16 for 1024-thread plans, 64 for 256-thread ones; computed in the
+    // same device launch as the closeness rows (ensure_hub_rows)
+    int nland = c->multigraph ? 0 : std::min(c->kd_block >= 1024 ? 16 : 64, n);
+    if (const char* e = getenv("SHD_ROUTE_LANDMARKS")) nland = c->multigraph ? 0 : std::max(0, std::min(atoi(e), n));
     if (want) {
-        const int rc = ensure_close(c);
+        const int rc = ensure_hub_rows(c, nland);
         if (rc) return rc;
         t_close = since();
         // rank by (closeness, vertex).  closeness is a mean of L integer distances, so L times
@@ -1392,8 +1387,6 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // (C3, 1024 roots over 256-thread rows: 16/32/64/256 landmarks 2.90/2.89/2.80/2.76 ms;
         // C4's 256 roots are 0.5% of its rows: 16 and 64 measure the same, and each landmark
         // is a host Dijkstra of the plan (~40 ms at C4))
-        int nland = c->multigraph ? 0 : std::min(c->kd_block >= 1024 ? 16 : 64, n);
-        if (const char* e = getenv("SHD_ROUTE_LANDMARKS")) nland = c->multigraph ? 0 : std::max(0, std::min(atoi(e), n));
         if (nland > 0) {
             const double t0 = since();
             const int rc = ensure_landmarks(c, nland);
@@ -1456,7 +1449,8 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // seed-chain depth cap); the sequential pass keeps a precomputed choice when every
         // row in it is usable -- then it is exactly the choice over the usable rows -- and
         // recomputes the row otherwise.
-        std::vector<Choice> pre(order.size());
+        // (not value-initialised: the worker threads first-touch their own pages)
+        std::unique_ptr<Choice[]> pre(new Choice[order.size()]);
         {
             const double th0 = since();
             const int nq = (int)order.size();
@@ -1540,19 +1534,12 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                   hipMalloc((void**)&P->d_prow, sizeof(uint32_t) * (size_t)rs * ntot) == hipSuccess;
         t_alloc = since();
         if (ok && P->nland) {
-            // landmark rows into the slots after the kept rows' (pads: unreached, no record)
-            std::vector<uint16_t> hd((size_t)rs * P->nland, 0xFFFFu);
-            std::vector<uint32_t> hp((size_t)rs * P->nland, KD_NONE);
-            for (int l = 0; l < P->nland; l++)
-                for (int v = 0; v < n; v++) {
-                    const double d = c->lm_d[l][v];
-                    hd[(size_t)l * rs + v] = d < 65535.0 ? (uint16_t)d : (uint16_t)0xFFFFu;
-                    hp[(size_t)l * rs + v] = c->lm_p[l][v];
-                }
-            ok = hipMemcpy(P->d_drow + (size_t)rs * P->nslots, hd.data(), sizeof(uint16_t) * hd.size(),
-                           hipMemcpyHostToDevice) == hipSuccess &&
-                 hipMemcpy(P->d_prow + (size_t)rs * P->nslots, hp.data(), sizeof(uint32_t) * hp.size(),
-                           hipMemcpyHostToDevice) == hipSuccess;
+            // landmark rows into the slots after the kept rows', device to device (the rows are
+            // in the store format already, pads included)
+            ok = hipMemcpy(P->d_drow + (size_t)rs * P->nslots, c->d_lm_drow, sizeof(uint16_t) * (size_t)rs * P->nland,
+                           hipMemcpyDeviceToDevice) == hipSuccess &&
+                 hipMemcpy(P->d_prow + (size_t)rs * P->nslots, c->d_lm_prow, sizeof(uint32_t) * (size_t)rs * P->nland,
+                           hipMemcpyDeviceToDevice) == hipSuccess;
         }
         t_store = since();
         if (ok) {
@@ -1591,38 +1578,45 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             // ~6 ms at C4.
             auto tk = [](double x) { return (long long)std::llround(x * 100.0); };
             const long long t_root = tk(root_cost), t_lm = tk(lm_cost), t_one = 100;
+            // buckets as singly linked lists through one array (no allocation per bucket): a
+            // bucket's rows are sorted by job when it is reached
             std::vector<long long> ready(nj, 0);
-            std::vector<std::vector<int>> bq(1);
+            std::vector<int> bhead(1024, -1), bnext(nj, -1), cur_b;
+            auto push = [&](long long t, int j) {
+                if ((size_t)t >= bhead.size()) bhead.resize(std::max((size_t)t + 1, 2 * bhead.size()), -1);
+                bnext[j] = bhead[t];
+                bhead[t] = j;
+            };
             size_t bq_n = 0;  // rows queued
-            for (int j = 0; j < nj; j++) if (!left[j]) { bq[0].push_back(j); bq_n++; }
+            for (int j = nj - 1; j >= 0; j--) if (!left[j]) { push(0, j); bq_n++; }
             typedef std::pair<long long, int> LI;
             std::priority_queue<LI, std::vector<LI>, std::greater<LI>> free_at;
             for (int w = 0; w < W; w++) free_at.push({0, w});
             std::vector<int> qorder;
             qorder.reserve(nj);
-            size_t cur = 0, pos = 0;  // current bucket and the next row in it
+            long long cur = -1;
+            size_t pos = 0;
             while (bq_n) {
-                while (pos >= bq[cur].size()) {
-                    std::vector<int>().swap(bq[cur]);
-                    cur++; pos = 0;
-                    if (cur < bq.size() && bq[cur].size() > 1) std::sort(bq[cur].begin(), bq[cur].end());
+                while (pos >= cur_b.size()) {  // next non-empty bucket
+                    cur++;
+                    cur_b.clear();
+                    pos = 0;
+                    if ((size_t)cur < bhead.size())
+                        for (int j = bhead[cur]; j >= 0; j = bnext[j]) cur_b.push_back(j);
+                    if (cur_b.size() > 1) std::sort(cur_b.begin(), cur_b.end());
                 }
-                const int j = bq[cur][pos++];
+                const int j = cur_b[pos++];
                 bq_n--;
                 const LI f = free_at.top(); free_at.pop();
                 const long long t = !nsd[j] ? t_root : lmseed[j][0] >= 0 ? t_lm : t_one;
-                const long long start = std::max(f.first, (long long)cur);
+                const long long start = std::max(f.first, cur);
                 free_at.push({start + t, f.second});
                 qorder.push_back(j);
                 const long long rel = start + std::max(1ll, tk(flag_at * (double)t / 100.0));
                 for (int e = dbeg[j]; e < dbeg[j + 1]; e++) {
                     const int d = dep[e];
                     ready[d] = std::max(ready[d], rel);
-                    if (--left[d] == 0) {
-                        if ((size_t)ready[d] >= bq.size()) bq.resize((size_t)ready[d] + 1);
-                        bq[ready[d]].push_back(d);
-                        bq_n++;
-                    }
+                    if (--left[d] == 0) { push(ready[d], d); bq_n++; }
                 }
             }
             t_sched = since();

@@ -255,7 +255,7 @@ constexpr int KD_MAXD = 32;           // phase C path walk: arcs held in registe
 #define KD_PREW 0                     // waves pre-initialising the next row during the walk (0: off)
 #endif
 constexpr int KD_PRESPIN = 32;        // pre-init: polls of a seed's flag (s_sleep 8 each) before giving up
-constexpr int KD_WQ = 4;              // phase C path walk: targets per thread
+constexpr int KD_WQ = 2;              // phase C path walk: targets per thread (4 measured 1% slower at C4: its registers put 39 VGPRs of the output function in callee-saved ranges, saved to scratch and restored around every row; 2: 13)
 constexpr int KD_ONE = 254;           // phase C: rtab slot holding 1.0 (the source's own step)
 constexpr int KD_NAN = 255;           // phase C: rtab slot holding NaN (unreachable vertices)
 constexpr int KD_RR = 512;  // parent-record ring slots (1024-thread workgroups; smaller ones use 256)

@@ -38,7 +38,7 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
-CFG_INDEX = {"c2": 1, "c3": 2, "c4": 3, "c5": 4}
+CFG_INDEX = {"c2": 1, "c3": 2, "c4": 3, "c5": 4, "c2f": 1, "c3f": 2}
 
 
 def b_src(n, nnz, nt):
@@ -192,7 +192,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=25)  # C4: ~1.2 s timed
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c5", "c2f", "c3f"])
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"])
     ap.add_argument("--allgather", action="store_true", help="strong: all-gather lat+rel shards in every step")
     ap.add_argument("--gather-reps", type=int, default=2, help="strong, N>1: separately timed all-gathers")
@@ -392,7 +392,8 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": f"{g.name}: Barabasi-Albert Internet-like topology, all-pairs latency/reliability "
-                        f"table (BASELINE.json configs[{CFG_INDEX[args.config]}])",
+                        f"table (BASELINE.json configs[{CFG_INDEX[args.config]}]"
+                        + (", two-decimal fractional latencies)" if args.config.endswith("f") else ")"),
             "n_vertices": n, "n_edges": g.m, "n_edges_nonloop": g.m_nonloop, "csr_arcs": nnz,
             "sources_total": total_src, "sources_per_gpu": ns, "targets": nt,
             "table_bytes": 16 * total_src * nt,
@@ -411,7 +412,7 @@ def main():
             "kernel": {0: "sssp_rows_kernel", 1: "sssp_k32_kernel",
                        2: ("sssp_batch_rows_kernel" if eng.info["reserved"] == 1
                            else "sssp_batch_kernel+path_attr_kernel"),
-                       4: "sssp_delta_kernel"}.get(eng.info["kernel"], str(eng.info["kernel"])),
+                       4: "sssp_delta_kernel", 5: "sssp_f64d_kernel"}.get(eng.info["kernel"], str(eng.info["kernel"])),
             "model": "compulsory bytes per launch = the lat + rel output rows (16 B per source-target pair); "
                      "achieved = those bytes / the rows kernel's HIP-event time; traffic = PMC HBM bytes per "
                      "launch (profiles/), traffic_frac = traffic / kernel time / peak",

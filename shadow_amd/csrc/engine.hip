@@ -11,6 +11,7 @@
 #include <queue>
 #include <thread>
 #include "sssp_f64.hpp"
+#include "sssp_f64d.hpp"
 #include "sssp_k32.hpp"
 #include "sssp_batch.hpp"
 #include "path_attr.hpp"
@@ -92,7 +93,14 @@ struct shd_route {
     std::vector<std::vector<uint32_t>> lm_p;
     uint16_t* d_lm_drow = nullptr;  // the landmark rows in the row-store format (device)
     uint32_t* d_lm_prow = nullptr;
-    int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD
+    int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD, 5 KF
+    // KF (fractional latencies, LDS-resident f64 delta-stepping)
+    int kf_block = 0, kf_slots = 0;
+    size_t kf_lds = 0;
+    double kf_delta = 1.0;
+    int kf_nrtab = 0;
+    uint8_t* d_kf_rix = nullptr;
+    double* d_kf_rtab = nullptr;
     // K4 (fw.hpp): u16 all-pairs table + dense u16 weights, Np x Np (Np = n rounded to 64)
     uint16_t* d_fwD = nullptr;
     uint32_t* d_fwinl = nullptr;  // K4 parent search: sorted in-arc keys per vertex (np x np)
@@ -248,7 +256,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 const std::vector<int>& col_in, const std::vector<double>& w_in) {
     const int n = c->n;
     const char* force = getenv("SHD_ROUTE_KERNEL");
-    if (force && !strcmp(force, "f64")) return SHD_ROUTE_OK;
+    if (force && (!strcmp(force, "f64") || !strcmp(force, "kf"))) return SHD_ROUTE_OK;
     if (force && !*force) force = nullptr;
     if (!c->integer_w || n > 65535 || c->multigraph) return SHD_ROUTE_OK;
     for (int a = 0; a < c->nnz; a++) if (w[a] > 65535.0) return SHD_ROUTE_OK;
@@ -652,6 +660,58 @@ const char* shd_route_strerror(int code) {
     }
 }
 
+// KF eligibility + device arrays (graphs the integer kernels do not take): per in-arc index
+// of its 1 - loss in a table of the distinct values, bucket width, block size.  Fits when
+// the per-source LDS state does and every thread holds at most 16 vertices in the level
+// passes (n <= 16 B).
+int prepare_kf(shd_route* c, const std::vector<int>& row_in, const std::vector<int>& col_in,
+               const std::vector<double>& w_in, const std::vector<double>& r_in) {
+    const int n = c->n;
+    const char* force = getenv("SHD_ROUTE_KERNEL");
+    if (force && *force && strcmp(force, "kf") && strcmp(force, "auto")) return SHD_ROUTE_OK;
+    if (c->nnz == 0 || n > 65535) return SHD_ROUTE_OK;
+    std::vector<double> rtab;
+    std::vector<uint8_t> rix(c->nnz);
+    {
+        std::vector<std::pair<uint64_t, int>> keyed(c->nnz);
+        for (int a = 0; a < c->nnz; a++) {
+            uint64_t bits;
+            std::memcpy(&bits, &r_in[a], 8);
+            keyed[a] = {bits, a};
+        }
+        std::sort(keyed.begin(), keyed.end());
+        for (int q = 0; q < c->nnz; q++) {
+            if (q == 0 || keyed[q].first != keyed[q - 1].first) {
+                if ((int)rtab.size() == 254) return SHD_ROUTE_OK;  // (255 marks unreachable)
+                double x;
+                std::memcpy(&x, &keyed[q].first, 8);
+                rtab.push_back(x);
+            }
+            rix[keyed[q].second] = (uint8_t)(rtab.size() - 1);
+        }
+    }
+    int blk = 0;
+    size_t lds = 0;
+    if (n <= 16 * 256 && kf_lds_bytes<256>(n) <= kLdsBudget / 4) { blk = 256; lds = kf_lds_bytes<256>(n); }
+    else if (n <= 16 * 1024 && kf_lds_bytes<1024>(n) <= kLdsBudget) { blk = 1024; lds = kf_lds_bytes<1024>(n); }
+    if (!blk) return SHD_ROUTE_OK;
+    std::vector<double> ws(w_in.begin(), w_in.end());
+    const size_t k = ws.size() * 12 / 100;
+    std::nth_element(ws.begin(), ws.begin() + k, ws.end());
+    double delta = ws[k];
+    if (const char* e = getenv("SHD_ROUTE_KFDELTA")) delta = atof(e);
+    if (!(delta > 0.0) || std::isinf(delta)) delta = c->min_w > 0 ? c->min_w : 1.0;
+    int rc = upload(c, &c->d_kf_rix, rix);
+    if (!rc) rc = upload(c, &c->d_kf_rtab, rtab);
+    if (!rc) rc = hip_check(hipFuncSetAttribute(blk == 256 ? (const void*)sssp_f64d_kernel<256> : (const void*)sssp_f64d_kernel<1024>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (rc) return rc;
+    c->kf_block = blk; c->kf_lds = lds; c->kf_delta = delta; c->kf_nrtab = (int)rtab.size();
+    c->kf_slots = 256 * std::max(1, std::min((int)(kLdsBudget / lds), 1024 / blk));
+    c->sel = 5;
+    return SHD_ROUTE_OK;
+}
+
 int shd_route_create(shd_route_t** out, const shd_graph_t* g, int device) {
     if (!out || !g) return SHD_ROUTE_EINVAL;
     *out = nullptr;
@@ -774,6 +834,9 @@ int shd_route_create(shd_route_t** out, const shd_graph_t* g, int device) {
     }
     if (!rc) rc = prepare_k32(c, row, col, w, eid, c->directed ? row_in : row, c->directed ? col_in : col,
                               c->directed ? w_in : w);
+    if (!rc && c->sel == 0)
+        rc = prepare_kf(c, c->directed ? row_in : row, c->directed ? col_in : col, c->directed ? w_in : w,
+                        c->directed ? r_in : r);
     if (rc) {
         shd_route_destroy(c);
         return rc;
@@ -808,7 +871,7 @@ int shd_route_get_info(const shd_route_t* c, shd_route_info_t* info) {
     info->kernel = c->sel;
     info->dist_bound = c->k32_bound;
     info->block = c->sel == 2 ? KB_BLOCK : c->sel == 3 ? 1024 : c->sel == 4 ? c->kd_block
-                : c->sel == 1 ? c->k32_block : kBlock;
+                : c->sel == 1 ? c->k32_block : c->sel == 5 ? c->kf_block : kBlock;
     info->reserved = c->sel == 4 ? c->kd_delta : c->sel == 2 ? c->kb_fused : 0;
     info->device_bytes = c->device_bytes;
     info->min_edge_latency = c->min_w;
@@ -903,6 +966,22 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
                                (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
         else
             hipLaunchKernelGGL(sssp_k32_kernel<1024>, dim3(grid), dim3(1024), c->k32_lds, st, k, d_src, ns, d_tgt, nt,
+                               (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
+        return hip_check(hipGetLastError());
+    }
+    if (c->sel == 5 && !(dispatch && c->prefer_direct)) {
+        DevF64D k;
+        k.n = c->n; k.nw = (c->n + 63) / 64; k.delta = c->kf_delta;
+        k.row = c->d_row; k.col = c->d_col; k.w = c->d_w;
+        k.row_in = c->d_row_in; k.col_in = c->d_col_in; k.w_in = c->d_w_in;
+        k.rix_in = c->d_kf_rix; k.rtab = c->d_kf_rtab; k.nrtab = c->kf_nrtab;
+        k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;
+        const int grid = std::min(ns, c->kf_slots);
+        if (c->kf_block == 256)
+            hipLaunchKernelGGL(sssp_f64d_kernel<256>, dim3(grid), dim3(256), c->kf_lds, st, k, d_src, ns, d_tgt, nt,
+                               (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
+        else
+            hipLaunchKernelGGL(sssp_f64d_kernel<1024>, dim3(grid), dim3(1024), c->kf_lds, st, k, d_src, ns, d_tgt, nt,
                                (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
         return hip_check(hipGetLastError());
     }
@@ -1596,6 +1675,10 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             qorder.reserve(nj);
             long long cur = -1;
             size_t pos = 0;
+            if (getenv("SHD_ROUTE_SCHED") && atoi(getenv("SHD_ROUTE_SCHED")) == 0) {  // A/B: plain rank order
+                for (int j = 0; j < nj; j++) qorder.push_back(j);
+                bq_n = 0;
+            }
             while (bq_n) {
                 while (pos >= cur_b.size()) {  // next non-empty bucket
                     cur++;

@@ -141,12 +141,24 @@ def complete_graph(n: int, seed: int, name: str = "complete") -> Graph:
                  vertex_packetloss=np.zeros(n), name=name)
 
 
+def fractional(g: Graph, seed: int = 0, name: Optional[str] = None) -> Graph:
+    """The same topology with two-decimal latencies (the format of the reference's own
+    resource/topology.graphml.xml.xz, e.g. 2293.85 ms): latency + U{0..99} / 100.  No
+    integer kernel applies; the fractional path (KF, or the generic f64 kernel) does."""
+    rng = np.random.default_rng(10_000 + seed)
+    lat = g.latency + rng.integers(0, 100, size=g.m) / 100.0
+    return dataclasses.replace(g, latency=lat, name=name or (g.name + "_frac"))
+
+
 CONFIGS = {
     # name: (builder, kwargs)  -- BASELINE.md section 3
     "c2": lambda vloss=False: internet_like(2000, 5, 1, vloss=vloss, name="c2_ba2k"),
     "c3": lambda vloss=False: internet_like(10000, 4, 2, vloss=vloss, hosts=27000, name="c3_ba10k_tor"),
     "c4": lambda vloss=False: internet_like(50000, 10, 3, exact_edges=500000, vloss=vloss, name="c4_as50k"),
     "c5": lambda vloss=False: complete_graph(4000, 4, name="c5_k4000"),
+    # fractional-latency variants of C2 / C3 (VERDICT r02 item 9: no integer kernel applies)
+    "c2f": lambda vloss=False: fractional(internet_like(2000, 5, 1, vloss=vloss, name="c2_ba2k"), 1),
+    "c3f": lambda vloss=False: fractional(internet_like(10000, 4, 2, vloss=vloss, hosts=27000, name="c3_ba10k_tor"), 2),
 }
 
 

@@ -22,10 +22,10 @@ def route():
     return r
 
 
-KERNEL_ID = {"f64": 0, "k32": 1, "kb": 2, "k16": 3, "kd": 4}
+KERNEL_ID = {"f64": 0, "k32": 1, "kb": 2, "k16": 3, "kd": 4, "kf": 5}
 
 
-@pytest.fixture(params=["auto", "kd", "k32", "f64"])  # K16: diagnostic build only
+@pytest.fixture(params=["auto", "kd", "k32", "f64", "kf"])  # K16: diagnostic build only
 def kernel(request, monkeypatch):
     """Run a test on the auto-selected kernel and on each forced kernel."""
     if request.param == "auto":
@@ -203,5 +203,8 @@ def test_kernel_selection(route):
     eng = route.RouteEngine(g)
     assert eng.info["kernel"] == 2 and 0 < eng.info["dist_bound"] < 65535
     g2 = internet_like(300, 2, seed=3)
-    g2.latency = g2.latency + 0.25  # fractional -> generic f64 kernel
-    assert route.RouteEngine(g2).info["kernel"] == 0
+    g2.latency = g2.latency + 0.25  # fractional -> KF (LDS-resident f64 delta-stepping)
+    assert route.RouteEngine(g2).info["kernel"] == 5
+    g3 = internet_like(20000, 2, seed=3)
+    g3.latency = g3.latency + 0.25  # fractional, past KF's LDS -> the generic f64 kernel
+    assert route.RouteEngine(g3).info["kernel"] == 0

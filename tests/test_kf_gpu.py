@@ -1,0 +1,124 @@
+"""KF (fractional-latency delta-stepping, sssp_f64d.hpp) against the oracle and the generic
+f64 kernel.  Latency bit-exact (any relaxation order reaches the same left fold);
+reliability bit-exact against the oracle's engine tie rule (ORC_TIE_MINKEY) with unit or
+absent vertex factors, within REL_TOL with vertex loss (f_t multiplied last)."""
+import numpy as np
+import pytest
+
+from shadow_amd.graph import Graph, config, fractional, internet_like
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def route():
+    from shadow_amd import route as r
+    r.load_library()
+    return r
+
+
+def _rows(route, g, src, tgt, kernel, monkeypatch):
+    monkeypatch.setenv("SHD_ROUTE_KERNEL", kernel)
+    eng = route.RouteEngine(g)
+    return eng, eng.rows(src, tgt, dispatch=False)
+
+
+@pytest.mark.parametrize("cfg,step", [("c2f", 7), ("c3f", 211)])
+def test_kf_fractional_bitexact(route, oracle_mod, monkeypatch, cfg, step):
+    g = config(cfg)
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 5  # KF is the fractional path at this size
+    src = np.arange(0, g.n, step, dtype=np.int32)
+    tgt = g.targets()
+    lat, rel, mn = eng.rows(src, tgt, dispatch=False)
+    og = oracle_mod.OracleGraph(g)
+    olat, orel, _, _ = og.source_rows(src, tgt, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(rel, orel)
+    assert np.array_equal(mn, olat.min(axis=1))
+
+
+def test_kf_many_sources_per_workgroup(route, monkeypatch):
+    # every source of C2f in one launch (about two per workgroup) against KF one source per
+    # workgroup: per-source state is reset between sources
+    g = config("c2f")
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    eng = route.RouteEngine(g)
+    tgt = g.targets()
+    lat, rel, mn = eng.rows(tgt, tgt, dispatch=False)
+    for part in (tgt[:200], tgt[1000:1100]):
+        l2, r2, m2 = eng.rows(part, tgt, dispatch=False)
+        assert np.array_equal(l2, lat[part]) and np.array_equal(r2, rel[part]) and np.array_equal(m2, mn[part])
+
+
+def test_kf_equals_generic_f64(route, monkeypatch):
+    g = config("c2f")
+    src = np.arange(0, g.n, 5, dtype=np.int32)
+    tgt = g.targets()
+    e1, (l1, r1, m1) = _rows(route, g, src, tgt, "kf", monkeypatch)
+    e0, (l0, r0, m0) = _rows(route, g, src, tgt, "f64", monkeypatch)
+    assert e1.info["kernel"] == 5 and e0.info["kernel"] == 0
+    assert np.array_equal(l1, l0) and np.array_equal(r1, r0) and np.array_equal(m1, m0)
+
+
+def test_kf_forced_on_integer_graphs(route, oracle_mod, monkeypatch):
+    # integer latencies through KF: the same rows as the oracle (and as KBF/KD)
+    g = internet_like(1500, 4, 21, name="kf_int")
+    src = np.arange(0, g.n, 11, dtype=np.int32)
+    eng, (lat, rel, mn) = _rows(route, g, src, g.targets(), "kf", monkeypatch)
+    assert eng.info["kernel"] == 5
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(src, g.targets(), oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat) and np.array_equal(rel, orel)
+
+
+def test_kf_vertex_loss_and_subset_targets(route, oracle_mod, monkeypatch):
+    g = fractional(internet_like(3000, 3, 5, vloss=True, hosts=2500, name="kf_vl"), 3)
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 5
+    tgt = g.targets()
+    src = tgt[::37]
+    lat, rel, mn = eng.rows(src, tgt, dispatch=False)
+    og = oracle_mod.OracleGraph(g)
+    olat, orel, _, _ = og.source_rows(src, tgt, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    np.testing.assert_allclose(rel, orel, rtol=REL_TOL, atol=0)
+    # unique shortest paths: igraph's own tie rule agrees
+    ilat, irel, iuq, _ = og.source_rows(src, tgt, oracle_mod.TIE_IGRAPH)
+    np.testing.assert_allclose(rel[iuq], irel[iuq], rtol=REL_TOL, atol=0)
+
+
+def test_kf_directed_and_ragged(route, oracle_mod, monkeypatch):
+    rng = np.random.default_rng(9)
+    n = 700
+    # a directed ring (strongly connected) plus random chords, fractional latencies
+    a = np.arange(n)
+    src = np.concatenate([a, rng.integers(0, n, 3000), a]).astype(np.int32)
+    dst = np.concatenate([(a + 1) % n, rng.integers(0, n, 3000), a]).astype(np.int32)
+    keep = (src != dst) | (np.arange(len(src)) >= n + 3000)
+    src, dst = src[keep], dst[keep]
+    _, first = np.unique(src.astype(np.int64) * n + dst, return_index=True)  # a simple graph
+    first = np.sort(first)
+    src, dst = src[first], dst[first]
+    lat = np.round(rng.uniform(0.5, 90.0, len(src)), 3)
+    loss = np.where(rng.random(len(src)) < 0.7, 0.0, rng.integers(1, 50, len(src)) * 1e-3)
+    g = Graph(n=n, src=src, dst=dst, latency=lat, packetloss=loss, directed=True, name="kf_dir")
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 5
+    for s_ in (np.array([0], np.int32), np.arange(0, n, 3, dtype=np.int32)):
+        t = np.arange(n - 1, -1, -2, dtype=np.int32)  # unsorted, a subset
+        lat_, rel_, mn_ = eng.rows(s_, t, dispatch=False)
+        olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(s_, t, oracle_mod.TIE_MINKEY)
+        assert np.array_equal(lat_, olat) and np.array_equal(rel_, orel)
+
+
+def test_kf_limits_fall_back(route, monkeypatch):
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    # more than 254 distinct reliabilities: the generic f64 kernel
+    g = fractional(internet_like(1000, 3, 8, name="kf_many_r"), 4)
+    g.packetloss = np.random.default_rng(1).uniform(0.0, 0.5, g.m)
+    assert route.RouteEngine(g).info["kernel"] == 0

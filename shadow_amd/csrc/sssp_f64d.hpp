@@ -27,7 +27,7 @@ namespace shd {
 
 struct DevF64D {
     int n, nw;
-    double delta;                        // bucket width (the 12th percentile of arc latencies)
+    double delta;                        // bucket width (the 40th percentile of arc latencies)
     const int* __restrict__ row;         // out-CSR (n+1), arcs by (u, v, eid)
     const int* __restrict__ col;
     const double* __restrict__ w;
@@ -40,25 +40,28 @@ struct DevF64D {
     const double* __restrict__ vf;
     const double* __restrict__ self_w;
     const double* __restrict__ self_r;
-    unsigned long long* dbg;             // SHD_STAMPS builds: 8 words per source
+    unsigned long long* dbg;             // SHD_STAMPS builds: 12 words per source
 };
 #ifdef SHD_STAMPS
-#define KF_STAMP(k) do { if (tid == 0 && g.dbg) g.dbg[(size_t)i * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
-#define KF_COUNT(k) do { if (tid == 0 && g.dbg) g.dbg[(size_t)i * 8 + (k)] += 1; } while (0)
+#define KF_STAMP(k) do { if (tid == 0 && g.dbg) g.dbg[(size_t)i * 12 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define KF_COUNT(k) do { if (tid == 0 && g.dbg) g.dbg[(size_t)i * 12 + (k)] += 1; } while (0)
+#define KF_MARK() unsigned long long kf_t = __builtin_amdgcn_s_memtime()
+#define KF_ACC(k) do { if (tid == 0 && g.dbg) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); g.dbg[(size_t)i * 12 + (k)] += t_ - kf_t; kf_t = t_; } } while (0)
 #else
+#define KF_MARK() do { } while (0)
+#define KF_ACC(k) do { } while (0)
 #define KF_STAMP(k) do { } while (0)
 #define KF_COUNT(k) do { } while (0)
 #endif
 
+constexpr int KF_HUB = 24;  // phase B: vertices of more in-arcs are done by a whole wave
+
 template <int B>
 struct KFSmall {
-    int off[B + 1];   // block scan of the queue slice's degrees
-    int u[B];
-    int beg[B];
-    int wsum[B / 64];
-    int qtail;
+    int qtail;     // ring entries queued (mod n); phase B: hub list length
+    int rhead;     // slices of the round taken
     int flag;
-    unsigned long long mpend;  // min distance (bits) over pending vertices left at or above T
+    unsigned long long mpend[2];  // lower bound of the pending distances (bits), by gather parity
     unsigned long long rmin;
 };
 
@@ -67,7 +70,7 @@ struct KFSmall {
 // A, the parents (u16 x n) and their reliability indices (u8 x n) afterwards
 template <int B>
 struct KFLayout {
-    size_t small, dist, pend, rowl, queue, par, rix, rtab, total;
+    size_t small, dist, pend, wmin, inq, rowl, queue, par, rix, rtab, total;
     __host__ __device__ static KFLayout make(int n) {
         KFLayout L;
         const size_t nw = (size_t)(n + 63) / 64;
@@ -75,6 +78,8 @@ struct KFLayout {
         L.small = o; o += a16(sizeof(KFSmall<B>));
         L.dist = o;  o += a16(8 * (size_t)n);
         L.pend = o;  o += a16(8 * nw);
+        L.wmin = o;  o += a16(8 * nw);
+        L.inq = o;   o += a16(8 * nw);
         const size_t ov = o;
         L.rowl = ov;
         L.queue = ov + a16(4 * ((size_t)n + 1));
@@ -90,28 +95,6 @@ template <int B>
 inline size_t kf_lds_bytes(int n) { return KFLayout<B>::make(n).total; }
 
 template <int B>
-__device__ inline int kf_block_excl_scan(int x, KFSmall<B>* sm, int* total) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int incl = x;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-    }
-    if (lane == 63) sm->wsum[wv] = incl;
-    __syncthreads();
-    int pre = 0, tot = 0;
-#pragma unroll
-    for (int k = 0; k < B / 64; k++) {
-        const int s = sm->wsum[k];
-        pre += (k < wv) ? s : 0;
-        tot += s;
-    }
-    *total = tot;
-    return pre + incl - x;
-}
-
-template <int B>
 __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __restrict__ src, int ns,
                                                       const int* __restrict__ tgt, int nt, long long ld,
                                                       double* __restrict__ lat_out, double* __restrict__ rel_out,
@@ -123,9 +106,13 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
     unsigned long long* dist = reinterpret_cast<unsigned long long*>(smem + L.dist);
     double* relv = reinterpret_cast<double*>(smem + L.dist);  // phase C, in place of dist
     unsigned long long* pend = reinterpret_cast<unsigned long long*>(smem + L.pend);
+    // per word a lower bound of its pending distances (bits): a gather opens only the words
+    // that can hold work below T
+    unsigned long long* wmin = reinterpret_cast<unsigned long long*>(smem + L.wmin);
     uint16_t* par = reinterpret_cast<uint16_t*>(smem + L.par);
     uint8_t* rix = reinterpret_cast<uint8_t*>(smem + L.rix);
-    uint16_t* queue = reinterpret_cast<uint16_t*>(smem + L.queue);
+    uint16_t* ring = reinterpret_cast<uint16_t*>(smem + L.queue);
+    unsigned long long* inq = reinterpret_cast<unsigned long long*>(smem + L.inq);  // vertex in the ring
     int* rowl = reinterpret_cast<int*>(smem + L.rowl);
     double* rtl = reinterpret_cast<double*>(smem + L.rtab);
     const int tid = threadIdx.x, lane = tid & 63;
@@ -138,91 +125,133 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
             continue;
         }
         for (int v = tid; v < n; v += B) dist[v] = kInfBits;
-        for (int k = tid; k < nw; k += B) pend[k] = 0ull;
+        for (int k = tid; k < nw; k += B) { pend[k] = 0ull; wmin[k] = kInfBits; inq[k] = 0ull; }
+        if (tid == 0) { sm->qtail = 0; sm->rhead = 0; sm->mpend[0] = sm->mpend[1] = kInfBits; }
+        int gpar = 0;  // gather parity
         for (int v = tid; v <= n; v += B) rowl[v] = g.row[v];  // (phase B reuses this LDS)
         __syncthreads();
         if (tid == 0) {
             dist[s] = 0ull;
             pend[s >> 6] = 1ull << (s & 63);
+            wmin[s >> 6] = 0ull;
         }
         double T = g.delta;
         __syncthreads();
         KF_STAMP(0);
 
         // ---- A: delta-stepping ------------------------------------------------------
+        // The queue is a ring (u16 x n; a vertex is in it at most once, by its inq bit): a
+        // round expands the entries queued before it, and a relaxation that brings a vertex
+        // below T queues it straight back, so a bucket's rounds need no gather.  Vertices
+        // improved to T or above wait in the pending bitmask with per-word lower bounds;
+        // only an empty ring (the bucket done) opens the next bucket by one gather.
+        unsigned qhead = 0;  // ring entries [qhead, sm->qtail) are queued (mod n)
         for (;;) {
-            if (tid == 0) { sm->qtail = 0; sm->mpend = kInfBits; }
-            __syncthreads();
-            // gather: pending vertices below T into the queue (one thread per word)
-            for (int k0 = 0; k0 < nw; k0 += B) {
-                const int k = k0 + tid;
-                unsigned long long bits = k < nw ? pend[k] : 0ull, take = 0ull;
-                unsigned long long rest = kInfBits;
-                for (unsigned long long b = bits; b;) {
-                    const int bi = __ffsll((long long)b) - 1;
-                    b &= b - 1;
-                    const unsigned long long dv = dist[(k << 6) + bi];
-                    if (as_d(dv) < T) take |= 1ull << bi;
-                    else rest = min(rest, dv);
+            KF_MARK();
+            if (qhead == (unsigned)sm->qtail) {
+                // bucket done: T of the next from the words' lower bounds, then one gather
+                for (int k = tid; k < nw; k += B) {
+                    const unsigned long long wm = wmin[k];
+                    if (wm != kInfBits) atomicMin(&sm->mpend[gpar], wm);
                 }
-                if (rest != kInfBits) atomicMin(&sm->mpend, rest);
-                const int cnt = __popcll(take);
-                const int incl = kd_wave_incl_sum(cnt);
-                int base = 0;
-                if (lane == 63 && incl) base = atomicAdd(&sm->qtail, incl);
-                base = __builtin_amdgcn_readlane(base, 63);
-                int pos = base + incl - cnt;
-                for (unsigned long long b = take; b;) {
-                    const int bi = __ffsll((long long)b) - 1;
-                    b &= b - 1;
-                    queue[pos++] = (uint16_t)((k << 6) + bi);
-                }
-                if (take) pend[k] = bits & ~take;
-            }
-            __syncthreads();
-            const int qn = sm->qtail;
-            KF_COUNT(6);
-            if (qn == 0) {
-                const unsigned long long m = sm->mpend;
-                if (m == kInfBits) break;                       // nothing pending: done
-                T = (floor(as_d(m) / g.delta) + 1.0) * g.delta;  // the next non-empty bucket
-                if (!(as_d(m) < T)) T = as_d(m) * 2.0 + g.delta; // (guard: rounding at huge m)
+                if (tid == 0) sm->mpend[gpar ^ 1] = kInfBits;  // (the next gather's; last read a gather ago)
                 __syncthreads();
-                continue;
+                const unsigned long long m = sm->mpend[gpar];
+                gpar ^= 1;
+                if (m == kInfBits) break;                        // nothing pending: done
+                T = (floor(as_d(m) / g.delta) + 1.0) * g.delta;   // the next non-empty bucket
+                if (!(as_d(m) < T)) T = as_d(m) * 2.0 + g.delta;  // (guard: rounding at huge m)
+                for (int k0 = 0; k0 < nw; k0 += B) {
+                    const int k = k0 + tid;
+                    unsigned long long take = 0ull, bits = 0ull, rest = kInfBits;
+                    const unsigned long long wm = k < nw ? wmin[k] : kInfBits;
+                    if (as_d(wm) < T) {
+                        bits = pend[k];
+                        for (unsigned long long b = bits; b;) {  // four bits per trip: reads in flight
+                            int vq[4];
+                            unsigned long long dq[4];
+#pragma unroll
+                            for (int h = 0; h < 4; h++) {
+                                vq[h] = b ? (k << 6) + __ffsll((long long)b) - 1 : -1;
+                                b &= b - 1;
+                            }
+#pragma unroll
+                            for (int h = 0; h < 4; h++) dq[h] = dist[vq[h] >= 0 ? vq[h] : 0];
+#pragma unroll
+                            for (int h = 0; h < 4; h++) {
+                                if (vq[h] < 0) continue;
+                                if (as_d(dq[h]) < T) take |= 1ull << (vq[h] & 63);
+                                else rest = min(rest, dq[h]);
+                            }
+                        }
+                        pend[k] = bits & ~take;
+                        wmin[k] = rest;
+                        if (take) atomicOr(&inq[k], take);
+                    }
+                    const int cnt = __popcll(take);
+                    const int incl = kd_wave_incl_sum(cnt);
+                    int base = 0;
+                    if (lane == 63 && incl) base = atomicAdd(&sm->qtail, incl);
+                    base = __builtin_amdgcn_readlane(base, 63);
+                    unsigned pos = (unsigned)(base + incl - cnt);
+                    for (unsigned long long b = take; b;) {
+                        const int bi = __ffsll((long long)b) - 1;
+                        b &= b - 1;
+                        ring[pos++ % (unsigned)n] = (uint16_t)((k << 6) + bi);
+                    }
+                }
+                __syncthreads();
+                KF_COUNT(10);
+                KF_ACC(8);
+                continue;  // (an empty gather -- a loose lower bound -- recomputes T)
             }
-            // expand the queue, B entries at a time, arcs load-balanced over the workgroup:
-            // each thread takes 4 arc positions per trip, owners by binary search over the
-            // entries' offsets, the 8 arc loads of a trip issued together
-            for (int c0 = 0; c0 < qn; c0 += B) {
-                const int q = c0 + tid;
+            // one round: the entries queued so far, B at a time, arcs load-balanced over the
+            // workgroup: each thread takes 4 arc positions per trip, owners by binary search
+            // over the entries' offsets, the 8 arc loads of a trip issued together
+            const unsigned qend = (unsigned)sm->qtail;
+            KF_COUNT(6);
+            const int qn = (int)(qend - qhead);
+            __syncthreads();  // every wave has read the round's end before any wave queues more
+            // waves pull 64-entry slices of the round's entries (no block barrier inside a
+            // round); a slice's arcs are spread over its lanes, 4 positions per lane and trip,
+            // owners by a binary search over the slice's lane offsets (ds_bpermute), the 8
+            // arc loads of a trip issued together
+            for (;;) {
+                int c = 0;
+                if (lane == 0) c = atomicAdd(&sm->rhead, 64);
+                c = __builtin_amdgcn_readfirstlane(c);
+                if (c >= qn) break;
+                const int q = c + lane;
                 int u = 0, beg = 0, deg = 0;
                 if (q < qn) {
-                    u = queue[q];
+                    u = ring[(qhead + (unsigned)q) % (unsigned)n];
+                    atomicAnd(&inq[u >> 6], ~(1ull << (u & 63)));  // (may be queued again below)
                     beg = rowl[u];
                     deg = rowl[u + 1] - beg;
                 }
-                int total;
-                const int off = kf_block_excl_scan<B>(deg, sm, &total);
-                const int cnt = min(B, qn - c0);
-                sm->off[tid] = off;
-                sm->u[tid] = u;
-                sm->beg[tid] = beg;
-                __syncthreads();
-                for (int e0 = 0; e0 < total; e0 += 4 * B) {
-                    int aq[4], uq[4];
+                const int incl = kd_wave_incl_sum(deg);
+                const int total = __builtin_amdgcn_readlane(incl, 63);
+                const int excl = incl - deg;
+                for (int p0 = 0; p0 < total; p0 += 4 * 64) {
+                    int lo[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (int step = 32; step >= 1; step >>= 1) {
+                        int ov[4];
+#pragma unroll
+                        for (int r = 0; r < 4; r++) ov[r] = __shfl(excl, lo[r] + step, 64);
+#pragma unroll
+                        for (int r = 0; r < 4; r++)
+                            if (lo[r] + step < 64 && ov[r] <= p0 + r * 64 + lane) lo[r] += step;
+                    }
+                    int aq[4], uq[4], vq[4];
+                    double wq[4];
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
-                        const int e = e0 + r * B + tid;
-                        int lo = 0, hi = cnt;  // last entry with off <= e
-                        while (hi - lo > 1) {
-                            const int mid = (lo + hi) >> 1;
-                            if (sm->off[mid] <= e) lo = mid; else hi = mid;
-                        }
-                        aq[r] = e < total ? sm->beg[lo] + (e - sm->off[lo]) : -1;
-                        uq[r] = sm->u[lo];
+                        const int p = p0 + r * 64 + lane;
+                        const int ob = __shfl(beg, lo[r], 64), oe = __shfl(excl, lo[r], 64);
+                        uq[r] = __shfl(u, lo[r], 64);
+                        aq[r] = p < total ? ob + (p - oe) : -1;
                     }
-                    int vq[4];
-                    double wq[4];
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         const int a = aq[r] >= 0 ? aq[r] : 0;
@@ -233,47 +262,136 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                     for (int r = 0; r < 4; r++) {
                         if (aq[r] < 0) continue;
                         const int v = vq[r];
-                        const unsigned long long nb = as_u(as_d(dist[uq[r]]) + wq[r]);
+                        const double nd = as_d(dist[uq[r]]) + wq[r];
+                        const unsigned long long nb = as_u(nd);
                         if (nb < dist[v]) {
                             const unsigned long long old = atomicMin(&dist[v], nb);
-                            if (nb < old) atomicOr(&pend[v >> 6], 1ull << (v & 63));
+                            if (nb < old) {
+                                const unsigned long long bit = 1ull << (v & 63);
+                                if (nd < T) {  // this bucket: straight back into the ring
+                                    if (!(atomicOr(&inq[v >> 6], bit) & bit)) {
+                                        const unsigned at = (unsigned)atomicAdd(&sm->qtail, 1);
+                                        ring[at % (unsigned)n] = (uint16_t)v;
+                                    }
+                                } else {
+                                    atomicOr(&pend[v >> 6], bit);
+                                    atomicMin(&wmin[v >> 6], nb);
+                                }
+                            }
                         }
                     }
                 }
-                __syncthreads();
             }
+            __syncthreads();
+            if (tid == 0) sm->rhead = 0;  // (every wave has left the loop above)
+            __syncthreads();
+            qhead = qend;
+            KF_ACC(9);
         }
 
         KF_STAMP(1);
         // ---- B: parents (tight in-arc with min (d[u], u), first in in-row order) ------
-        for (int v = tid; v < n; v += B) {
-            const double dv = as_d(dist[v]);
-            int pu = v, pr = 255;
-            if (v != s && dv < INFINITY) {
+        // two vertices per trip, four in-arcs of each: eight arc loads in flight.  Vertices
+        // of more than KF_HUB in-arcs (the BA hubs: one would hold its thread, and the
+        // workgroup, for hundreds of trips) are listed and done by whole waves below.
+        if (tid == 0) sm->qtail = 0;  // (hub list length; the ring is free now)
+        __syncthreads();
+        for (int v0 = tid; v0 < n; v0 += 2 * B) {
+            int vv[2], a0[2], a1[2], bu[2], ba[2];
+            double dv[2], bd[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                vv[h] = v0 + h * B;
+                const bool ok = vv[h] < n;
+                dv[h] = ok ? as_d(dist[vv[h]]) : INFINITY;
+                const bool scan = ok && vv[h] != s && dv[h] < INFINITY;
+                a0[h] = scan ? g.row_in[vv[h]] : 0;
+                a1[h] = scan ? g.row_in[vv[h] + 1] : 0;
+                if (a1[h] - a0[h] > KF_HUB) {
+                    ring[atomicAdd(&sm->qtail, 1)] = (uint16_t)vv[h];
+                    a1[h] = a0[h];
+                    vv[h] = -1 - vv[h];  // (written by the wave below)
+                }
+                bd[h] = INFINITY; bu[h] = 0x7fffffff; ba[h] = -1;
+            }
+            for (int t0 = 0; t0 < max(a1[0] - a0[0], a1[1] - a0[1]); t0 += 4) {
+                int uq[2][4];
+                double wq[2][4];
+#pragma unroll
+                for (int h = 0; h < 2; h++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int a = min(a0[h] + t0 + q, max(a1[h] - 1, 0));
+                        uq[h][q] = g.col_in[a];
+                        wq[h][q] = g.w_in[a];
+                    }
+#pragma unroll
+                for (int h = 0; h < 2; h++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        if (a0[h] + t0 + q >= a1[h]) continue;
+                        const double du = as_d(dist[uq[h][q]]);
+                        if (du + wq[h][q] == dv[h] && (du < bd[h] || (du == bd[h] && uq[h][q] < bu[h]))) {
+                            bd[h] = du; bu[h] = uq[h][q]; ba[h] = a0[h] + t0 + q;
+                        }
+                    }
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int v = vv[h];
+                if (v < 0 || v >= n) continue;
+                int pu = v, pr = 255;
+                if (ba[h] >= 0) { pu = bu[h]; pr = g.rix_in[ba[h]]; }
+                else if (v != s && dv[h] < INFINITY) raise_err(err, SHD_ROUTE_EUNREACH);  // (cannot happen)
+                par[v] = (uint16_t)pu;
+                rix[v] = (uint8_t)pr;
+            }
+        }
+        __syncthreads();
+        {
+            // hubs: 16 lanes per hub (four hubs per wave at a time), 4 in-arcs per lane and
+            // step with the loads in flight, then the lexicographic (d[u], u, arc) minimum
+            // over the hub's 16 lanes
+            const int nhub = sm->qtail;
+            const int sub = lane >> 4, sl = lane & 15;
+            for (int h0 = (tid >> 6) * 4; h0 < nhub; h0 += (B / 64) * 4) {
+                const int h = h0 + sub;
+                const bool hv = h < nhub;
+                const int v = hv ? ring[h] : 0;
+                const double dv = as_d(dist[v]);
+                const int a0 = hv ? g.row_in[v] : 0, a1 = hv ? g.row_in[v + 1] : 0;
                 double bd = INFINITY;
-                int bu = 0x7fffffff, ba = -1;
-                const int a1 = g.row_in[v + 1];
-                for (int a0 = g.row_in[v]; a0 < a1; a0 += 4) {
+                int bu = 0x7fffffff, ba = 0x7fffffff;
+                for (int t = a0 + sl; __any(t < a1); t += 64) {
                     int uq[4];
                     double wq[4];
 #pragma unroll
-                    for (int h = 0; h < 4; h++) {
-                        const int a = min(a0 + h, a1 - 1);
-                        uq[h] = g.col_in[a];
-                        wq[h] = g.w_in[a];
+                    for (int q = 0; q < 4; q++) {
+                        const int a = min(t + 16 * q, max(a1 - 1, 0));
+                        uq[q] = g.col_in[a];
+                        wq[q] = g.w_in[a];
                     }
 #pragma unroll
-                    for (int h = 0; h < 4; h++) {
-                        if (a0 + h >= a1) continue;
-                        const double du = as_d(dist[uq[h]]);
-                        if (du + wq[h] == dv && (du < bd || (du == bd && uq[h] < bu))) { bd = du; bu = uq[h]; ba = a0 + h; }
+                    for (int q = 0; q < 4; q++) {
+                        const int a = t + 16 * q;
+                        if (a >= a1) continue;
+                        const double du = as_d(dist[uq[q]]);
+                        if (du + wq[q] == dv && (du < bd || (du == bd && (uq[q] < bu || (uq[q] == bu && a < ba))))) {
+                            bd = du; bu = uq[q]; ba = a;
+                        }
                     }
                 }
-                if (ba >= 0) { pu = bu; pr = g.rix_in[ba]; }
-                else raise_err(err, SHD_ROUTE_EUNREACH);  // (a finite distance always has a tight arc)
+#pragma unroll
+                for (int d = 8; d >= 1; d >>= 1) {  // within the 16 lanes of the hub
+                    const double od = __shfl_xor(bd, d, 64);
+                    const int ou = __shfl_xor(bu, d, 64), oa = __shfl_xor(ba, d, 64);
+                    if (od < bd || (od == bd && (ou < bu || (ou == bu && oa < ba)))) { bd = od; bu = ou; ba = oa; }
+                }
+                if (hv && sl == 0) {
+                    if (ba != 0x7fffffff) { par[v] = (uint16_t)bu; rix[v] = g.rix_in[ba]; }
+                    else { par[v] = (uint16_t)v; rix[v] = 255; raise_err(err, SHD_ROUTE_EUNREACH); }
+                }
             }
-            par[v] = (uint16_t)pu;
-            rix[v] = (uint8_t)pr;
         }
         __syncthreads();
 
@@ -309,26 +427,47 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
         }
         __syncthreads();
         // level passes: a vertex whose parent is done takes relv[p] * r(p, v); every vertex is
-        // written once, after its parent, so the products are the source-first left folds
+        // written once, after its parent, so the products are the source-first left folds.
+        // A thread keeps its vertices' parents and factors in registers and reads all their
+        // parents' values at once per pass; a value written during a pass may be read in the
+        // same pass (64-bit LDS accesses are not torn), which only finishes chains sooner
+        // (parents and factor indices packed: 2 x u16 and 4 x u8 per register)
+        uint32_t pk2[8], rx4[4];
+        unsigned rem = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) pk2[k] = (uint32_t)s | ((uint32_t)s << 16);
+#pragma unroll
+        for (int k = 0; k < 4; k++) rx4[k] = 0u;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int v = tid + k * B;
+            if (v < n) {
+                pk2[k >> 1] = (pk2[k >> 1] & ~(0xFFFFu << (16 * (k & 1)))) | ((uint32_t)par[v] << (16 * (k & 1)));
+                rx4[k >> 2] |= (uint32_t)rix[v] << (8 * (k & 3));
+                if (relv[v] == -1.0) rem |= 1u << k;
+            }
+        }
         if (tid == 0) sm->flag = 0;
         __syncthreads();
         for (;;) {
             int prog = 0;
-            double nv[16];
-            unsigned todo = 0;
-            int k = 0;
-            for (int v = tid; v < n; v += B, k++) {
-                if (k >= 16) break;
-                if (relv[v] == -1.0) {
-                    const double rp = relv[par[v]];
-                    if (rp != -1.0) { nv[k] = rp * rtl[rix[v]]; todo |= 1u << k; }
+#pragma unroll
+            for (int k0 = 0; k0 < 16; k0 += 8) {
+                if (!((rem >> k0) & 0xFFu)) continue;
+                double rp[8], rf[8];
+#pragma unroll
+                for (int k = k0; k < k0 + 8; k++) {
+                    const bool live = (rem >> k) & 1u;
+                    rp[k - k0] = live ? relv[(pk2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu] : -1.0;
+                    rf[k - k0] = rtl[(rx4[k >> 2] >> (8 * (k & 3))) & 0xFFu];
                 }
-            }
-            __syncthreads();
-            k = 0;
-            for (int v = tid; v < n; v += B, k++) {
-                if (k >= 16) break;
-                if ((todo >> k) & 1u) { relv[v] = nv[k]; prog = 1; }
+#pragma unroll
+                for (int k = k0; k < k0 + 8; k++)
+                    if (((rem >> k) & 1u) && rp[k - k0] != -1.0) {
+                        relv[tid + k * B] = rp[k - k0] * rf[k - k0];
+                        rem &= ~(1u << k);
+                        prog = 1;
+                    }
             }
             if (__any(prog) && lane == 0) sm->flag = 1;
             __syncthreads();

@@ -54,6 +54,20 @@ def test_kf_many_sources_per_workgroup(route, monkeypatch):
         assert np.array_equal(l2, lat[part]) and np.array_equal(r2, rel[part]) and np.array_equal(m2, mn[part])
 
 
+def test_kf_repeated_launches_identical(route, monkeypatch):
+    # every C2f source, three launches, against the generic f64 kernel's rows: the
+    # workgroups' asynchronous rounds must give the same table every time
+    g = config("c2f")
+    tgt = g.targets()
+    _, (l0, r0, m0) = _rows(route, g, tgt, tgt, "f64", monkeypatch)
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 5
+    for _ in range(3):
+        lat, rel, mn = eng.rows(tgt, tgt, dispatch=False)
+        assert np.array_equal(lat, l0) and np.array_equal(rel, r0) and np.array_equal(mn, m0)
+
+
 def test_kf_equals_generic_f64(route, monkeypatch):
     g = config("c2f")
     src = np.arange(0, g.n, 5, dtype=np.int32)

@@ -90,7 +90,10 @@ typedef struct shd_route_info {
     int32_t lds_resident;    /* per-source state fits the 160 KiB LDS */
     uint64_t device_bytes;   /* resident graph bytes */
     double min_edge_latency;
-    int32_t kernel;          /* SSSP kernel: 0 = generic f64, 1 = integer K32 (LDS keys) */
+    int32_t kernel;          /* SSSP kernel: 0 = generic f64, 1 = integer K32 (LDS keys), 2 = KB/KBF
+                              * (8 sources per workgroup, C2-class), 4 = KD (delta-stepping, u16
+                              * distances, seeded plans), 5 = KF (f64 delta-stepping in LDS: the
+                              * fractional-latency path); 3 = K16 in diagnostic builds only */
     int32_t dist_bound;      /* K32: proven bound on every shortest-path latency (ms) */
     int32_t block;           /* threads per workgroup of the SSSP kernel */
     int32_t reserved;        /* KD: bucket width delta; KB: 1 when path attributes are fused */

@@ -40,13 +40,13 @@ struct DevF64D {
     const double* __restrict__ vf;
     const double* __restrict__ self_w;
     const double* __restrict__ self_r;
-    unsigned long long* dbg;             // SHD_STAMPS builds: 12 words per source
+    unsigned long long* dbg;             // SHD_STAMPS builds: 16 words per source
 };
 #ifdef SHD_STAMPS
-#define KF_STAMP(k) do { if (tid == 0 && g.dbg) g.dbg[(size_t)i * 12 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
-#define KF_COUNT(k) do { if (tid == 0 && g.dbg) g.dbg[(size_t)i * 12 + (k)] += 1; } while (0)
+#define KF_STAMP(k) do { if (tid == 0 && g.dbg) g.dbg[(size_t)i * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define KF_COUNT(k) do { if (tid == 0 && g.dbg) g.dbg[(size_t)i * 16 + (k)] += 1; } while (0)
 #define KF_MARK() unsigned long long kf_t = __builtin_amdgcn_s_memtime()
-#define KF_ACC(k) do { if (tid == 0 && g.dbg) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); g.dbg[(size_t)i * 12 + (k)] += t_ - kf_t; kf_t = t_; } } while (0)
+#define KF_ACC(k) do { if (tid == 0 && g.dbg) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); g.dbg[(size_t)i * 16 + (k)] += t_ - kf_t; kf_t = t_; } } while (0)
 #else
 #define KF_MARK() do { } while (0)
 #define KF_ACC(k) do { } while (0)
@@ -61,6 +61,7 @@ struct KFSmall {
     int qtail;     // ring entries queued (mod n); phase B: hub list length
     int rhead;     // slices of the round taken
     int flag;
+    unsigned long long wmark[B / 64][4];  // per wave: start marks of a trip's four windows
     unsigned long long mpend[2];  // lower bound of the pending distances (bits), by gather parity
     unsigned long long rmin;
 };
@@ -221,6 +222,8 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                 if (lane == 0) c = atomicAdd(&sm->rhead, 64);
                 c = __builtin_amdgcn_readfirstlane(c);
                 if (c >= qn) break;
+                KF_COUNT(11);
+                KF_ACC(9);
                 const int q = c + lane;
                 int u = 0, beg = 0, deg = 0;
                 if (q < qn) {
@@ -232,17 +235,29 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                 const int incl = kd_wave_incl_sum(deg);
                 const int total = __builtin_amdgcn_readlane(incl, 63);
                 const int excl = incl - deg;
+                KF_ACC(12);
+                // (every queued vertex has an out-arc -- the graph is strongly connected -- so
+                // the slice's non-empty entries are lanes 0 .. R-1)
+                const bool valid = q < qn;
+                unsigned long long* wm4 = sm->wmark[tid >> 6];
                 for (int p0 = 0; p0 < total; p0 += 4 * 64) {
-                    int lo[4] = {0, 0, 0, 0};
+                    // owners: each entry marks its start in the window (of 64 positions) that
+                    // holds it; the owner of position p is the entries starting before the
+                    // window plus the marks at or below p, minus one
+                    if (lane < 4) wm4[lane] = 0ull;
+                    __builtin_amdgcn_wave_barrier();
+                    const int rel = excl - p0;
+                    if (valid && rel >= 0 && rel < 4 * 64) atomicOr(&wm4[rel >> 6], 1ull << (rel & 63));
+                    __builtin_amdgcn_wave_barrier();
+                    int lo[4];
 #pragma unroll
-                    for (int step = 32; step >= 1; step >>= 1) {
-                        int ov[4];
-#pragma unroll
-                        for (int r = 0; r < 4; r++) ov[r] = __shfl(excl, lo[r] + step, 64);
-#pragma unroll
-                        for (int r = 0; r < 4; r++)
-                            if (lo[r] + step < 64 && ov[r] <= p0 + r * 64 + lane) lo[r] += step;
+                    for (int r = 0; r < 4; r++) {
+                        const unsigned long long before = __ballot(valid && excl < p0 + r * 64);
+                        const unsigned long long mk = wm4[r];
+                        const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+                        lo[r] = max(0, __popcll(before) + __popcll(mk & upto) - 1);
                     }
+                    __builtin_amdgcn_wave_barrier();  // (the marks are read before the next trip clears them)
                     int aq[4], uq[4], vq[4];
                     double wq[4];
 #pragma unroll
@@ -252,12 +267,15 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                         uq[r] = __shfl(u, lo[r], 64);
                         aq[r] = p < total ? ob + (p - oe) : -1;
                     }
+                    KF_ACC(13);
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         const int a = aq[r] >= 0 ? aq[r] : 0;
                         vq[r] = g.col[a];
                         wq[r] = g.w[a];
                     }
+                    if (tid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    KF_ACC(14);
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         if (aq[r] < 0) continue;

@@ -203,3 +203,21 @@ def test_c2_rows_pinned_by_networkx(oracle_mod):
         assert sha(lat) == r["lat_sha"] and sha(rel) == r["rel_sha"]
         n_lat, n_rel = pin_row(G, g, int(s), T, lat, rel, uq)
         assert n_lat == len(T) - 1 and n_rel == int(uq.sum()) - 1
+
+
+def test_fractional_rows_pinned_by_networkx(oracle_mod):
+    """The fractional variants (two-decimal latencies, the reference topology file's format)
+    that KF computes: the oracle's rows equal networkx's latencies bit for bit (left folds
+    from the source) and Shadow's product along networkx's path on every unique pair.
+    Parity for KF rows themselves is tests/test_kf_gpu.py (against this oracle)."""
+    from shadow_amd.graph import config
+    from tests.golden.nx_pin import nx_graph, pin_row
+    g = config("c2f")
+    assert not np.all(g.latency == np.floor(g.latency))
+    og = oracle_mod.OracleGraph(g)
+    G = nx_graph(g)
+    T = g.targets()
+    for s in T[::250]:
+        lat, rel, uq, _ = og.source_row(int(s), T, oracle_mod.TIE_MINKEY)
+        n_lat, n_rel = pin_row(G, g, int(s), T, lat, rel, uq)
+        assert n_lat == len(T) - 1 and n_rel == int(uq.sum()) - 1

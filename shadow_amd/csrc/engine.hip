@@ -4,11 +4,13 @@
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <sys/mman.h>
-#include <queue>
+
 #include <thread>
 #include "sssp_f64.hpp"
 #include "sssp_f64d.hpp"
@@ -27,6 +29,57 @@ using namespace shd;
 // =============================================================================
 // Host side
 // =============================================================================
+// The planner's host workers: created with a context that plans (KD), parked on a condition
+// variable between plans, so a plan does not pay ~15 thread creations (~0.5 ms).  run(f)
+// starts f on every worker; wait() returns once all of them have returned from it.
+struct HostPool {
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv, cv_done;
+    std::function<void()> fn;
+    uint64_t gen = 0;
+    int busy = 0;
+    bool stop = false;
+    explicit HostPool(int n) {
+        for (int i = 0; i < n; i++) th.emplace_back([this] { loop(); });
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> l(m);
+                cv.wait(l, [&] { return stop || gen != seen; });
+                if (stop) return;
+                seen = gen;
+                f = fn;
+            }
+            f();
+            std::lock_guard<std::mutex> l(m);
+            if (--busy == 0) cv_done.notify_all();
+        }
+    }
+    void run(std::function<void()> f) {
+        std::lock_guard<std::mutex> l(m);
+        fn = std::move(f);
+        busy = (int)th.size();
+        gen++;
+        cv.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> l(m);
+        cv_done.wait(l, [&] { return busy == 0; });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> l(m);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& t : th) t.join();
+    }
+};
+
 struct shd_route {
     int device = 0;
     int n = 0, m = 0, nnz = 0;
@@ -93,6 +146,8 @@ struct shd_route {
     std::vector<std::vector<uint32_t>> lm_p;
     uint16_t* d_lm_drow = nullptr;  // the landmark rows in the row-store format (device)
     uint32_t* d_lm_prow = nullptr;
+    std::unique_ptr<HostPool> pool;  // the planner's host workers (KD contexts)
+    std::mutex plan_lock;            // one plan at a time uses the pool
     int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD, 5 KF
     // KF (fractional latencies, LDS-resident f64 delta-stepping)
     int kf_block = 0, kf_slots = 0;
@@ -116,6 +171,8 @@ struct shd_route {
 };
 
 namespace {
+
+HostPool* host_pool(shd_route* c);
 
 // KD workgroup sizes: f(std::integral_constant<int, B>) for the runtime block size
 template <typename F>
@@ -844,6 +901,7 @@ int shd_route_create(shd_route_t** out, const shd_graph_t* g, int device) {
         shd_route_destroy(c);
         return rc;
     }
+    if (c->sel == 4 && c->kd_fused) host_pool(c);  // the planner's workers, parked until a plan
     *out = c;
     return SHD_ROUTE_OK;
 }
@@ -1176,6 +1234,16 @@ struct shd_route_plan {
 
 namespace {
 
+// the context's planner workers (created once; none when one host thread is asked for)
+HostPool* host_pool(shd_route* c) {
+    if (!c->pool) {
+        int nth = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+        if (const char* e = getenv("SHD_ROUTE_PLAN_THREADS")) nth = std::max(1, std::min(64, atoi(e)));
+        if (nth > 1) c->pool.reset(new HostPool(nth - 1));
+    }
+    return c->pool.get();
+}
+
 // Exact rows of `verts` on the device for the planner: one unplanned KD launch whose jobs
 // write no output row (row -1) but keep their row in store slot k, the format seeded rows
 // read (u16 distances, 0xFFFF = unreached, and the engine tie-rule parent record
@@ -1267,7 +1335,6 @@ int ensure_hub_rows(shd_route* c, int k) {
     c->lm_p = std::move(Pr);
     return SHD_ROUTE_OK;
 }
-int ensure_close(shd_route* c) { return c->close.empty() ? ensure_hub_rows(c, 16) : SHD_ROUTE_OK; }
 int ensure_landmarks(shd_route* c, int k) { return ensure_hub_rows(c, k); }
 
 }  // namespace
@@ -1461,7 +1528,9 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // <= 256): D0 = w(s,x) + w(x,u) + d_u(.) is as consistent as a neighbour's, and u's
         // own record is the arc (x,u), tight whenever u keeps D0.
         bool two_hop = true;
+        int hop_deg = 256;  // largest degree of a two-hop row's middle vertex x
         if (const char* e = getenv("SHD_ROUTE_SEED2HOP")) two_hop = atoi(e) != 0;
+        if (const char* e = getenv("SHD_ROUTE_HOPDEG")) hop_deg = std::max(1, atoi(e));
         // The roots (the rows that would start unseeded) seed from host-computed landmark
         // rows instead: D0 = d(s, L) + d_L(.) is consistent for any landmark L, and L's own
         // record is the last arc (x, L) of a shortest s -> L path (tight whenever L keeps
@@ -1503,7 +1572,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             };
             for (int a = c->h_row[s]; a < c->h_row[s + 1]; a++) {
                 const int x = c->h_col[a];
-                if (x == s || c->h_row[x + 1] - c->h_row[x] > 256) continue;
+                if (x == s || c->h_row[x + 1] - c->h_row[x] > hop_deg) continue;
                 for (int b = c->h_row[x]; b < c->h_row[x + 1]; b++) {
                     const int u = c->h_col[b];
                     if (u == s || u == x || rk[u] >= rk[s] || !avail(u)) continue;
@@ -1533,21 +1602,37 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // recomputes the row otherwise.
         // (not value-initialised: the worker threads first-touch their own pages)
         std::unique_ptr<Choice[]> pre(new Choice[order.size()]);
-        {
-            const double th0 = since();
-            const int nq = (int)order.size();
-            std::atomic<int> nextq{nroot_min};
-            auto work = [&]() {
-                for (int q0 = nextq.fetch_add(256); q0 < nq; q0 = nextq.fetch_add(256))
-                    for (int qq = q0; qq < std::min(nq, q0 + 256); qq++)
-                        choose(order[qq], [&](int u) { return first[u] >= 0; }, pre[qq]);
-            };
-            const int nth = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
-            std::vector<std::thread> th;
-            for (int t = 1; t < nth; t++) th.emplace_back(work);
-            work();
-            for (auto& t : th) t.join();
-            t_hop = since() - th0;
+        // The worker threads take chunks of 256 choices in order and mark each one done; the
+        // sequential pass below runs concurrently, consuming the chunks as they complete (and
+        // taking a chunk itself while the one it needs is not done), so it hides behind the
+        // choices instead of following them (C4: ~1.4 ms).
+        const int nq = (int)order.size(), CH = 256;
+        const int nchunk = nq > nroot_min ? (nq - nroot_min + CH - 1) / CH : 0;
+        std::unique_ptr<std::atomic<int>[]> chunk_done(new std::atomic<int>[std::max(1, nchunk)]);
+        for (int k = 0; k < nchunk; k++) chunk_done[k].store(0, std::memory_order_relaxed);
+        std::atomic<int> nextq{nroot_min};
+        auto take_chunk = [&]() {
+            if (nextq.load(std::memory_order_relaxed) >= nq) return false;  // (no unbounded fetch_add)
+            const int q0 = nextq.fetch_add(CH);
+            if (q0 >= nq) return false;
+            for (int qq = q0; qq < std::min(nq, q0 + CH); qq++)
+                choose(order[qq], [&](int u) { return first[u] >= 0; }, pre[qq]);
+            chunk_done[(q0 - nroot_min) / CH].store(1, std::memory_order_release);
+            return true;
+        };
+        const double th0 = since();
+        std::lock_guard<std::mutex> plan_guard(c->plan_lock);
+        HostPool* pool = host_pool(c);
+        struct PoolWait {
+            HostPool* p;
+            bool on;
+            void operator()() { if (on) { p->wait(); on = false; } }
+            ~PoolWait() { (*this)(); }
+        } pool_wait{pool, pool && nchunk > 0};
+        if (pool_wait.on) pool->run([&]() { while (take_chunk()) {} });
+        if (getenv("SHD_ROUTE_PIPE") && atoi(getenv("SHD_ROUTE_PIPE")) == 0) {  // A/B: choices first, then the pass
+            while (take_chunk()) {}
+            pool_wait();
         }
         int nlev = 1, q = 0;
         t_loop0 = since();
@@ -1555,6 +1640,11 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             const int p = job_pos[j], s = src[p];
             const int qi = q;
             const bool seedable = q++ >= nroot_min;
+            if (seedable && (qi - nroot_min) % CH == 0) {
+                std::atomic<int>& dn = chunk_done[(qi - nroot_min) / CH];
+                while (!dn.load(std::memory_order_acquire))
+                    if (!take_chunk()) std::this_thread::yield();
+            }
             Choice ch;
             ch.m = ch.nh = 0;
             if (seedable) {
@@ -1604,6 +1694,8 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             nlev = std::max(nlev, lvl[j] + 1);
             if (first[src[p]] == j && lvl[j] + 1 < depth) fl[src[p]] = p;
         }
+        pool_wait();
+        t_hop = since() - th0;
         t_seeds = since();
         const long long rs = kd_row_stride(n);
         bool uses_lm = false;
@@ -1611,20 +1703,30 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         P->nland = uses_lm ? nland : 0;
         const int ntot = P->nslots + P->nland;
         P->store_bytes = (uint64_t)ntot * (uint64_t)rs * 6u;
-        bool ok = ntot > 0 &&
-                  hipMalloc((void**)&P->d_drow, sizeof(uint16_t) * (size_t)rs * ntot) == hipSuccess &&
-                  hipMalloc((void**)&P->d_prow, sizeof(uint32_t) * (size_t)rs * ntot) == hipSuccess;
+        // the row store's allocation and the landmark rows' device copies run on a second host
+        // thread while this one builds the schedule (C4: ~0.5 ms of hipMalloc and copies)
+        bool store_ok = false;
+        std::thread store_th;
+        if (ntot > 0)
+            store_th = std::thread([&]() {
+                bool r = hipSetDevice(c->device) == hipSuccess &&
+                         hipMalloc((void**)&P->d_drow, sizeof(uint16_t) * (size_t)rs * ntot) == hipSuccess &&
+                         hipMalloc((void**)&P->d_prow, sizeof(uint32_t) * (size_t)rs * ntot) == hipSuccess;
+                if (r && P->nland)
+                    // landmark rows into the slots after the kept rows' (the rows are in the store
+                    // format already, pads included)
+                    r = hipMemcpy(P->d_drow + (size_t)rs * P->nslots, c->d_lm_drow,
+                                  sizeof(uint16_t) * (size_t)rs * P->nland, hipMemcpyDeviceToDevice) == hipSuccess &&
+                        hipMemcpy(P->d_prow + (size_t)rs * P->nslots, c->d_lm_prow,
+                                  sizeof(uint32_t) * (size_t)rs * P->nland, hipMemcpyDeviceToDevice) == hipSuccess;
+                // the job array and the launch's queue counter + ready flags
+                r = r && hipMalloc((void**)&P->d_jobs, sizeof(KDJob) * (size_t)nj) == hipSuccess &&
+                    hipMalloc((void**)&P->d_next, sizeof(int) * (1 + (size_t)ntot)) == hipSuccess;
+                store_ok = r;
+            });
+        struct JoinOne { std::thread& t; ~JoinOne() { if (t.joinable()) t.join(); } } join_store{store_th};
         t_alloc = since();
-        if (ok && P->nland) {
-            // landmark rows into the slots after the kept rows', device to device (the rows are
-            // in the store format already, pads included)
-            ok = hipMemcpy(P->d_drow + (size_t)rs * P->nslots, c->d_lm_drow, sizeof(uint16_t) * (size_t)rs * P->nland,
-                           hipMemcpyDeviceToDevice) == hipSuccess &&
-                 hipMemcpy(P->d_prow + (size_t)rs * P->nslots, c->d_lm_prow, sizeof(uint32_t) * (size_t)rs * P->nland,
-                           hipMemcpyDeviceToDevice) == hipSuccess;
-        }
-        t_store = since();
-        if (ok) {
+        if (ntot > 0) {
             std::vector<int> cnt(nlev + 1, 0);
             for (int j = 0; j < nj; j++) cnt[lvl[j] + 1]++;
             for (int k = 0; k < nlev; k++) cnt[k + 1] += cnt[k];
@@ -1671,9 +1773,17 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             };
             size_t bq_n = 0;  // rows queued
             for (int j = nj - 1; j >= 0; j--) if (!left[j]) { push(0, j); bq_n++; }
-            typedef std::pair<long long, int> LI;
-            std::priority_queue<LI, std::vector<LI>, std::greater<LI>> free_at;
-            for (int w = 0; w < W; w++) free_at.push({0, w});
+            // free walker slots: a second bucket queue over ticks (a slot frees at its row's
+            // start + cost >= the current minimum, so this minimum only grows too); it replaced
+            // a binary heap of (tick, slot) pairs, 11.4 -> 7.4 ms for C4's schedule on the host
+            std::vector<int> fhead(1024, -1), fnext(W, -1);
+            auto fpush = [&](long long t, int w) {
+                if ((size_t)t >= fhead.size()) fhead.resize(std::max((size_t)t + 1, 2 * fhead.size()), -1);
+                fnext[w] = fhead[t];
+                fhead[t] = w;
+            };
+            for (int w = W - 1; w >= 0; w--) fpush(0, w);
+            long long fcur = 0;
             std::vector<int> qorder;
             qorder.reserve(nj);
             long long cur = -1;
@@ -1693,10 +1803,12 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 }
                 const int j = cur_b[pos++];
                 bq_n--;
-                const LI f = free_at.top(); free_at.pop();
+                while (fhead[fcur] < 0) fcur++;
+                const int fw = fhead[fcur];
+                fhead[fcur] = fnext[fw];
                 const long long t = !nsd[j] ? t_root : lmseed[j][0] >= 0 ? t_lm : t_one;
-                const long long start = std::max(f.first, cur);
-                free_at.push({start + t, f.second});
+                const long long start = std::max(fcur, cur);
+                fpush(start + t, fw);
                 qorder.push_back(j);
                 const long long rel = start + std::max(1ll, tk(flag_at * (double)t / 100.0));
                 for (int e = dbeg[j]; e < dbeg[j + 1]; e++) {
@@ -1712,10 +1824,9 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 fprintf(stderr, "plan world %d rank %d: jobs %d levels %d seeds:", world, rank, nj, nlev);
                 for (int k = 0; k <= KD_SEEDS; k++) fprintf(stderr, " %d:%d", k, hist[k]);
                 fprintf(stderr, "  closeness rows %.2f ms, rank sort done %.2f, order sort done %.2f, landmark rows %.2f ms, "
-                        "seed choices (threads) %.2f ms, seeds done %.2f, store %.2f, schedule %.2f ms\n",
-                        1e3 * t_close, 1e3 * t_rk, 1e3 * t_order, 1e3 * t_land, 1e3 * t_hop, 1e3 * t_seeds, 1e3 * t_store,
-                        1e3 * t_sched);
-                fprintf(stderr, "  seq loop start %.2f (recomputed %d), alloc done %.2f, deps done %.2f\n", 1e3 * t_loop0, n_recomp,
+                        "seed choices (threads, overlapping the pass) %.2f ms, seeds done %.2f, schedule done %.2f ms\n",
+                        1e3 * t_close, 1e3 * t_rk, 1e3 * t_order, 1e3 * t_land, 1e3 * t_hop, 1e3 * t_seeds, 1e3 * t_sched);
+                fprintf(stderr, "  seq loop start %.2f (recomputed %d), store thread started %.2f, deps done %.2f\n", 1e3 * t_loop0, n_recomp,
                         1e3 * t_alloc, 1e3 * t_deps);
             }
             jobs.resize(nj);
@@ -1729,17 +1840,18 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                     J.u[k] = su[j][k]; J.wr[k] = wr[j][k]; J.rec[k] = srec[j][k];
                 }
             }
+        }
+        if (store_th.joinable()) store_th.join();
+        t_store = since();
+        if (store_ok) {
             P->seeded = 1;
         } else {
-            if (P->d_drow) (void)hipFree(P->d_drow);
-            P->d_drow = nullptr;
+            for (void** q : {(void**)&P->d_drow, (void**)&P->d_prow, (void**)&P->d_jobs, (void**)&P->d_next})
+                if (*q) { (void)hipFree(*q); *q = nullptr; }
             P->nslots = 0; P->nroots = 0; P->nland = 0; P->store_bytes = 0;
         }
     }
     if (P->seeded) {
-        if (hipMalloc((void**)&P->d_jobs, sizeof(KDJob) * jobs.size()) != hipSuccess ||
-            hipMalloc((void**)&P->d_next, sizeof(int) * (1 + (size_t)P->nslots + P->nland)) != hipSuccess)
-            return SHD_ROUTE_ENOMEM;
         if (hipMemcpy(P->d_jobs, jobs.data(), sizeof(KDJob) * jobs.size(), hipMemcpyHostToDevice) != hipSuccess)
             return SHD_ROUTE_EDEVICE;
     } else {
@@ -1752,7 +1864,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             return SHD_ROUTE_EDEVICE;
         P->nroots = nr;
     }
-    if (getenv("SHD_ROUTE_PLAN_DEBUG")) fprintf(stderr, "  plan total %.2f ms\n", 1e3 * since());
+    if (getenv("SHD_ROUTE_PLAN_DEBUG")) fprintf(stderr, "  store thread joined %.2f, plan total %.2f ms\n", 1e3 * t_store, 1e3 * since());
     *out = P.release();
     return SHD_ROUTE_OK;
 }

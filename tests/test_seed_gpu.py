@@ -227,13 +227,16 @@ def test_c3_writer_ring_no_stall(monkeypatch):
     d_min = torch.empty(len(T), dtype=torch.float64, device=dev)
     plan.rows_async(d_tgt, d_lat, d_rel, d_min, dispatch=False)
     eng.sync()
-    worst = 0.0
+    times = []
     for _ in range(6):
         t0 = time.perf_counter()
         plan.rows_async(d_tgt, d_lat, d_rel, d_min, dispatch=False)
         eng.sync()
-        worst = max(worst, time.perf_counter() - t0)
-    assert worst < 0.04, worst
+        times.append(time.perf_counter() - t0)
+    # relative to this box's own fastest launch (a stall cost ~110 ms against ~3 ms): no
+    # launch may take 4x it (floor 20 ms for launch jitter), and the fastest is not a stall
+    fast = min(times)
+    assert fast < 0.05 and max(times) < max(4.0 * fast, 0.02), times
     row_of = {int(v): i for i, v in enumerate(T)}
     idx = torch.tensor([row_of[r["src"]] for r in dig["rows"]], device=dev)
     lat, rel = d_lat[idx].cpu().numpy(), d_rel[idx].cpu().numpy()

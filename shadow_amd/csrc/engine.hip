@@ -29,9 +29,11 @@ using namespace shd;
 // =============================================================================
 // Host side
 // =============================================================================
-// The planner's host workers: created with a context that plans (KD), parked on a condition
-// variable between plans, so a plan does not pay ~15 thread creations (~0.5 ms).  run(f)
-// starts f on every worker; wait() returns once all of them have returned from it.
+// The planner's host workers: one process-wide set, created with the first context that plans
+// (KD) and parked on a condition variable between plans, so a plan does not pay ~15 thread
+// creations (~0.5 ms).  run(f) starts f on every worker; wait() returns once all of them have
+// returned from it.  A plan that finds the set in use (plans on several devices at once)
+// starts its own.
 struct HostPool {
     std::vector<std::thread> th;
     std::mutex m;
@@ -142,12 +144,11 @@ struct shd_route {
     // landmark rows (planner): the most central vertices' distances and tie-rule parent
     // records computed on the host, uploaded as seed rows for the plan's roots
     std::vector<int> lm_v;
-    std::vector<std::vector<double>> lm_d;
-    std::vector<std::vector<uint32_t>> lm_p;
+    std::vector<uint16_t> lm_hd;  // landmark l's u16 distance of v at [l * lm_rs + v] (0xFFFF: unreached)
+    std::vector<uint32_t> lm_hp;  // and its parent record
+    long long lm_rs = 0;
     uint16_t* d_lm_drow = nullptr;  // the landmark rows in the row-store format (device)
     uint32_t* d_lm_prow = nullptr;
-    std::unique_ptr<HostPool> pool;  // the planner's host workers (KD contexts)
-    std::mutex plan_lock;            // one plan at a time uses the pool
     int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD, 5 KF
     // KF (fractional latencies, LDS-resident f64 delta-stepping)
     int kf_block = 0, kf_slots = 0;
@@ -172,7 +173,10 @@ struct shd_route {
 
 namespace {
 
-HostPool* host_pool(shd_route* c);
+HostPool* host_pool();
+int plan_threads();
+std::mutex g_pool_mu, g_pool_use;
+std::unique_ptr<HostPool> g_pool;
 
 // KD workgroup sizes: f(std::integral_constant<int, B>) for the runtime block size
 template <typename F>
@@ -901,7 +905,7 @@ int shd_route_create(shd_route_t** out, const shd_graph_t* g, int device) {
         shd_route_destroy(c);
         return rc;
     }
-    if (c->sel == 4 && c->kd_fused) host_pool(c);  // the planner's workers, parked until a plan
+    if (c->sel == 4 && c->kd_fused) host_pool();  // the planner's workers, parked until a plan
     *out = c;
     return SHD_ROUTE_OK;
 }
@@ -1234,14 +1238,17 @@ struct shd_route_plan {
 
 namespace {
 
-// the context's planner workers (created once; none when one host thread is asked for)
-HostPool* host_pool(shd_route* c) {
-    if (!c->pool) {
-        int nth = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
-        if (const char* e = getenv("SHD_ROUTE_PLAN_THREADS")) nth = std::max(1, std::min(64, atoi(e)));
-        if (nth > 1) c->pool.reset(new HostPool(nth - 1));
-    }
-    return c->pool.get();
+// host threads of a plan (the box's CPU quota is 16)
+int plan_threads() {
+    int nth = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+    if (const char* e = getenv("SHD_ROUTE_PLAN_THREADS")) nth = std::max(1, std::min(64, atoi(e)));
+    return nth;
+}
+// the process-wide planner workers (created once; none when one host thread is asked for)
+HostPool* host_pool() {
+    std::lock_guard<std::mutex> l(g_pool_mu);
+    if (!g_pool && plan_threads() > 1) g_pool.reset(new HostPool(plan_threads() - 1));
+    return g_pool.get();
 }
 
 // Exact rows of `verts` on the device for the planner: one unplanned KD launch whose jobs
@@ -1250,10 +1257,13 @@ HostPool* host_pool(shd_route* c) {
 // `parent | ridx << 16 | w << 24` of every vertex).  The store stays in dd / dp (device) and
 // is copied back into d_out / p_out.  Blocks: the planner runs once per context, before any
 // planned launch.
-int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, DevBuf& dp,
-                      std::vector<std::vector<double>>& d_out, std::vector<std::vector<uint32_t>>& p_out) {
+int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, DevBuf& dp, std::vector<uint16_t>& hd,
+                      std::vector<uint32_t>& hp) {
     const int k = (int)verts.size(), n = c->n;
     if (k == 0) return SHD_ROUTE_OK;
+    const auto h0 = std::chrono::steady_clock::now();
+    auto hs = [&]() { return 1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - h0).count(); };
+    double h_alloc = 0, h_launch = 0, h_copy = 0;
     const long long rs = kd_row_stride(n);
     std::vector<KDJob> jobs(k);
     for (int q = 0; q < k; q++) {
@@ -1268,6 +1278,7 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, D
     if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
     int rc = take_err(c);
     if (rc) return rc;
+    h_alloc = hs();
     if (hipMemcpy(dj.p, jobs.data(), sizeof(KDJob) * k, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(dn.p, 0, sizeof(int) * (1 + (size_t)k)) != hipSuccess)
         return SHD_ROUTE_EDEVICE;
@@ -1279,21 +1290,15 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, D
         return rc;
     if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
     if ((rc = take_err(c))) return rc;
-    std::vector<uint16_t> hd((size_t)rs * k);
-    std::vector<uint32_t> hp((size_t)rs * k);
+    h_launch = hs();
+    hd.resize((size_t)rs * k);
+    hp.resize((size_t)rs * k);
     if (hipMemcpy(hd.data(), dd.p, sizeof(uint16_t) * hd.size(), hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(hp.data(), dp.p, sizeof(uint32_t) * hp.size(), hipMemcpyDeviceToHost) != hipSuccess)
         return SHD_ROUTE_EDEVICE;
-    d_out.assign(k, {});
-    p_out.assign(k, {});
-    for (int q = 0; q < k; q++) {
-        d_out[q].resize(n);
-        for (int v = 0; v < n; v++) {
-            const uint16_t x = hd[(size_t)q * rs + v];
-            d_out[q][v] = x == 0xFFFFu ? INFINITY : (double)x;
-        }
-        p_out[q].assign(hp.begin() + (size_t)q * rs, hp.begin() + (size_t)q * rs + n);
-    }
+    h_copy = hs();
+    if (getenv("SHD_ROUTE_PLAN_DEBUG"))
+        fprintf(stderr, "hub rows (%d): alloc+sync %.2f, launch done %.2f, copies done %.2f ms\n", k, h_alloc, h_launch, h_copy);
     return SHD_ROUTE_OK;
 }
 
@@ -1314,16 +1319,20 @@ int ensure_hub_rows(shd_route* c, int k) {
         return deg(a) != deg(b) ? deg(a) > deg(b) : a < b;
     });
     std::vector<int> lv(ord.begin(), ord.begin() + k);
-    std::vector<std::vector<double>> D;
-    std::vector<std::vector<uint32_t>> Pr;
+    std::vector<uint16_t> hd;
+    std::vector<uint32_t> hp;
     DevBuf dd, dp;
-    int rc = device_store_rows(c, lv, dd, dp, D, Pr);
+    int rc = device_store_rows(c, lv, dd, dp, hd, hp);
     if (rc) return rc;
     const int L = std::min(k, 16);
+    const long long rs = kd_row_stride(n);
     c->close.assign(n, 0.0);
     for (int v = 0; v < n; v++) {
         double sum = 0;
-        for (int q = 0; q < L; q++) sum += D[q][v];
+        for (int q = 0; q < L; q++) {
+            const uint16_t x = hd[(size_t)q * rs + v];
+            sum += x == 0xFFFFu ? INFINITY : (double)x;
+        }
         c->close[v] = sum / L;
     }
     if (c->d_lm_drow) (void)hipFree(c->d_lm_drow);
@@ -1331,8 +1340,9 @@ int ensure_hub_rows(shd_route* c, int k) {
     c->d_lm_drow = (uint16_t*)dd.p; dd.p = nullptr;
     c->d_lm_prow = (uint32_t*)dp.p; dp.p = nullptr;
     c->lm_v = lv;
-    c->lm_d = std::move(D);
-    c->lm_p = std::move(Pr);
+    c->lm_hd = std::move(hd);
+    c->lm_hp = std::move(hp);
+    c->lm_rs = rs;
     return SHD_ROUTE_OK;
 }
 int ensure_landmarks(shd_route* c, int k) { return ensure_hub_rows(c, k); }
@@ -1621,8 +1631,13 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             return true;
         };
         const double th0 = since();
-        std::lock_guard<std::mutex> plan_guard(c->plan_lock);
-        HostPool* pool = host_pool(c);
+        HostPool* pool = host_pool();
+        std::unique_lock<std::mutex> lease(g_pool_use, std::try_to_lock);
+        std::unique_ptr<HostPool> own;  // the shared workers are busy with another plan
+        if (pool && !lease.owns_lock()) {
+            own.reset(new HostPool(plan_threads() - 1));
+            pool = own.get();
+        }
         struct PoolWait {
             HostPool* p;
             bool on;
@@ -1659,8 +1674,10 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             if (!seedable && nland > 0) {
                 // nearest landmarks by d(s, L) (undirected: d_L(s)), up to kseeds
                 std::vector<std::pair<double, int>> lc;
-                for (int l = 0; l < nland; l++)
-                    if (c->lm_d[l][s] < INFINITY && c->lm_d[l][s] < 65535.0) lc.push_back({c->lm_d[l][s], l});
+                for (int l = 0; l < nland; l++) {
+                    const uint16_t dls = c->lm_hd[(size_t)l * c->lm_rs + s];
+                    if (dls != 0xFFFFu) lc.push_back({(double)dls, l});
+                }
                 std::sort(lc.begin(), lc.end());
                 int mk = 0;
                 for (const auto& pr : lc) {
@@ -1670,8 +1687,9 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                     if (L != s) {
                         // the last arc (x, L) of the shortest s -> L path in L's tree
                         int x = s;
-                        while ((int)(c->lm_p[l][x] & 0xFFFFu) != L) x = (int)(c->lm_p[l][x] & 0xFFFFu);
-                        const uint32_t px = c->lm_p[l][x];  // L | ridx(x,L) << 16 | w << 24
+                        const uint32_t* lp = c->lm_hp.data() + (size_t)l * c->lm_rs;
+                        while ((int)(lp[x] & 0xFFFFu) != L) x = (int)(lp[x] & 0xFFFFu);
+                        const uint32_t px = lp[x];  // L | ridx(x,L) << 16 | w << 24
                         rec = (uint32_t)x | (px & 0xFFFF0000u);
                     }
                     su[j][mk] = L; wr[j][mk] = (int)pr.first; srec[j][mk] = (int)rec; lmseed[j][mk] = l;
@@ -1784,12 +1802,22 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             };
             for (int w = W - 1; w >= 0; w--) fpush(0, w);
             long long fcur = 0;
-            std::vector<int> qorder;
-            qorder.reserve(nj);
+            // each job is written into the launch's job array as it is scheduled (queue order)
+            jobs.resize(nj);
+            int qi = 0;
+            auto emit = [&](int j) {
+                KDJob& J = jobs[qi++];
+                std::memset(&J, 0, sizeof(J));
+                J.row = job_row[j]; J.s = src[job_pos[j]]; J.store = slot[j]; J.nseed = nsd[j];
+                for (int k = 0; k < nsd[j]; k++) {
+                    J.seed[k] = lmseed[j][k] >= 0 ? P->nslots + lmseed[j][k] : slot[seedjob[j][k]];
+                    J.u[k] = su[j][k]; J.wr[k] = wr[j][k]; J.rec[k] = srec[j][k];
+                }
+            };
             long long cur = -1;
             size_t pos = 0;
             if (getenv("SHD_ROUTE_SCHED") && atoi(getenv("SHD_ROUTE_SCHED")) == 0) {  // A/B: plain rank order
-                for (int j = 0; j < nj; j++) qorder.push_back(j);
+                for (int j = 0; j < nj; j++) emit(j);
                 bq_n = 0;
             }
             while (bq_n) {
@@ -1809,7 +1837,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 const long long t = !nsd[j] ? t_root : lmseed[j][0] >= 0 ? t_lm : t_one;
                 const long long start = std::max(fcur, cur);
                 fpush(start + t, fw);
-                qorder.push_back(j);
+                emit(j);
                 const long long rel = start + std::max(1ll, tk(flag_at * (double)t / 100.0));
                 for (int e = dbeg[j]; e < dbeg[j + 1]; e++) {
                     const int d = dep[e];
@@ -1828,17 +1856,6 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                         1e3 * t_close, 1e3 * t_rk, 1e3 * t_order, 1e3 * t_land, 1e3 * t_hop, 1e3 * t_seeds, 1e3 * t_sched);
                 fprintf(stderr, "  seq loop start %.2f (recomputed %d), store thread started %.2f, deps done %.2f\n", 1e3 * t_loop0, n_recomp,
                         1e3 * t_alloc, 1e3 * t_deps);
-            }
-            jobs.resize(nj);
-            int qi = 0;
-            for (int j : qorder) {
-                KDJob& J = jobs[qi++];
-                std::memset(&J, 0, sizeof(J));
-                J.row = job_row[j]; J.s = src[job_pos[j]]; J.store = slot[j]; J.nseed = nsd[j];
-                for (int k = 0; k < nsd[j]; k++) {
-                    J.seed[k] = lmseed[j][k] >= 0 ? P->nslots + lmseed[j][k] : slot[seedjob[j][k]];
-                    J.u[k] = su[j][k]; J.wr[k] = wr[j][k]; J.rec[k] = srec[j][k];
-                }
             }
         }
         if (store_th.joinable()) store_th.join();

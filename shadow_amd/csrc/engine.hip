@@ -1530,6 +1530,8 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         if (const char* e = getenv("SHD_ROUTE_SEEDS")) kseeds = std::max(1, std::min(KD_SEEDS, atoi(e)));
         if (const char* e = getenv("SHD_ROUTE_SEED_ROOTS")) nroot_min = std::max(0, atoi(e));
         if (const char* e = getenv("SHD_ROUTE_SEED_DEPTH")) depth = std::max(1, atoi(e));
+        int klm = kseeds;  // landmark seeds of a root row
+        if (const char* e = getenv("SHD_ROUTE_LMSEEDS")) klm = std::max(1, std::min(KD_SEEDS, atoi(e)));
         // seeds of each job: the kseeds neighbours u (jobs of this rank, smaller rank, level
         // below the cap) with the smallest w(s,u) + closeness(u), i.e. the likely gateways
         // of most shortest paths from s
@@ -1672,7 +1674,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             }
             int m = ch.m;
             if (!seedable && nland > 0) {
-                // nearest landmarks by d(s, L) (undirected: d_L(s)), up to kseeds
+                // nearest landmarks by d(s, L) (undirected: d_L(s)), up to klm (default kseeds)
                 std::vector<std::pair<double, int>> lc;
                 for (int l = 0; l < nland; l++) {
                     const uint16_t dls = c->lm_hd[(size_t)l * c->lm_rs + s];
@@ -1681,7 +1683,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 std::sort(lc.begin(), lc.end());
                 int mk = 0;
                 for (const auto& pr : lc) {
-                    if (mk == kseeds) break;
+                    if (mk == klm) break;
                     const int l = pr.second, L = c->lm_v[l];
                     uint32_t rec = KD_SRC_MARK;
                     if (L != s) {

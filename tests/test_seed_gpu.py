@@ -73,6 +73,38 @@ def test_seeded_equals_unseeded_shuffled_sources(kd):
     assert np.array_equal(lat, lat0) and np.array_equal(rel, rel0) and np.array_equal(mn, mn0)
 
 
+def test_plans_independent_of_host_workers(oracle_mod, kd):
+    """The plan does not depend on how its host work is spread: seed choices first and the
+    sequential pass after them (SHD_ROUTE_PIPE=0), the pass consuming the choices as the
+    workers finish them (default), and two plans at once on two contexts (the second finds
+    the shared workers busy and starts its own)."""
+    import threading
+    from shadow_amd import route
+    g = _graph("c2")
+    T = g.targets()
+    eng = route.RouteEngine(g)
+    ref = eng.plan(T).info
+    assert ref["seeded"] == 1
+    kd.setenv("SHD_ROUTE_PIPE", "0")
+    assert eng.plan(T).info == ref
+    kd.delenv("SHD_ROUTE_PIPE")
+    engs = [route.RouteEngine(g) for _ in range(2)]
+    out = [None, None]
+
+    def run(i):
+        out[i] = engs[i].plan(T).info
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert out[0] == ref and out[1] == ref
+    lat, rel, _ = engs[1].rows(T[::5], T, dispatch=False)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(T[::5], T, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat) and np.array_equal(rel, orel)
+
+
 def test_directed_plan_falls_back(oracle_mod, kd):
     from shadow_amd import route
     g = _graph("dir")

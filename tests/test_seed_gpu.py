@@ -74,10 +74,11 @@ def test_seeded_equals_unseeded_shuffled_sources(kd):
 
 
 def test_plans_independent_of_host_workers(oracle_mod, kd):
-    """The plan does not depend on how its host work is spread: seed choices first and the
-    sequential pass after them (SHD_ROUTE_PIPE=0), the pass consuming the choices as the
-    workers finish them (default), and two plans at once on two contexts (the second finds
-    the shared workers busy and starts its own)."""
+    """The plan does not depend on where its seed choices are made: on the device (default),
+    on the host workers with the sequential pass consuming them as they finish
+    (SHD_ROUTE_GPUCHOICE=0), choices first and the pass after them (SHD_ROUTE_PIPE=0), and two
+    host-choice plans at once on two contexts (the second finds the shared workers busy and
+    starts its own)."""
     import threading
     from shadow_amd import route
     g = _graph("c2")
@@ -85,6 +86,8 @@ def test_plans_independent_of_host_workers(oracle_mod, kd):
     eng = route.RouteEngine(g)
     ref = eng.plan(T).info
     assert ref["seeded"] == 1
+    kd.setenv("SHD_ROUTE_GPUCHOICE", "0")  # seed choices on the host workers, not the device
+    assert eng.plan(T).info == ref
     kd.setenv("SHD_ROUTE_PIPE", "0")
     assert eng.plan(T).info == ref
     kd.delenv("SHD_ROUTE_PIPE")

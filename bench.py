@@ -266,7 +266,7 @@ def main():
         # cache holds each unordered pair once, topology.c:1307-1336), latency as u16 where
         # exact, and all-gathers the packed segments (padded to the largest rank's)
         from shadow_amd.shard import tri_offsets, allgather_payload, TriangleIndex
-        lat16 = bool(eng.info["integer_weights"]) and 0 < eng.info["dist_bound"] < 0xFFFF
+        lat16 = bool(eng.info["lat16"])  # integer latencies and self-loops below 0xFFFF
         pos = np.asarray(plan.positions, np.int64)  # attached positions (sources = the sorted targets)
         off, tot = tri_offsets(pos, nt)
         seg_t = torch.tensor([tot], dtype=torch.int64, device=dev)
@@ -336,15 +336,15 @@ def main():
             og = OracleGraph(g)
             mine = np.asarray(pos_by_rank[world - 1])
             pick = mine[np.linspace(0, len(mine) - 1, num=min(3, len(mine))).astype(int)]
+            from shadow_amd.shard import decode_lat16
             gl, gr = gathered["lat"].cpu().numpy(), gathered["rel"].cpu().numpy()
-            if lat16:
-                gl = gl.view(np.uint16)
             gathered_ok = True
             for i in pick:
                 olat, orel, _, _ = og.source_row(int(targets[i]), targets, TIE_MINKEY)
                 k = tindex.index(np.full(nt - i, i), np.arange(i, nt))
-                L = gl[k].astype(np.float64)
-                gathered_ok &= bool(np.array_equal(L, olat[i:]) and np.array_equal(gr[k], orel[i:]))
+                L = decode_lat16(gl[k]) if lat16 else gl[k]
+                gathered_ok &= bool(np.array_equal(L, olat[i:], equal_nan=True) and
+                                    np.array_equal(gr[k], orel[i:], equal_nan=True))
     dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)

@@ -97,6 +97,8 @@ typedef struct shd_route_info {
     int32_t dist_bound;      /* K32: proven bound on every shortest-path latency (ms) */
     int32_t block;           /* threads per workgroup of the SSSP kernel */
     int32_t reserved;        /* KD: bucket width delta; KB: 1 when path attributes are fused */
+    int32_t lat16;           /* 1 when every table latency, the self-loop diagonal included, is an
+                              * integer below 0xFFFF: the SHD_ROUTE_PAYLOAD_LAT16 eligibility */
 } shd_route_info_t;
 
 int shd_route_create(shd_route_t** out, const shd_graph_t* graph, int device);
@@ -205,8 +207,9 @@ int shd_route_fill_triangle(shd_route_t* ctx, const int32_t* A, int32_t na, int3
  * keeps the targets j >= d_pos[r], packed at element offset d_off[r] - d_off[0] of
  * d_out_lat / d_out_rel (d_off: int64 per row, the caller's prefix sums of na - pos).
  * With SHD_ROUTE_PAYLOAD_LAT16 latencies go out as u16 (exact: integer latencies whose
- * shortest paths are below 65535 ms, proven at create; NaN -> 0xFFFF; else
- * SHD_ROUTE_EUNSUPPORTED), otherwise as f64; rel always as f64.  C4 over 8 GPUs: 10 B
+ * shortest paths are below 65535 ms, proven at create, and integer self-loops below 65535
+ * ms -- info.lat16; NaN -> 0xFFFF, which no latency takes; else SHD_ROUTE_EUNSUPPORTED),
+ * otherwise as f64; rel always as f64.  C4 over 8 GPUs: 10 B
  * per pair of the triangle instead of 16 B per pair of the square (0.31x the bytes). */
 #define SHD_ROUTE_PAYLOAD_LAT16 0x1u
 int shd_route_tri_payload_async(shd_route_t* ctx, const double* d_lat, const double* d_rel, int64_t ld,
@@ -214,6 +217,14 @@ int shd_route_tri_payload_async(shd_route_t* ctx, const double* d_lat, const dou
                                 void* d_out_lat, double* d_out_rel, void* stream);
 
 void* shd_route_host_alloc(size_t bytes);  /* pinned host memory (NULL on failure) */
+
+/* KD liveness counters since the last reset (no reference equivalent): s_sleep rounds the
+ * delta-stepping kernel's waves spent waiting on each other -- out[0] compute waves waiting
+ * for space in the parent-record ring, out[1] the writer wave on a reserved record not yet
+ * written, out[2] a wave on a work-queue entry not yet written; out[3] 0.  A stall (both
+ * sides of the ring spinning to their caps) shows as millions; a healthy C3 table is a few
+ * thousand at most.  Synchronises the device; reset != 0 zeroes the counters. */
+int shd_route_kd_stats(shd_route_t* ctx, uint64_t* out, int32_t reset);
 void shd_route_host_free(void* p);
 
 /* K4: all-pairs shortest latencies by blocked min-plus

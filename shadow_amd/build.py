@@ -1,6 +1,7 @@
 """Build the HIP engine in-tree for gfx950 (no JIT cache: the .so travels with the repo)."""
 from __future__ import annotations
 
+import glob
 import os
 import subprocess
 import sys
@@ -11,7 +12,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 SOURCES = [os.path.join(HERE, "csrc", "engine.hip")]
-HEADERS = [os.path.join(HERE, "csrc", f) for f in ("common.hpp", "sssp_f64.hpp", "sssp_k32.hpp", "sssp_batch.hpp", "path_attr.hpp", "sssp_k16.hpp", "sssp_delta.hpp", "direct_fw.hpp", "fw.hpp")]
+# every kernel header the engine includes (a glob: a new header cannot be left out of the
+# staleness check, as sssp_f64d.hpp was in round 3)
+HEADERS = sorted(glob.glob(os.path.join(HERE, "csrc", "*.hpp")))
 OUT = os.path.join(HERE, "libshd_route.so")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
          "-Wall", "-Wno-unused-result"]

@@ -86,6 +86,7 @@ struct shd_route {
     int device = 0;
     int n = 0, m = 0, nnz = 0;
     int directed = 0, prefer_direct = 0, complete = 0, integer_w = 0, multigraph = 0;
+    int self16 = 1;  // every self-loop latency (the table's diagonal) is an integer below 0xFFFF
     double min_w = 0;
     // device graph
     int* d_row = nullptr; int* d_col = nullptr; double* d_w = nullptr; double* d_r = nullptr;
@@ -134,6 +135,7 @@ struct shd_route {
     int vf_lossy = 0;  // some vertex factor is not exactly 1.0 (else every present f_v is a no-op)
     int kd_rone = -1;  // rtab index of exactly 1.0 (-1: none)
     char* d_kd_ws = nullptr;
+    unsigned long long* d_kd_stats = nullptr;  // KD liveness counters (shd_route_kd_stats)
     int* d_kd_next = nullptr;  // KD source queue counter
     // host copies for seeded planning (shd_route_plan_*): out-CSR, rtab index per arc and
     // the landmark closeness of every vertex (computed on the first plan)
@@ -529,6 +531,10 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 c->allocs.push_back(c->d_kd_ws);
                 if (hipMalloc((void**)&c->d_kd_next, sizeof(int)) != hipSuccess) return SHD_ROUTE_ENOMEM;
                 c->allocs.push_back(c->d_kd_next);
+                if (hipMalloc((void**)&c->d_kd_stats, sizeof(unsigned long long) * 4) != hipSuccess ||
+                    hipMemset(c->d_kd_stats, 0, sizeof(unsigned long long) * 4) != hipSuccess)
+                    return SHD_ROUTE_ENOMEM;
+                c->allocs.push_back(c->d_kd_stats);
                 for (int pk = 0; pk < 2 && !rc; pk++) {
                     const void* fn = kd_dispatch(blk, [&](auto B) {
                         return pk ? (const void*)kd_plan_rows_kernel<decltype(B)::value>
@@ -672,23 +678,26 @@ DevDelta kd_args(const shd_route* c) {
     // tests shrink the tie-event list to force the unseeded rerun of overflowing rows
     if (const char* e = getenv("SHD_ROUTE_EVCAP")) k.evcap = std::max(0, std::min(c->n, atoi(e)));
     k.next = nullptr;
+    k.stats = c->d_kd_stats;
     return k;
 }
 
 // one KD launch of ns sources (k.jobs: planned jobs, else d_src); `next` is zeroed
 int kd_launch(shd_route* c, DevDelta k, int* next, const int32_t* d_src, int ns, const int32_t* d_tgt, int nt,
-              int64_t ld, double* d_lat, double* d_rel, double* d_row_min, hipStream_t st, bool planner = false) {
+              int64_t ld, double* d_lat, double* d_rel, double* d_row_min, hipStream_t st, bool planner = false,
+              char* ws = nullptr, int max_grid = 0) {
     if (ns <= 0) return SHD_ROUTE_OK;
     k.next = next;
-    const int grid = std::min(ns, c->kd_slots);
+    if (!ws) ws = c->d_kd_ws;
+    const int grid = std::min(ns, max_grid > 0 ? std::min(max_grid, c->kd_slots) : c->kd_slots);
     kd_dispatch(c->kd_block, [&](auto B) {
         constexpr int b = decltype(B)::value;
         if (planner)
             hipLaunchKernelGGL(kd_plan_rows_kernel<b>, dim3(grid), dim3(b), c->kd_lds, st, k, d_src, ns, d_tgt,
-                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kd_ws, c->kd_stride);
+                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, ws, c->kd_stride);
         else
             hipLaunchKernelGGL(sssp_delta_kernel<b>, dim3(grid), dim3(b), c->kd_lds, st, k, d_src, ns, d_tgt,
-                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kd_ws, c->kd_stride);
+                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, ws, c->kd_stride);
         return 0;
     });
     return hip_check(hipGetLastError());
@@ -832,6 +841,8 @@ int shd_route_create(shd_route_t** out, const shd_graph_t* g, int device) {
         else { ir.push_back(b); ic.push_back(a); ie.push_back(e); }
     }
     c->integer_w = integral && (double)n * maxw < 2147483647.0;
+    for (int v = 0; v < n; v++)
+        if (!std::isnan(self_w[v]) && !(self_w[v] == std::floor(self_w[v]) && self_w[v] < 65535.0)) c->self16 = 0;
     std::vector<int> row, col, row_in, col_in, eid;
     std::vector<double> w, r, w_in, r_in;
     build_csr(n, ar, ac, ae, c->e_lat, c->e_rel, row, col, w, r, &eid);
@@ -921,6 +932,12 @@ void shd_route_destroy(shd_route_t* c) {
     delete c;
 }
 
+// u16 latency payloads are exact: integer latencies whose shortest paths are proven below
+// 0xFFFF and integer self-loops (the diagonal, kept out of the CSR and its bound) below it
+static bool lat16_ok(const shd_route* c) {
+    return c->integer_w && c->self16 && c->k32_bound > 0 && c->k32_bound < 0xFFFF;
+}
+
 int shd_route_get_info(const shd_route_t* c, shd_route_info_t* info) {
     if (!c || !info) return SHD_ROUTE_EINVAL;
     info->n_vertices = c->n;
@@ -938,6 +955,7 @@ int shd_route_get_info(const shd_route_t* c, shd_route_info_t* info) {
     info->block = c->sel == 2 ? KB_BLOCK : c->sel == 3 ? 1024 : c->sel == 4 ? c->kd_block
                 : c->sel == 1 ? c->k32_block : c->sel == 5 ? c->kf_block : kBlock;
     info->reserved = c->sel == 4 ? c->kd_delta : c->sel == 2 ? c->kb_fused : 0;
+    info->lat16 = lat16_ok(c) ? 1 : 0;
     info->device_bytes = c->device_bytes;
     info->min_edge_latency = c->min_w;
     return SHD_ROUTE_OK;
@@ -1377,11 +1395,15 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, D
         std::memset(&jobs[q], 0, sizeof(KDJob));
         jobs[q].row = -1; jobs[q].s = verts[q]; jobs[q].store = q; jobs[q].nseed = 0;
     }
-    DevBuf dj, dn;
+    // the launch's own per-workgroup scratch (at most 64 workgroups): the context's is left to
+    // its rows launches, so none of those can share it even if one is still in flight
+    const int grid = std::min(k, 64);
+    DevBuf dj, dn, dw;
     if (dj.alloc(sizeof(KDJob) * k) || dd.alloc(sizeof(uint16_t) * (size_t)rs * k) ||
-        dp.alloc(sizeof(uint32_t) * (size_t)rs * k) || dn.alloc(sizeof(int) * (1 + (size_t)k)))
+        dp.alloc(sizeof(uint32_t) * (size_t)rs * k) || dn.alloc(sizeof(int) * (1 + (size_t)k)) ||
+        dw.alloc(c->kd_stride * (size_t)grid))
         return SHD_ROUTE_ENOMEM;
-    // the context's scratch is shared with its rows launches: none may be in flight
+    // (errors of earlier launches are reported by their own sync, not by this plan)
     if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
     int rc = take_err(c);
     if (rc) return rc;
@@ -1393,7 +1415,8 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, D
     g.jobs = (const KDJob*)dj.p;
     g.drow = (const uint16_t*)dd.p; g.drow_out = (uint16_t*)dd.p; g.prow = (uint32_t*)dp.p; g.rstride = rs;
     g.done = (int*)dn.p + 1;
-    if ((rc = kd_launch(c, g, (int*)dn.p, nullptr, k, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, true)))
+    if ((rc = kd_launch(c, g, (int*)dn.p, nullptr, k, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, true,
+                        (char*)dw.p, grid)))
         return rc;
     if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
     if ((rc = take_err(c))) return rc;
@@ -2319,7 +2342,7 @@ int shd_route_tri_payload_async(shd_route_t* c, const double* d_lat, const doubl
     if (!c || nrows < 0 || na < 0 || ld < na || (nrows && (!d_lat || !d_rel || !d_pos || !d_off || !d_out_lat || !d_out_rel)))
         return SHD_ROUTE_EINVAL;
     const bool l16 = (flags & SHD_ROUTE_PAYLOAD_LAT16) != 0;
-    if (l16 && !(c->integer_w && c->k32_bound > 0 && c->k32_bound < 0xFFFF)) return SHD_ROUTE_EUNSUPPORTED;
+    if (l16 && !lat16_ok(c)) return SHD_ROUTE_EUNSUPPORTED;
     if (nrows == 0) return SHD_ROUTE_OK;
     if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
     hipStream_t st = (hipStream_t)stream;
@@ -2466,6 +2489,17 @@ int shd_route_fill_triangle(shd_route_t* c, const int32_t* A, int32_t na, int32_
 }
 
 }  // extern "C"
+
+extern "C" int shd_route_kd_stats(shd_route_t* c, uint64_t* out, int reset) {
+    if (!c || !out) return SHD_ROUTE_EINVAL;
+    for (int q = 0; q < 4; q++) out[q] = 0;
+    if (!c->d_kd_stats) return SHD_ROUTE_OK;
+    if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
+    if (hipMemcpy(out, c->d_kd_stats, sizeof(uint64_t) * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return SHD_ROUTE_EDEVICE;
+    if (reset && hipMemset(c->d_kd_stats, 0, sizeof(uint64_t) * 4) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    return SHD_ROUTE_OK;
+}
 
 #ifdef SHD_STAMPS
 // Diagnostic builds only (not part of include/shd_route.h): per-source phase stamps.

@@ -143,6 +143,9 @@ struct DevDelta {
                                         // absent, a no-op in every product: vf is not read)
     int dflags;                         // diagnostic builds: 1 = skip the output-row stores
     unsigned long long* dbg;            // SHD_STAMPS builds: KD_NACC words per source
+    unsigned long long* stats;          // liveness counters (s_sleep rounds): [0] compute waves waiting
+                                        // for writer-ring space, [1] the writer on a reserved record
+                                        // not yet written, [2] a slice on a queue entry not yet written
 };
 
 constexpr int KD_NACC = 40;
@@ -1115,8 +1118,11 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
             bool bad = s < 0 || s >= n || sm->job.nseed < 0 || sm->job.nseed > KD_SEEDS;
             for (int q = 0; q < KD_SEEDS; q++)
                 if (q < sm->job.nseed) bad = bad || sm->job.u[q] < 0 || sm->job.u[q] >= n || sm->job.seed[q] < 0;
-            if (bad) {
+            if (bad) {  // (uniform: every thread read the same job)
                 if (tid == 0) { raise_err(err, SHD_ROUTE_EINVAL); sm->npre = 0; }
+                // njb = -1 (thread 0, above) visible to every thread before the loop
+                // increment reads it: all take the next job from kd_next_source together
+                __syncthreads();
                 continue;
             }
         }
@@ -1339,6 +1345,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
                                && w8 < (1 << 22); w8++)
                             __builtin_amdgcn_s_sleep(1);
                         if (w8 >= (1 << 22)) raise_err(err, SHD_ROUTE_EDEVICE);
+                        if (w8 && g.stats) atomicAdd(&g.stats[0], (unsigned long long)w8);
                     }
                     rb = __builtin_amdgcn_readfirstlane(rb);
                     if (mine) {
@@ -1389,8 +1396,10 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
                     if (act) {
                         volatile uint16_t* slot = ring + h + lane;
                         unsigned x = *slot;
-                        for (int w8 = 0; x == 0xFFFFu && w8 < (1 << 22); w8++) { __builtin_amdgcn_s_sleep(1); x = *slot; }
+                        int w8 = 0;
+                        for (; x == 0xFFFFu && w8 < (1 << 22); w8++) { __builtin_amdgcn_s_sleep(1); x = *slot; }
                         if (x == 0xFFFFu) raise_err(err, SHD_ROUTE_EDEVICE);
+                        if (w8 && g.stats) atomicAdd(&g.stats[2], (unsigned long long)w8);
                         u = x == 0xFFFFu ? s : (int)x;
                     }
                     const unsigned du0 = act ? ld16(dist, u) : 0u;
@@ -1610,6 +1619,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
                                     rv = *sp;
                                 }
                                 if (w8 >= (1 << 22)) raise_err(err, SHD_ROUTE_EDEVICE);
+                                if (w8 && g.stats) atomicAdd(&g.stats[1], (unsigned long long)w8);
                                 const uint32_t x = (uint32_t)rv, y = (uint32_t)(rv >> 32);
                                 *sp = 0xFFFFFFFF00000000ull;
                                 const int u = (int)(y & 0xFFFFu);

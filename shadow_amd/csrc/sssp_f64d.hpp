@@ -61,6 +61,7 @@ struct KFSmall {
     int qtail;     // ring entries queued (mod n); phase B: hub list length
     int rhead;     // slices of the round taken
     int flag;
+    int ovf;       // a push of this round found no free ring slot (the ring is dropped after it)
     unsigned long long wmark[B / 64][4];  // per wave: start marks of a trip's four windows
     unsigned long long mpend[2];  // lower bound of the pending distances (bits), by gather parity
     unsigned long long rmin;
@@ -127,7 +128,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
         }
         for (int v = tid; v < n; v += B) dist[v] = kInfBits;
         for (int k = tid; k < nw; k += B) { pend[k] = 0ull; wmin[k] = kInfBits; inq[k] = 0ull; }
-        if (tid == 0) { sm->qtail = 0; sm->rhead = 0; sm->mpend[0] = sm->mpend[1] = kInfBits; }
+        if (tid == 0) { sm->qtail = 0; sm->rhead = 0; sm->ovf = 0; sm->mpend[0] = sm->mpend[1] = kInfBits; }
         int gpar = 0;  // gather parity
         for (int v = tid; v <= n; v += B) rowl[v] = g.row[v];  // (phase B reuses this LDS)
         __syncthreads();
@@ -288,8 +289,13 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                                 const unsigned long long bit = 1ull << (v & 63);
                                 if (nd < T) {  // this bucket: straight back into the ring
                                     if (!(atomicOr(&inq[v >> 6], bit) & bit)) {
+                                        // slots [qhead, qhead + n) may still hold this round's
+                                        // unread entries (a wave can take its slice and read it
+                                        // late): a push past them is dropped and flagged, and the
+                                        // round's end moves the whole ring to the pending bitmask
                                         const unsigned at = (unsigned)atomicAdd(&sm->qtail, 1);
-                                        ring[at % (unsigned)n] = (uint16_t)v;
+                                        if (at - qhead < (unsigned)n) ring[at % (unsigned)n] = (uint16_t)v;
+                                        else sm->ovf = 1;
                                     }
                                 } else {
                                     atomicOr(&pend[v >> 6], bit);
@@ -302,8 +308,17 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
             }
             __syncthreads();
             if (tid == 0) sm->rhead = 0;  // (every wave has left the loop above)
-            __syncthreads();
             qhead = qend;
+            if (sm->ovf) {  // (uniform) ring overflow: its vertices (inq) become pending, the ring empty
+                for (int k = tid; k < nw; k += B) {
+                    const unsigned long long b = inq[k];
+                    if (b) { pend[k] |= b; wmin[k] = 0ull; inq[k] = 0ull; }  // (0: a valid lower bound)
+                }
+                qhead = (unsigned)sm->qtail;
+                KF_COUNT(15);
+            }
+            __syncthreads();
+            if (tid == 0) sm->ovf = 0;  // (every thread has read it)
             KF_ACC(9);
         }
 

@@ -301,21 +301,21 @@ static double now_s(void) {
  * attach every old pair is still a pair: the attached set only grows).  A reader that
  * still holds the retired fill may count into it after this pass has read a pair:
  * packet counts are approximate across a late attach (Shadow attaches every host before
- * the simulation starts, so this does not arise there).  Each stripe's spill map is
- * read under its lock, as a concurrent wrap may be growing it. */
+ * the simulation starts, so this does not arise there).  The spill maps are read under
+ * their locks, as a concurrent wrap may be growing one: every stripe is locked once for
+ * the whole pass (a lock round trip per pair was O(na^2) of them). */
 static void carry_counters(pcache* o, pcache* c) {
+    for (int k = 0; k < PC_STRIPES; k++) pthread_mutex_lock(&o->pc[k].lock);
     for (int32_t i = 0; i < o->na; i++)
         for (int32_t j = i; j < o->na; j++) {
             const size_t ko = tri(o->na, i, j);
             uint64_t v = __atomic_load_n(&o->cnt[ko], __ATOMIC_RELAXED);
-            pcmap* m = &o->pc[pc_stripe((uint64_t)ko + 1)];
-            pthread_mutex_lock(&m->lock);
+            const pcmap* m = &o->pc[pc_stripe((uint64_t)ko + 1)];
             if (m->cap) {
                 size_t h = (((uint64_t)ko + 1) * 0x9E3779B97F4A7C15ull) & (m->cap - 1);
                 while (m->s[h].key && m->s[h].key != (uint64_t)ko + 1) h = (h + 1) & (m->cap - 1);
                 if (m->s[h].key) v += m->s[h].val;
             }
-            pthread_mutex_unlock(&m->lock);
             if (!v) continue;
             int32_t a = c->cid[o->A[i]], b = c->cid[o->A[j]];
             if (a > b) { int32_t x = a; a = b; b = x; }
@@ -326,6 +326,7 @@ static void carry_counters(pcache* o, pcache* c) {
                 *pc_slot(mm, (uint64_t)k + 1) = v & ~(uint64_t)UINT32_MAX;
             }
         }
+    for (int k = PC_STRIPES - 1; k >= 0; k--) pthread_mutex_unlock(&o->pc[k].lock);
 }
 
 static int fill_locked(shd_topology_t* t) {

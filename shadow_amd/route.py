@@ -50,6 +50,7 @@ class _Info(C.Structure):
         ("integer_weights", C.c_int32), ("multigraph", C.c_int32), ("device", C.c_int32),
         ("lds_resident", C.c_int32), ("device_bytes", C.c_uint64), ("min_edge_latency", C.c_double),
         ("kernel", C.c_int32), ("dist_bound", C.c_int32), ("block", C.c_int32), ("reserved", C.c_int32),
+        ("lat16", C.c_int32),
     ]
 
 
@@ -70,6 +71,7 @@ EXPORTS = (
     "shd_route_plan_create", "shd_route_plan_destroy", "shd_route_plan_get_info", "shd_route_plan_rows",
     "shd_route_rows_planned_async", "shd_route_fw_table_async", "shd_route_fw_rows_async",
     "shd_route_fill_triangle", "shd_route_host_alloc", "shd_route_host_free", "shd_route_tri_payload_async",
+    "shd_route_kd_stats",
 )
 
 _lib = None
@@ -125,6 +127,8 @@ def load_library():
     L.shd_route_plan_rows.argtypes = [P, P]
     L.shd_route_rows_planned_async.restype = C.c_int
     L.shd_route_rows_planned_async.argtypes = [P, P, P, I32, I64, U32, P, P, P, P]
+    L.shd_route_kd_stats.restype = C.c_int
+    L.shd_route_kd_stats.argtypes = [P, P, I32]
     _lib = L
     return L
 
@@ -257,6 +261,13 @@ class RouteEngine:
             self._h, ptr(d_lat), ptr(d_rel), ld, ptr(d_pos), ptr(d_off), nrows, int(na),
             PAYLOAD_LAT16 if lat16 else 0, ptr(out_lat), ptr(out_rel), C.c_void_p(stream) if stream else None),
             "shd_route_tri_payload_async")
+
+    def kd_stats(self, reset: bool = True):
+        """shd_route_kd_stats: KD wait counters (s_sleep rounds) since the last reset:
+        ring space, writer on an unwritten record, slice on an unwritten queue entry."""
+        out = np.zeros(4, np.uint64)
+        _check(load_library().shd_route_kd_stats(self._h, _p(out), int(reset)), "shd_route_kd_stats")
+        return [int(x) for x in out[:3]]
 
     def plan(self, sources, world: int = 1, rank: int = 0) -> "RoutePlan":
         return RoutePlan(self, sources, world, rank)

@@ -1,9 +1,11 @@
 """Multi-GPU sharding of source rows (one process per GPU, torch.distributed).
 
-Source rows are independent: attached sources are split into contiguous
-blocks, one per rank; the only exchange step is the runahead minimum (all-reduce MIN
-of one double) and, where a device-resident full table is needed, an all-gather of
-the row shards (RCCL over xGMI with backend "nccl"; gloo on CPU for tests).
+Source rows are independent.  The seeded plan (engine shd_route_plan_create)
+assigns each rank whole subtrees of the seed forest, with the heavy top levels replicated
+as helper rows (shard_range keeps the plain contiguous split for unplanned launches).  The
+exchange steps are the runahead minimum (all-reduce MIN of one double) and, where a
+device-resident full table is needed, an all-gather of the rows' upper triangles (RCCL
+over xGMI with backend "nccl"; gloo on CPU for tests).
 """
 from __future__ import annotations
 
@@ -108,6 +110,18 @@ class TriangleIndex:
         return self.start[i] + (j - i)
 
 
+LAT16_NONE = 0xFFFF  # u16 payload code of a NaN latency (no latency takes it: info["lat16"])
+
+
+def decode_lat16(x):
+    """u16 payload latencies back to the f64 table values: exact integers, 0xFFFF -> NaN."""
+    import numpy as np
+    x = np.asarray(x).view(np.uint16) if np.asarray(x).dtype == np.int16 else np.asarray(x, np.uint16)
+    out = x.astype(np.float64)
+    out[x == LAT16_NONE] = np.nan
+    return out
+
+
 def pack_triangle_host(lat_rows, rel_rows, pos, na: int, lat16: bool = True):
     """Host statement of shd_route_tri_payload_async (tests): the rows' triangles in row
     order, latency as u16 (NaN -> 0xFFFF) or f64."""
@@ -117,7 +131,7 @@ def pack_triangle_host(lat_rows, rel_rows, pos, na: int, lat16: bool = True):
     R = np.empty(tot, np.float64)
     for r, p in enumerate(pos):
         seg = lat_rows[r, p:na]
-        L[off[r]:off[r + 1]] = np.where(np.isnan(seg), 0xFFFF, seg).astype(np.uint16) if lat16 else seg
+        L[off[r]:off[r + 1]] = np.where(np.isnan(seg), LAT16_NONE, seg).astype(np.uint16) if lat16 else seg
         R[off[r]:off[r + 1]] = rel_rows[r, p:na]
     return L, R
 

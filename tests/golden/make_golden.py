@@ -94,17 +94,34 @@ def sha(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a, np.float64).tobytes()).hexdigest()
 
 
+def _embedded_graphml(f):
+    """The graphml a reference file embeds: a config's CDATA block, the first xml block of
+    a markdown doc, or the CDATA block inside a C string literal (escaped quotes, backslash
+    line continuations)."""
+    text = open(f).read()
+    if f.endswith(".md"):
+        i = text.find("<graphml")
+        j = text.find("</graphml>", i)
+        return None if i < 0 or j < 0 else text[text.rfind("<?xml", 0, i):j + len("</graphml>")]
+    if f.endswith(".c"):
+        text = text.replace("\\\n", "\n").replace('\\"', '"')
+    i = text.find("<![CDATA[")
+    if i < 0:
+        return None
+    return text[i + 9:text.find("]]>", i)]
+
+
 def ref_kats():
     out = []
     files = sorted(glob.glob(f"{REF}/src/test/**/*.config.xml", recursive=True))
-    files += [f"{REF}/resource/examples/shadow.config.xml"]
+    files += [f"{REF}/resource/examples/shadow.config.xml",
+              f"{REF}/docs/3.2-Network-Config.md",           # the documented example topology
+              f"{REF}/src/main/core/support/examples.c"]     # example_getTestContents()
     for f in files:
-        text = open(f).read()
-        i = text.find("<![CDATA[")
-        if i < 0:
+        xml = _embedded_graphml(f)
+        if xml is None:
             continue
-        j = text.find("]]>", i)
-        g = parse_graphml_text(text[i + 9:j])
+        g = parse_graphml_text(xml)
         og = O.OracleGraph(g)
         complete = og.is_complete()
         lat, rel = og.direct(0, 0) if complete else (None, None)

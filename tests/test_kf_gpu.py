@@ -136,3 +136,24 @@ def test_kf_limits_fall_back(route, monkeypatch):
     g = fractional(internet_like(1000, 3, 8, name="kf_many_r"), 4)
     g.packetloss = np.random.default_rng(1).uniform(0.0, 0.5, g.m)
     assert route.RouteEngine(g).info["kernel"] == 0
+
+
+@pytest.mark.parametrize("delta", ["1e9", "0.004", "1e-6"])
+def test_kf_extreme_bucket_widths(route, oracle_mod, monkeypatch, delta):
+    """Bucket width far above every distance (one bucket: the ring holds a Bellman-Ford
+    frontier, the case where a push could find no free slot -- ADVICE r03) and far below
+    the arc latencies (a bucket per distinct distance): bit-exact against the oracle, and
+    the overflow path (pushes moved to the pending bitmask) leaves nothing behind."""
+    g = config("c2f")
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    monkeypatch.setenv("SHD_ROUTE_KFDELTA", delta)
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 5
+    src = np.arange(3, g.n, 97, dtype=np.int32)
+    tgt = g.targets()
+    lat, rel, mn = eng.rows(src, tgt, dispatch=False)
+    og = oracle_mod.OracleGraph(g)
+    olat, orel, _, _ = og.source_rows(src, tgt, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(rel, orel)
+    assert np.array_equal(mn, olat.min(axis=1))

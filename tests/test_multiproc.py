@@ -115,7 +115,7 @@ def test_triangle_payload_gather(world, oracle_mod):
     pair of the attached set arrives once, latency exact as u16, reliability bit-exact,
     and each pair's value is the row of its smaller position (first writer over both
     directions, topology.c:1307-1336)."""
-    from shadow_amd.shard import TriangleIndex
+    from shadow_amd.shard import TriangleIndex, decode_lat16
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -133,6 +133,6 @@ def test_triangle_payload_gather(world, oracle_mod):
     ii, jj = np.triu_indices(na)
     k = start[ii] + (jj - ii)
     assert len(np.unique(k)) == len(k) and k.max() < world * seg
-    assert np.array_equal(gl[k].astype(np.float64), ref[ii, jj])
+    assert np.array_equal(decode_lat16(gl[k]), ref[ii, jj], equal_nan=True)
     assert np.array_equal(gr[k], rref[ii, jj])
     assert gl.nbytes + gr.nbytes <= 0.5 * 16 * na * na * world / world + 16 * world * na

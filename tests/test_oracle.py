@@ -36,6 +36,13 @@ def test_reference_config_kats(oracle_mod):
         assert oracle_mod.runahead_ns(lat) == k["runahead_ns"] == int(k["edge_latency"][0]) * 1_000_000
     ex = [k for k in kats if k["config"] == "resource/examples/shadow.config.xml"][0]
     assert (ex["lat"], ex["rel"], ex["runahead_ns"]) == (50.0, 0.99, 50_000_000)
+    # the documented example (docs/3.2-Network-Config.md:31-38: latency 50.0, packetloss
+    # 0.001, vertex packetloss 0.0) and example_getTestContents() (examples.c:27-45:
+    # latency 1.0, packetloss 0.0)
+    doc = [k for k in kats if k["config"] == "docs/3.2-Network-Config.md"][0]
+    assert (doc["lat"], doc["rel"], doc["runahead_ns"]) == (50.0, 1.0 - 0.001, 50_000_000)
+    exc = [k for k in kats if k["config"] == "src/main/core/support/examples.c"][0]
+    assert (exc["lat"], exc["rel"], exc["runahead_ns"]) == (1.0, 1.0, 1_000_000)
 
 
 def _bundled():

@@ -196,9 +196,29 @@ int shd_route_rows_planned_async(shd_route_t* ctx, const shd_route_plan_t* plan,
  * written (topology.c:1374-1385), *seconds_out = the wall time (nullable).  Flags as
  * shd_route_rows (SHD_ROUTE_DISPATCH for the topology.c:2019 dispatch).  The rank's rows
  * are held whole in HBM (2 x 8 x rows x na bytes + 2 GiB; C4 on one GPU: 41 GB): a
- * larger request is SHD_ROUTE_ENOMEM (shard it over more devices). */
+ * larger request is SHD_ROUTE_ENOMEM (shard it over more devices).
+ *
+ * With SHD_ROUTE_FILL_LAT16 in flags the triangle is the compact layout instead (10.7 B per
+ * pair against 16): row i starts a 64-byte line at line shd_route_tri16_line(na, i), and
+ * its pairs j >= i go six to a line, pair e = j - i in line row_start + e / 6 at slot
+ * e % 6 -- the line holds rel as 6 doubles (bytes 0-47), then lat as 6 u16 (bytes 48-59,
+ * 0xFFFF = NaN), 4 pad bytes; a lookup is still one cache line.  Exact only when every
+ * latency written is an integer below 0xFFFF (info.lat16, and the caller's direct-path
+ * and self-path latencies): else SHD_ROUTE_EUNSUPPORTED.  lr_out then points at
+ * 64 * shd_route_tri16_line(na, na) bytes (16-byte aligned). */
+#define SHD_ROUTE_FILL_LAT16 0x100u
 int shd_route_fill_triangle(shd_route_t* ctx, const int32_t* A, int32_t na, int32_t world, int32_t rank,
                             uint32_t flags, double* lr_out, double* min_out, double* seconds_out);
+
+/* first 64-byte line of row i in the SHD_ROUTE_FILL_LAT16 triangle (i = na: the line count):
+ * sum over r < i of ceil((na - r) / 6) */
+static inline int64_t shd_route_tri16_line(int32_t na, int32_t i) {
+    /* sum of (na - r) over r < i, plus the pads (6 - (na - r) % 6) % 6: period 6, sum 15 */
+    int64_t pairs = (int64_t)i * na - (int64_t)i * (i - 1) / 2;
+    int64_t pad = (int64_t)(i / 6) * 15;
+    for (int32_t t = 0; t < i % 6; t++) pad += (6 - ((na - t) % 6 + 6) % 6) % 6;
+    return (pairs + pad) / 6;
+}
 /* ---- multi-GPU table assembly payload (no reference equivalent: Shadow 1.14 is one
  * process, master.c:414-416).  The Path cache needs each unordered pair once
  * (topology.c:1307-1336: the first writer stores both directions), so the rows a rank

@@ -104,6 +104,11 @@ uint64_t shd_topology_runahead_ns(shd_topology_t* top);
 /* Explicit eager fill (otherwise done by the first accessor); seconds spent in
  * *elapsed_s (nullable), like shortestPathTotalTime (topology.c:1751-1788). */
 int shd_topology_fill(shd_topology_t* top, double* elapsed_s);
+/* Host bytes of the current fill's triangle (0 before the first fill): 16 per pair
+ * (interleaved lat/rel doubles) or the compact layout of shd_route_fill_triangle
+ * (SHD_ROUTE_FILL_LAT16, 64 bytes per six pairs of a row), chosen at creation when every
+ * stored latency is an integer below 0xFFFF (env SHD_TOPOLOGY_LAT16=0 keeps the doubles). */
+uint64_t shd_topology_triangle_bytes(shd_topology_t* top);
 
 /* _topology_logAllCachedPaths (topology.c:1929-1967): one line per cached Path. */
 int shd_topology_dump_paths(shd_topology_t* top, FILE* out);

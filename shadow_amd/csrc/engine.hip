@@ -87,7 +87,7 @@ struct shd_route {
     int n = 0, m = 0, nnz = 0;
     int directed = 0, prefer_direct = 0, complete = 0, integer_w = 0, multigraph = 0;
     int self16 = 1;  // every self-loop latency (the table's diagonal) is an integer below 0xFFFF
-    double min_w = 0;
+    double min_w = 0, max_w = 0;
     // device graph
     int* d_row = nullptr; int* d_col = nullptr; double* d_w = nullptr; double* d_r = nullptr;
     int* d_row_in = nullptr; int* d_col_in = nullptr; double* d_w_in = nullptr; double* d_r_in = nullptr;
@@ -673,6 +673,7 @@ DevDelta kd_args(const shd_route* c) {
 #ifdef SHD_STAMPS
     if (const char* e = getenv("SHD_ROUTE_DFLAGS")) k.dflags = atoi(e);
 #endif
+
     k.jobs = nullptr; k.drow = nullptr; k.drow_out = nullptr; k.prow = nullptr; k.rstride = 0; k.evcap = c->n;
     k.done = nullptr;
     // tests shrink the tie-event list to force the unseeded rerun of overflowing rows
@@ -841,6 +842,7 @@ int shd_route_create(shd_route_t** out, const shd_graph_t* g, int device) {
         else { ir.push_back(b); ic.push_back(a); ie.push_back(e); }
     }
     c->integer_w = integral && (double)n * maxw < 2147483647.0;
+    c->max_w = maxw;
     for (int v = 0; v < n; v++)
         if (!std::isnan(self_w[v]) && !(self_w[v] == std::floor(self_w[v]) && self_w[v] < 65535.0)) c->self16 = 0;
     std::vector<int> row, col, row_in, col_in, eid;
@@ -2296,6 +2298,43 @@ __global__ __launch_bounds__(256) void tri_pack_kernel(const double* __restrict_
     }
 }
 
+// the same into the compact SHD_ROUTE_FILL_LAT16 layout: row r's pairs six to a 64-byte line
+// (rel f64 x 6, lat u16 x 6 with NaN -> 0xFFFF, 4 pad bytes) from line loff[r] - loff[r0]
+__global__ __launch_bounds__(256) void tri_pack16_kernel(const double* __restrict__ lat, const double* __restrict__ rel,
+                                                         long long ld, const int* __restrict__ pos,
+                                                         const long long* __restrict__ loff, int r0, int r1, int na,
+                                                         uint4* __restrict__ out, unsigned long long* __restrict__ mn) {
+    for (int r = r0 + blockIdx.x; r < r1; r += gridDim.x) {
+        const int i = pos[r];
+        const double* lr = lat + (long long)r * ld;
+        const double* rr = rel + (long long)r * ld;
+        uint4* o = out + 4 * (loff[r] - loff[r0]);
+        const int nl = (na - i + 5) / 6;
+        double m = INFINITY;
+        for (int l = threadIdx.x; l < nl; l += 256) {
+            double R[6];
+            uint32_t L16[3] = {0u, 0u, 0u};
+#pragma unroll
+            for (int e = 0; e < 6; e++) {
+                const int j = i + 6 * l + e;
+                const double L = j < na ? lr[j] : NAN;
+                R[e] = j < na ? rr[j] : 0.0;
+                if (!isnan(L)) m = fmin(m, L);
+                const uint32_t x = isnan(L) ? 0xFFFFu : (uint32_t)L;
+                L16[e >> 1] |= x << (16 * (e & 1));
+            }
+            uint4* q = o + 4 * (long long)l;
+            q[0] = make_uint4((uint32_t)as_u(R[0]), (uint32_t)(as_u(R[0]) >> 32), (uint32_t)as_u(R[1]), (uint32_t)(as_u(R[1]) >> 32));
+            q[1] = make_uint4((uint32_t)as_u(R[2]), (uint32_t)(as_u(R[2]) >> 32), (uint32_t)as_u(R[3]), (uint32_t)(as_u(R[3]) >> 32));
+            q[2] = make_uint4((uint32_t)as_u(R[4]), (uint32_t)(as_u(R[4]) >> 32), (uint32_t)as_u(R[5]), (uint32_t)(as_u(R[5]) >> 32));
+            q[3] = make_uint4(L16[0], L16[1], L16[2], 0u);
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) m = fmin(m, __shfl_xor(m, d, 64));
+        if ((threadIdx.x & 63) == 0 && m < INFINITY) atomicMin(mn, as_u(m));
+    }
+}
+
 // multi-GPU table assembly payload: row r (caller position pos[r] in the attached list)
 // keeps its upper-triangle targets j >= pos[r]; lat goes out as u16 (integer latencies
 // below 65535, NaN -> 0xFFFF) or f64, rel as f64, each into its own packed array at
@@ -2403,6 +2442,13 @@ int shd_route_fill_triangle(shd_route_t* c, const int32_t* A, int32_t na, int32_
                             double* lr_out, double* min_out, double* seconds_out) {
     if (!c || na < 0 || (na && (!A || !lr_out)) || world < 1 || rank < 0 || rank >= world) return SHD_ROUTE_EINVAL;
     if (min_out) *min_out = INFINITY;
+    const bool l16 = (flags & SHD_ROUTE_FILL_LAT16) != 0;
+    // u16 latencies are exact for the source paths (info.lat16) and, with the dispatch, for
+    // the direct paths it writes (edge latencies)
+    if (l16 && !(lat16_ok(c) && (!(flags & SHD_ROUTE_DISPATCH) || !(c->complete || c->prefer_direct) ||
+                                 c->max_w < 65535.0)))
+        return SHD_ROUTE_EUNSUPPORTED;
+    flags &= ~SHD_ROUTE_FILL_LAT16;
     if (na == 0) return SHD_ROUTE_OK;
     if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
     auto t0 = std::chrono::steady_clock::now();
@@ -2419,6 +2465,12 @@ int shd_route_fill_triangle(shd_route_t* c, const int32_t* A, int32_t na, int32_
     off[nr] = off[nr - 1] + (na - P->row_pos[nr - 1]);
     std::vector<long long> roff(nr + 1, 0);  // packed offsets (pairs) in plan row order
     for (int r = 0; r < nr; r++) roff[r + 1] = roff[r] + (na - P->row_pos[r]);
+    // the compact layout in 64-byte lines: triangle line of each row, packed lines in row order
+    std::vector<long long> loff(nr + 1), rline(nr + 1, 0);
+    if (l16) {
+        for (int r = 0; r < nr; r++) loff[r] = shd_route_tri16_line(na, P->row_pos[r]);
+        for (int r = 0; r < nr; r++) rline[r + 1] = rline[r] + (na - P->row_pos[r] + 5) / 6;
+    }
     const size_t table = sizeof(double) * (size_t)nr * (size_t)na;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) return SHD_ROUTE_EDEVICE;
@@ -2439,6 +2491,8 @@ int shd_route_fill_triangle(shd_route_t* c, const int32_t* A, int32_t na, int32_
               hipMemcpy(dpos.p, posv.data(), sizeof(int) * nr, hipMemcpyHostToDevice) == hipSuccess &&
               hipMemcpy(doff.p, roff.data(), sizeof(long long) * (nr + 1), hipMemcpyHostToDevice) == hipSuccess &&
               hipMemsetAsync(dmn.p, 0xFF, sizeof(unsigned long long), cs) == hipSuccess;
+    if (ok && l16)
+        ok = hipMemcpy(doff.p, rline.data(), sizeof(long long) * (nr + 1), hipMemcpyHostToDevice) == hipSuccess;
     if (ok) rc = shd_route_rows_planned_async(c, P, (const int32_t*)dtgt.p, na, na, flags, (double*)dlat.p,
                                               (double*)drel.p, nullptr, cs);
     else rc = SHD_ROUTE_EDEVICE;
@@ -2448,24 +2502,38 @@ int shd_route_fill_triangle(shd_route_t* c, const int32_t* A, int32_t na, int32_
     for (int b = 0; b < 2; b++) { (void)hipEventCreateWithFlags(&packed[b], hipEventDisableTiming); (void)hipEventCreateWithFlags(&copied[b], hipEventDisableTiming); }
     int buf = 0;
     bool first[2] = {true, true};
+    const std::vector<long long>& pk = l16 ? rline : roff;  // packed units: lines or pairs
+    const long long stage_units = l16 ? (long long)(16 * stage_pairs / 64) : (long long)stage_pairs;
     for (int r0 = 0; r0 < nr && !rc; buf ^= 1) {
         int r1 = r0;
-        while (r1 < nr && roff[r1 + 1] - roff[r0] <= (long long)stage_pairs) r1++;
+        while (r1 < nr && pk[r1 + 1] - pk[r0] <= stage_units) r1++;
         if (r1 == r0) r1 = r0 + 1;  // (a row longer than a stage buffer cannot happen: na < 2^25)
         if (!first[buf] && hipStreamWaitEvent(cs, copied[buf], 0) != hipSuccess) { rc = SHD_ROUTE_EDEVICE; break; }
         first[buf] = false;
-        hipLaunchKernelGGL(tri_pack_kernel, dim3(std::min(r1 - r0, 4096)), dim3(256), 0, cs, (const double*)dlat.p,
-                           (const double*)drel.p, (long long)na, (const int*)dpos.p, (const long long*)doff.p, r0, r1,
-                           na, (double*)dstage[buf].p, (unsigned long long*)dmn.p);
+        if (l16)
+            hipLaunchKernelGGL(tri_pack16_kernel, dim3(std::min(r1 - r0, 4096)), dim3(256), 0, cs, (const double*)dlat.p,
+                               (const double*)drel.p, (long long)na, (const int*)dpos.p, (const long long*)doff.p, r0, r1,
+                               na, (uint4*)dstage[buf].p, (unsigned long long*)dmn.p);
+        else
+            hipLaunchKernelGGL(tri_pack_kernel, dim3(std::min(r1 - r0, 4096)), dim3(256), 0, cs, (const double*)dlat.p,
+                               (const double*)drel.p, (long long)na, (const int*)dpos.p, (const long long*)doff.p, r0, r1,
+                               na, (double*)dstage[buf].p, (unsigned long long*)dmn.p);
         if (hipGetLastError() != hipSuccess || hipEventRecord(packed[buf], cs) != hipSuccess ||
             hipStreamWaitEvent(xs, packed[buf], 0) != hipSuccess) { rc = SHD_ROUTE_EDEVICE; break; }
         // copy: consecutive rows with consecutive triangle offsets go out in one piece
         for (int a = r0; a < r1;) {
             int b = a + 1;
-            while (b < r1 && off[b] == off[b - 1] + (na - P->row_pos[b - 1])) b++;
-            const size_t pairs = (size_t)(roff[b] - roff[a]);
-            if (hipMemcpyAsync(lr_out + 2 * off[a], (double*)dstage[buf].p + 2 * (roff[a] - roff[r0]), 16 * pairs,
-                               hipMemcpyDeviceToHost, xs) != hipSuccess) { rc = SHD_ROUTE_EDEVICE; break; }
+            if (l16) {
+                while (b < r1 && loff[b] == loff[b - 1] + (na - P->row_pos[b - 1] + 5) / 6) b++;
+                const size_t lines = (size_t)(rline[b] - rline[a]);
+                if (hipMemcpyAsync((char*)lr_out + 64 * loff[a], (char*)dstage[buf].p + 64 * (rline[a] - rline[r0]),
+                                   64 * lines, hipMemcpyDeviceToHost, xs) != hipSuccess) { rc = SHD_ROUTE_EDEVICE; break; }
+            } else {
+                while (b < r1 && off[b] == off[b - 1] + (na - P->row_pos[b - 1])) b++;
+                const size_t pairs = (size_t)(roff[b] - roff[a]);
+                if (hipMemcpyAsync(lr_out + 2 * off[a], (double*)dstage[buf].p + 2 * (roff[a] - roff[r0]), 16 * pairs,
+                                   hipMemcpyDeviceToHost, xs) != hipSuccess) { rc = SHD_ROUTE_EDEVICE; break; }
+            }
             a = b;
         }
         if (hipEventRecord(copied[buf], xs) != hipSuccess) rc = SHD_ROUTE_EDEVICE;

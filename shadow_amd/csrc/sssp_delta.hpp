@@ -189,6 +189,8 @@ struct KDSmall {
     int evovf;          // seeded: more tie events than the slice holds (rerun unseeded)
     int tsorted;        // the target list is strictly increasing: positions from tmask/tpre
     int jflag[3];       // phase C pointer jumping: "some pointer moved" per round (mod 3)
+    int wnext;          // phase C walks (wdyn): the next block of targets
+    int wnext2, novf;   // phase C capped walks (KD_WCAP): next block of the second pass, chains listed
     KDJob job;          // the current job (kept in LDS: read where needed, not held in
                         // registers across phase A, whose expansion needs all of them)
     // Pre-init (planned launches, B >= 1024): the next job is taken at the start of this
@@ -256,6 +258,26 @@ struct KDLayout {
 constexpr int KD_MAXD = 32;           // phase C path walk: arcs held in registers
 #ifndef KD_PREW
 #define KD_PREW 0                     // waves pre-initialising the next row during the walk (0: off)
+#endif
+// build-time variants (A/B builds, tools/build_var.sh; the defaults are the shipped kernel)
+#ifndef KD_SDIV
+#define KD_SDIV 0   // phase A: a grab takes max(KD_SMIN, queued / KD_SDIV) entries, at most 64 (0: min(64, queued))
+#endif
+#ifndef KD_SMIN
+#define KD_SMIN 16
+#endif
+#ifndef KD_WDYN
+#define KD_WDYN 0   // phase C: waves take 128-target walk blocks from a counter (0: static blocks)
+#endif
+#ifndef KD_WCAP
+#define KD_WCAP 0   // phase C: first-pass walks capped at KD_WCAP blocks of 4 arcs, the rest in a second pass (0: one pass)
+#endif
+static_assert(KD_WCAP == 0 || KD_PREW == 0, "the capped walk's second pass needs every wave");
+#ifndef KD_FUSELAT
+#define KD_FUSELAT 0  // phase C: the lat row written inside the pipelined parent copy (identity target lists)
+#endif
+#ifndef KD_ICOND
+#define KD_ICOND 0  // seeded init: a seed's records loaded only for 4-vertex groups where it attains D0
 #endif
 constexpr int KD_PRESPIN = 32;        // pre-init: polls of a seed's flag (s_sleep 8 each) before giving up
 constexpr int KD_WQ = 2;              // phase C path walk: targets per thread (4 measured 1% slower at C4: its registers put 39 VGPRs of the output function in callee-saved ranges, saved to scratch and restored around every row; 2: 13)
@@ -597,7 +619,14 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
         else { Lv = (double)dist[t]; lmin = fmin(lmin, Lv); }
         return Lv;
     };
-    if (tsorted) {
+    // fused lat row (KD_FUSELAT, the walk path over an identity target list, i.e. every vertex a
+    // target in order: positions = vertex ids): the lat row goes out inside the parent copy
+    // below, the copy's record loads for the next trip issued before this trip's stores, so
+    // neither waits for the other (one in-order vmcnt per wave)
+    const bool fuse_lat = KD_FUSELAT && g.walk && rrow && lrow && tsorted && nt == n &&
+                          !(((uintptr_t)lrow >> 3) & 1);
+    if (fuse_lat) {
+    } else if (tsorted) {
         // two adjacent vertices per lane: consecutive positions go out as one 16-B store
         const int lpar = (int)(((uintptr_t)lrow >> 3) & 1);
         for (int v = 2 * tid; v < (i >= 0 ? n : 0); v += 2 * B) {
@@ -622,7 +651,7 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
     // taken after every job it seeds from), so the pre-init waves below can stream its seeds
     const bool queued = sm->jobs != nullptr;
     if (tid == 0) {
-        sm->deep = 0; sm->rmin = kInfBits;
+        sm->deep = 0; sm->rmin = kInfBits; sm->wnext = 0; sm->wnext2 = 0; sm->novf = 0;
         if (queued) sm->njb = atomicAdd(sm->qnext, 1);
     }
     __syncthreads();
@@ -650,21 +679,17 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
         // vertices per trip: C4 takes 4 trips instead of the 7 of one 4-B load per vertex)
         // (wpr rows hold n + 8 records, dist n + 1 entries padded to 16 B: the last group's
         // reads stay inside; its writes past n are dropped)
-        for (int v0 = 4 * tid; v0 < n; v0 += 16 * B) {
-            kd_u4 pr[4];
+        auto copy_trip = [&](const int v0, const kd_u4 (&pr)[4], const bool with_lat) __attribute__((always_inline)) {
             uint2 dv[4];
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int vq = min(v0 + q * 4 * B, (n - 1) & ~3);
-                pr[q] = *reinterpret_cast<const KD_GLOBAL kd_u4*>(wpr + vq);
-                dv[q] = *reinterpret_cast<const uint2*>(dist + vq);
-            }
+            for (int q = 0; q < 4; q++) dv[q] = *reinterpret_cast<const uint2*>(dist + min(v0 + q * 4 * B, (n - 1) & ~3));
             // (each thread overwrites only the dist entries it read itself)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int vb = v0 + q * 4 * B;
                 if (vb >= n) continue;
                 uint32_t pw[2] = {0u, 0u}, rw = 0u;
+                double Lq[4];
 #pragma unroll
                 for (int h = 0; h < 4; h++) {
                     const int v = vb + h;
@@ -678,16 +703,55 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                                         : ri == (uint32_t)rone ? (uint32_t)KD_ONE : ri;
                     pw[h >> 1] |= pv << (16 * (h & 1));
                     rw |= rx << (8 * h);
+                    if (with_lat) {  // lat_of(v) from the distance in hand
+                        double Lv = 0.0;
+                        if (v < n) {
+                            if (src_v) {
+                                if (isnan(sw_s)) { raise_err(err, SHD_ROUTE_ENOEDGE); Lv = NAN; }
+                                else { Lv = 0.0 + sw_s; lmin = fmin(lmin, Lv); }
+                            } else if (unr) { raise_err(err, SHD_ROUTE_EUNREACH); Lv = NAN; }
+                            else { Lv = (double)d; lmin = fmin(lmin, Lv); }
+                        }
+                        Lq[h] = Lv;
+                    }
                 }
                 if (vb + 4 <= n) {
+                    if (with_lat && KD_OUT) {
+                        __builtin_nontemporal_store(kd_d2{Lq[0], Lq[1]}, reinterpret_cast<KD_GLOBAL kd_d2*>(lrow + vb));
+                        __builtin_nontemporal_store(kd_d2{Lq[2], Lq[3]}, reinterpret_cast<KD_GLOBAL kd_d2*>(lrow + vb + 2));
+                    }
                     *reinterpret_cast<uint2*>(parv + vb) = make_uint2(pw[0], pw[1]);
                     *reinterpret_cast<uint32_t*>(rixl + vb) = rw;
                 } else {
                     for (int h = 0; h < n - vb; h++) {
+                        if (with_lat && KD_OUT) __builtin_nontemporal_store(Lq[h], lrow + vb + h);
                         parv[vb + h] = (uint16_t)((pw[h >> 1] >> (16 * (h & 1))) & 0xFFFFu);
                         rixl[vb + h] = (uint8_t)((rw >> (8 * h)) & 0xFFu);
                     }
                 }
+            }
+        };
+        auto load_trip = [&](const int v0, kd_u4 (&pr)[4]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                pr[q] = *reinterpret_cast<const KD_GLOBAL kd_u4*>(wpr + min(v0 + q * 4 * B, (n - 1) & ~3));
+        };
+        if (fuse_lat) {
+            // software-pipelined: trip k + 1's record loads go out before trip k's lat stores
+            kd_u4 pa[4], pb[4];
+            load_trip(4 * tid, pa);
+            for (int v0 = 4 * tid; v0 < n; v0 += 32 * B) {
+                load_trip(v0 + 16 * B, pb);
+                copy_trip(v0, pa, true);
+                if (v0 + 16 * B >= n) break;
+                load_trip(v0 + 32 * B, pa);
+                copy_trip(v0 + 16 * B, pb, true);
+            }
+        } else {
+            for (int v0 = 4 * tid; v0 < n; v0 += 16 * B) {
+                kd_u4 pr[4];
+                load_trip(v0, pr);
+                copy_trip(v0, pr, false);
             }
         }
         __syncthreads();
@@ -752,33 +816,27 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
         const bool pre = KD_PREW > 0 && B >= 1024 && njb >= 0 && __builtin_amdgcn_readfirstlane(sm->njob.nseed) > 0;
         const int BW = pre ? B - 64 * KD_PREW : B;
         if (tid < BW) {
-        for (int j0 = tid; j0 < lim; j0 += KD_WQ * BW) {
-            // KD_WQ targets per thread: independent parent chains in flight.  A chain that
-            // reaches the source stays there (parv[s] = s, factor 1.0), so a step is two LDS
-            // reads and a byte insert, and the wave stops when every chain is parked.
-            int t2[KD_WQ], cur[KD_WQ], jq[KD_WQ];
-            uint32_t pk[KD_WQ][KD_MAXD / 4];
+        // one set of KD_WQ chains per thread: walk <= NB blocks of 4 arcs, fold source-first,
+        // store.  In a capped first pass (ovl != nullptr) a chain still short of the source
+        // after NB blocks is listed in ovl (v | j << 16) instead of stored, and the second pass
+        // walks the listed chains again in dense waves: a wave then runs for its deepest
+        // ordinary chain, not for the deepest chain of any 128 targets (KD_WCAP)
+        auto walk_set = [&](auto NBC, int (&t2)[KD_WQ], int (&jq)[KD_WQ], KD_GLOBAL uint32_t* ovl)
+                            __attribute__((always_inline)) {
+            constexpr int NB = decltype(NBC)::value;
+            int cur[KD_WQ];
+            uint32_t pk[KD_WQ][NB];
 #pragma unroll
             for (int q = 0; q < KD_WQ; q++) {
-                const int j = j0 + q * BW;
-                if (tsorted) {
-                    // chains (0, 1) and (2, 3) are adjacent vertices: paired 16-B stores
-                    const int v = (j0 - tid) + (q >> 1) * 2 * BW + 2 * tid + (q & 1);
-                    jq[q] = v < n ? tpos(v) : -1;
-                    t2[q] = jq[q] >= 0 ? v : -1;
-                } else {
-                    jq[q] = j < nt ? j : -1;
-                    t2[q] = j < nt ? tgt[j] : -1;
-                }
                 cur[q] = t2[q] >= 0 && t2[q] < n ? t2[q] : s;
 #pragma unroll
-                for (int k = 0; k < KD_MAXD / 4; k++) pk[q][k] = 0u;
+                for (int k = 0; k < NB; k++) pk[q][k] = 0u;
             }
             // blocks of 4 arcs (parked chains multiply an exact 1.0, so the padding is
             // harmless): one packed word per chain and block keeps the loop off the VALU
             int nb = 0;  // blocks walked, wave-uniform (unrolled: pk stays in registers)
 #pragma unroll
-            for (int b = 0; b < KD_MAXD / 4; b++) {
+            for (int b = 0; b < NB; b++) {
                 bool any = false;
 #pragma unroll
                 for (int q = 0; q < KD_WQ; q++) any = any || cur[q] != s;
@@ -799,7 +857,24 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                 for (int q = 0; q < KD_WQ; q++) pk[q][b] = acc[q];
                 nb = b + 1;
             }
-            {
+            if (ovl) {
+#pragma unroll
+                for (int q = 0; q < KD_WQ; q++) {
+                    const bool more = cur[q] != s;  // (t2 >= 0: parked chains sit at s)
+                    const unsigned long long m = __ballot(more);
+                    if (m) {
+                        int base = 0;
+                        if (lane == 0) base = atomicAdd(&sm->novf, __popcll(m));
+                        base = __builtin_amdgcn_readfirstlane(base);
+                        if (more) {
+                            const int at = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                            ovl[at] = (uint32_t)t2[q] | ((uint32_t)jq[q] << 16);
+                            jq[q] = -1;  // stored by the second pass
+                        }
+                    }
+                }
+            } else {
                 bool any = false;
 #pragma unroll
                 for (int q = 0; q < KD_WQ; q++) any = any || cur[q] != s;
@@ -809,7 +884,7 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
 #pragma unroll
             for (int q = 0; q < KD_WQ; q++) rr[q] = cs;
 #pragma unroll
-            for (int k4 = KD_MAXD / 4 - 1; k4 >= 0; k4--) {  // source-first: the last arc walked first
+            for (int k4 = NB - 1; k4 >= 0; k4--) {  // source-first: the last arc walked first
                 if (k4 >= nb) continue;  // (uniform)
                 uint32_t wq[KD_WQ];
 #pragma unroll
@@ -849,6 +924,66 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                         if (jb >= 0) __builtin_nontemporal_store(Rv[q + 1], rrow + jb);
                     }
                 }
+            }
+        };
+        // blocks of KD_WQ x WB targets: the whole workgroup's threads share a block in turn
+        // (static), or each wave takes the next block of KD_WQ x 64 from a counter (wdyn: a
+        // wave of shallow chains takes more blocks, no wave waits at the barrier for another)
+        constexpr bool wdyn = KD_WDYN != 0;
+        const int WB = wdyn ? 64 : BW;
+        const int li = wdyn ? lane : tid;  // this thread's place in its block
+        // (capped first pass: its list over relv's HBM slice, unused by the walks)
+        KD_GLOBAL uint32_t* const ovl = KD_WCAP > 0 ? reinterpret_cast<KD_GLOBAL uint32_t*>(relv) : nullptr;
+        for (int blk = 0;; blk++) {
+            int jbase;
+            if constexpr (wdyn) {
+                int c = 0;
+                if (lane == 0) c = atomicAdd(&sm->wnext, 1);
+                jbase = __builtin_amdgcn_readfirstlane(c) * (KD_WQ * 64);
+            } else {
+                jbase = blk * (KD_WQ * BW);
+            }
+            if (jbase >= lim) break;
+            const int j0 = jbase + li;
+            // KD_WQ targets per thread: independent parent chains in flight.  A chain that
+            // reaches the source stays there (parv[s] = s, factor 1.0), so a step is two LDS
+            // reads and a byte insert, and the wave stops when every chain is parked.
+            int t2[KD_WQ], jq[KD_WQ];
+#pragma unroll
+            for (int q = 0; q < KD_WQ; q++) {
+                const int j = j0 + q * WB;
+                if (tsorted) {
+                    // chains (0, 1) and (2, 3) are adjacent vertices: paired 16-B stores
+                    const int v = jbase + (q >> 1) * 2 * WB + 2 * li + (q & 1);
+                    jq[q] = v < n ? tpos(v) : -1;
+                    t2[q] = jq[q] >= 0 ? v : -1;
+                } else {
+                    jq[q] = j < nt ? j : -1;
+                    t2[q] = j < nt ? tgt[j] : -1;
+                }
+            }
+            if constexpr (KD_WCAP > 0) walk_set(std::integral_constant<int, KD_WCAP>{}, t2, jq, ovl);
+            else walk_set(std::integral_constant<int, KD_MAXD / 4>{}, t2, jq, nullptr);
+        }
+        if constexpr (KD_WCAP > 0) {
+            // second pass: the listed chains, 128 per wave-block, walked in full
+            wait_stores();  // (the list, in HBM, visible to every wave)
+            __syncthreads();
+            const int novf = sm->novf;
+            for (;;) {
+                int c = 0;
+                if (lane == 0) c = atomicAdd(&sm->wnext2, 1);
+                const int e0 = __builtin_amdgcn_readfirstlane(c) * (KD_WQ * 64);
+                if (e0 >= novf) break;
+                int t2[KD_WQ], jq[KD_WQ];
+#pragma unroll
+                for (int q = 0; q < KD_WQ; q++) {
+                    const int e = e0 + q * 64 + lane;
+                    const uint32_t x = e < novf ? ovl[e] : 0xFFFFFFFFu;
+                    t2[q] = e < novf ? (int)(x & 0xFFFFu) : -1;
+                    jq[q] = e < novf ? (int)(x >> 16) : -1;
+                }
+                walk_set(std::integral_constant<int, KD_MAXD / 4>{}, t2, jq, nullptr);
             }
         }
 #ifdef SHD_STAMPS
@@ -1186,6 +1321,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
             // parents of the seeds attaining D0(v), u_j's own vertex having parent s.  Phase
             // A's records overwrite the vertices that do improve.
             // 4 vertices per lane: 8-B distance and 16-B parent-record loads of every seed
+            constexpr bool icond = KD_ICOND != 0;
             for (int v0 = 4 * tid; v0 <= n; v0 += 4 * B) {
                 const int vl = min(v0, n & ~3);
                 uint2 dq[KD_SEEDS];
@@ -1194,10 +1330,37 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
                 for (int q = 0; q < KD_SEEDS; q++) {
                     if (q < nseed) {
                         dq[q] = *reinterpret_cast<const uint2*>(sdrow[q] + vl);
-                        pq[q] = *reinterpret_cast<const uint4*>(sprow[q] + vl);
+                        if (!icond) pq[q] = *reinterpret_cast<const uint4*>(sprow[q] + vl);
                     } else {
                         dq[q] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
                         pq[q] = make_uint4(KD_NONE, KD_NONE, KD_NONE, KD_NONE);
+                    }
+                }
+                if constexpr (icond) {
+                    // records only of the seeds that attain D0 at one of the 4 vertices (a seed
+                    // that attains nowhere cannot win; the seed vertex's own record is rsu)
+                    unsigned dmin[4];
+#pragma unroll
+                    for (int h = 0; h < 4; h++) {
+                        dmin[h] = 0xFFFFu;
+#pragma unroll
+                        for (int q = 0; q < KD_SEEDS; q++) {
+                            const uint32_t d2 = (h < 2) ? dq[q].x : dq[q].y;
+                            const unsigned d = (h & 1) ? (d2 >> 16) : (d2 & 0xFFFFu);
+                            if (q < nseed) dmin[h] = min(dmin[h], min(0xFFFFu, wsu[q] + d));
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < KD_SEEDS; q++) {
+                        bool need = false;
+#pragma unroll
+                        for (int h = 0; h < 4; h++) {
+                            const uint32_t d2 = (h < 2) ? dq[q].x : dq[q].y;
+                            const unsigned d = (h & 1) ? (d2 >> 16) : (d2 & 0xFFFFu);
+                            need = need || (q < nseed && min(0xFFFFu, wsu[q] + d) == dmin[h] && v0 + h != su[q]);
+                        }
+                        if (need) pq[q] = *reinterpret_cast<const uint4*>(sprow[q] + vl);
+                        else pq[q] = make_uint4(KD_NONE, KD_NONE, KD_NONE, KD_NONE);
                     }
                 }
                 uint32_t dw[2], rw[4];
@@ -1366,6 +1529,9 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
                             h = __hip_atomic_load(&sm->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             const int t = min(__hip_atomic_load(&sm->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), rc);
                             nn = min(64, t - h);
+                            // a short queue spread over more waves (each slice pays the same
+                            // two global-load latencies, whatever its size)
+                            if (KD_SDIV > 0 && B >= 1024) nn = min(nn, max(KD_SMIN, (t - h + KD_SDIV - 1) / max(KD_SDIV, 1)));
                             if (nn > 0 && atomicCAS(&sm->head, h, h + nn) != h) nn = 0;
                             if (nn <= 0) { nn = 0; atomicSub(&sm->busy, 1); }
                         }

@@ -51,7 +51,11 @@ typedef struct pcache {
     int32_t na;
     int32_t* A;          /* sorted attached vertices */
     int32_t* cid;        /* vertex -> index in A, -1 = not attached */
-    double* lr;          /* (lat, rel) pairs: one cache line serves both getters */
+    double* lr;          /* (lat, rel) pairs: one cache line serves both getters; or, with
+                          * l16, the compact layout of shd_route.h (SHD_ROUTE_FILL_LAT16): six
+                          * pairs per 64-byte line, rel f64 x 6 then lat u16 x 6 */
+    int l16;
+    int64_t* row16;      /* l16: first line of each row (na + 1) */
     uint32_t* cnt;       /* packet counters per pair (calloc: pages commit on first touch);
                           * each 2^32 wrap adds 2^32 to the striped spill map pc */
     double min_lat;
@@ -67,6 +71,9 @@ struct shd_topology {
     shd_route_t** eng;
     int32_t n;
     int complete, directed, prefer_direct;
+    int lat16;           /* the fill may use the compact layout: every latency it stores is an
+                          * integer below 0xFFFF (engine info.lat16; direct and self paths are
+                          * edge latencies or twice one: 2 * max edge latency < 0xFFFF) */
     /* host adjacency for the prefer-direct isDirect flags */
     int32_t* arow;
     int32_t* acol;
@@ -81,11 +88,38 @@ struct shd_topology {
     shd_attach_t* at;    /* host attachment index (graphml topologies only) */
 };
 
-#define LAT(c, k) ((c)->lr[2 * (size_t)(k)])
-#define REL(c, k) ((c)->lr[2 * (size_t)(k) + 1])
-
 static inline size_t tri(int32_t na, int32_t i, int32_t j) { /* i <= j */
     return (size_t)i * (size_t)na - ((size_t)i * (size_t)(i - 1)) / 2 + (size_t)(j - i);
+}
+
+/* the stored Path of pair (i, j), i <= j: latency (NaN = never stored) and reliability,
+ * from the interleaved doubles or from the compact line layout (widened exactly) */
+static inline double lat_at(const pcache* c, int32_t i, int32_t j) {
+    if (c->l16) {
+        const int64_t e = j - i;
+        const unsigned char* line = (const unsigned char*)c->lr + 64 * (c->row16[i] + e / 6);
+        const uint16_t x = ((const uint16_t*)(line + 48))[e % 6];
+        return x == 0xFFFFu ? NAN : (double)x;
+    }
+    return c->lr[2 * tri(c->na, i, j)];
+}
+static inline double rel_at(const pcache* c, int32_t i, int32_t j) {
+    if (c->l16) {
+        const int64_t e = j - i;
+        return ((const double*)((const unsigned char*)c->lr + 64 * (c->row16[i] + e / 6)))[e % 6];
+    }
+    return c->lr[2 * tri(c->na, i, j) + 1];
+}
+static inline void set_at(pcache* c, int32_t i, int32_t j, double lat, double rel) {
+    if (c->l16) {
+        const int64_t e = j - i;
+        unsigned char* line = (unsigned char*)c->lr + 64 * (c->row16[i] + e / 6);
+        ((uint16_t*)(line + 48))[e % 6] = isnan(lat) ? (uint16_t)0xFFFFu : (uint16_t)lat;
+        ((double*)line)[e % 6] = rel;
+        return;
+    }
+    c->lr[2 * tri(c->na, i, j)] = lat;
+    c->lr[2 * tri(c->na, i, j) + 1] = rel;
 }
 
 static int cmp_i32(const void* a, const void* b) {
@@ -133,7 +167,7 @@ static uint64_t* pc_slot(pcmap* m, uint64_t key);
 static void pcache_free(pcache* c) {
     while (c) {
         pcache* o = c->older;
-        free(c->A); free(c->cid); shd_route_host_free(c->lr); free(c->cnt);
+        free(c->A); free(c->cid); shd_route_host_free(c->lr); free(c->cnt); free(c->row16);
         for (int k = 0; k < PC_STRIPES; k++) { pthread_mutex_destroy(&c->pc[k].lock); free(c->pc[k].s); }
         free(c);
         c = o;
@@ -156,6 +190,11 @@ static shd_topology_t* finish_new(shd_topology_t* t, const int* devices, int nde
     t->complete = info.is_complete;
     t->directed = info.directed;
     t->prefer_direct = info.prefer_direct;
+    double maxw = 0;
+    for (int32_t e = 0; e < t->g.n_edges; e++)
+        if (t->g.edge_latency[e] > maxw) maxw = t->g.edge_latency[e];
+    const char* e16 = getenv("SHD_TOPOLOGY_LAT16");  /* "0": keep the interleaved doubles (A/B) */
+    t->lat16 = info.lat16 && 2.0 * maxw < 65535.0 && !(e16 && atoi(e16) == 0);
     t->attached = calloc((size_t)t->n, 1);
     build_adjacency(t);
     pthread_mutex_init(&t->lock, NULL);
@@ -280,8 +319,8 @@ static void* fill_worker(void* arg) {
     fill_job* job = arg;
     pcache* c = job->c;
     double mn = INFINITY;
-    int rc = shd_route_fill_triangle(job->t->eng[job->dev], c->A, c->na, job->nd, job->dev, SHD_ROUTE_DISPATCH, c->lr,
-                                     &mn, NULL);
+    int rc = shd_route_fill_triangle(job->t->eng[job->dev], c->A, c->na, job->nd, job->dev,
+                                     SHD_ROUTE_DISPATCH | (c->l16 ? SHD_ROUTE_FILL_LAT16 : 0u), c->lr, &mn, NULL);
     /* ENOEDGE: a self pair without a self-loop; that entry stays NaN, i.e. not stored by
      * the batch, as the reference skips the failed target (topology.c:1488-1495,
      * 1812-1870); fill_locked resolves it below.  EUNREACH (not after the
@@ -343,8 +382,17 @@ static int fill_locked(shd_topology_t* t) {
         if (t->attached[v]) { c->cid[v] = c->na; c->A[c->na++] = v; }
     }
     const size_t ntri = (size_t)c->na * ((size_t)c->na + 1) / 2;
+    c->l16 = t->lat16;
+    size_t bytes = 2 * sizeof(double) * ntri;
+    if (c->l16) {
+        c->row16 = malloc(sizeof(int64_t) * ((size_t)c->na + 1));
+        if (!c->row16) { pcache_free(c); return SHD_ROUTE_ENOMEM; }
+        c->row16[0] = 0;
+        for (int32_t i = 0; i < c->na; i++) c->row16[i + 1] = c->row16[i] + (c->na - i + 5) / 6;
+        bytes = 64 * (size_t)c->row16[c->na];
+    }
     /* pinned: the device copies its rows straight into the triangle at full PCIe rate */
-    c->lr = shd_route_host_alloc(2 * sizeof(double) * (ntri ? ntri : 1));
+    c->lr = shd_route_host_alloc(bytes ? bytes : 16);
     c->cnt = calloc(ntri ? ntri : 1, sizeof(uint32_t));
     if (!c->lr || !c->cnt) { pcache_free(c); return SHD_ROUTE_ENOMEM; }
     int rc = SHD_ROUTE_OK;
@@ -374,16 +422,15 @@ static int fill_locked(shd_topology_t* t) {
         int32_t nself = 0;
         int32_t* sv = malloc(sizeof(int32_t) * ((size_t)c->na + 1));
         for (int32_t i = 0; i < c->na; i++)
-            if (isnan(LAT(c, tri(c->na, i, i)))) sv[nself++] = c->A[i];
+            if (isnan(lat_at(c, i, i))) sv[nself++] = c->A[i];
         if (nself) {
             double* sl = malloc(sizeof(double) * (size_t)nself);
             double* sr = malloc(sizeof(double) * (size_t)nself);
             rc = shd_route_self(t->eng[0], sv, nself, sl, sr);
             if (rc == SHD_ROUTE_ENOEDGE) rc = SHD_ROUTE_OK;  /* no out-edge: stays unstored */
             for (int32_t q = 0; q < nself && !rc; q++) {
-                const size_t k = tri(c->na, c->cid[sv[q]], c->cid[sv[q]]);
-                LAT(c, k) = sl[q];
-                REL(c, k) = sr[q];
+                const int32_t ii = c->cid[sv[q]];
+                set_at(c, ii, ii, sl[q], sr[q]);
                 if (!isnan(sl[q]) && sl[q] < mn_fill) mn_fill = sl[q];
             }
             free(sl); free(sr);
@@ -398,6 +445,12 @@ static int fill_locked(shd_topology_t* t) {
     t->fill_seconds += now_s() - t0;
     __atomic_store_n(&t->cache, c, __ATOMIC_RELEASE);
     return SHD_ROUTE_OK;
+}
+
+uint64_t shd_topology_triangle_bytes(shd_topology_t* t) {
+    const pcache* c = t ? __atomic_load_n(&t->cache, __ATOMIC_ACQUIRE) : NULL;
+    if (!c) return 0;
+    return c->l16 ? 64 * (uint64_t)c->row16[c->na] : 16 * ((uint64_t)c->na * ((uint64_t)c->na + 1) / 2);
 }
 
 int shd_topology_fill(shd_topology_t* t, double* elapsed_s) {
@@ -420,28 +473,33 @@ static pcache* cache_of(shd_topology_t* t) {
     return rc ? NULL : c;
 }
 
-/* _topology_getPathEntry (topology.c:1969-2051) -> index into the triangle of *cp, or -1 */
-static int64_t entry(shd_topology_t* t, int32_t s, int32_t d, pcache** cp) {
+/* _topology_getPathEntry (topology.c:1969-2051) -> index into the triangle of *cp, or -1;
+ * *ip <= *jp its attached positions */
+static int64_t entry_ij(shd_topology_t* t, int32_t s, int32_t d, pcache** cp, int32_t* ip, int32_t* jp) {
     if (!t || s < 0 || d < 0 || s >= t->n || d >= t->n) return -1;
     pcache* c = cache_of(t);
     if (!c) return -1;
-    const int32_t i = c->cid[s], j = c->cid[d];
+    int32_t i = c->cid[s], j = c->cid[d];
     if (i < 0 || j < 0) return -1;  /* address not connected to the topology */
-    const int64_t k = (int64_t)(i <= j ? tri(c->na, i, j) : tri(c->na, j, i));
-    *cp = c;
-    return isnan(LAT(c, k)) ? -1 : k;  /* never stored (topology.c:2040-2046) */
+    if (i > j) { const int32_t x = i; i = j; j = x; }
+    *cp = c; *ip = i; *jp = j;
+    return isnan(lat_at(c, i, j)) ? -1 : (int64_t)tri(c->na, i, j);  /* never stored (topology.c:2040-2046) */
+}
+static int64_t entry(shd_topology_t* t, int32_t s, int32_t d, pcache** cp) {
+    int32_t i, j;
+    return entry_ij(t, s, d, cp, &i, &j);
 }
 
 double shd_topology_get_latency(shd_topology_t* t, int32_t s, int32_t d) {
     pcache* c;
-    int64_t k = entry(t, s, d, &c);
-    return k < 0 ? -1.0 : LAT(c, k);
+    int32_t i, j;
+    return entry_ij(t, s, d, &c, &i, &j) < 0 ? -1.0 : lat_at(c, i, j);
 }
 
 double shd_topology_get_reliability(shd_topology_t* t, int32_t s, int32_t d) {
     pcache* c;
-    int64_t k = entry(t, s, d, &c);
-    return k < 0 ? -1.0 : REL(c, k);
+    int32_t i, j;
+    return entry_ij(t, s, d, &c, &i, &j) < 0 ? -1.0 : rel_at(c, i, j);
 }
 
 int shd_topology_is_routable(shd_topology_t* t, int32_t s, int32_t d) {
@@ -539,7 +597,7 @@ int shd_topology_dump_paths(shd_topology_t* t, FILE* out) {
             /* path_toString (path.c:62-74) inside _topology_logAllCachedPathsHelper2 */
             fprintf(out, "Found path %s%s%s in cache: SourceIndex=%d DestinationIndex=%d Latency=%f "
                          "Reliability=%f PacketCount=%llu isDirect=%s\n",
-                    ia, t->directed ? "->" : "<->", ib, a, b, LAT(c, k), REL(c, k), (unsigned long long)pc,
+                    ia, t->directed ? "->" : "<->", ib, a, b, lat_at(c, i, j), rel_at(c, i, j), (unsigned long long)pc,
                     (t->complete || (t->prefer_direct && adjacent(t, a, b))) ? "True" : "False");
         }
     return SHD_ROUTE_OK;

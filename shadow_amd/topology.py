@@ -26,7 +26,7 @@ EXPORTS = (
     "shd_topology_get_reliability", "shd_topology_is_routable",
     "shd_topology_increment_path_packet_counter", "shd_topology_get_path_packet_count",
     "shd_topology_is_direct_path", "shd_topology_min_path_latency", "shd_topology_runahead_ns",
-    "shd_topology_fill", "shd_topology_dump_paths",
+    "shd_topology_fill", "shd_topology_dump_paths", "shd_topology_triangle_bytes",
     "shd_attach_create", "shd_attach_find_vertex", "shd_attach_destroy", "shd_topology_attach",
 )
 
@@ -85,6 +85,8 @@ def load_library():
     L.shd_topology_runahead_ns.argtypes = [P]
     L.shd_topology_fill.restype = C.c_int
     L.shd_topology_fill.argtypes = [P, C.POINTER(D)]
+    L.shd_topology_triangle_bytes.restype = C.c_uint64
+    L.shd_topology_triangle_bytes.argtypes = [P]
     L.shd_topology_dump_paths.restype = C.c_int
     L.shd_topology_dump_paths.argtypes = [P, P]
     S = C.c_char_p
@@ -251,6 +253,10 @@ class Topology:
         if rc:
             raise RuntimeError(f"fill failed ({rc})")
         return t.value
+
+    def triangle_bytes(self) -> int:
+        """Host bytes of the filled triangle (16 per pair, or the compact u16 layout)."""
+        return int(load_library().shd_topology_triangle_bytes(self._h))
 
     def get_latency(self, s, d) -> float:
         return load_library().shd_topology_get_latency(self._h, int(s), int(d))

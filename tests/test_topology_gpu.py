@@ -273,3 +273,45 @@ def test_topology_attach_hosts(topo, tmp_path):
             assert t.get_latency(a, b) == ring(a, b) and t.get_reliability(a, b) == 1.0
     assert t.min_path_latency() == min(ring(a, b) for a in A for b in A)
     idx.close()
+
+
+@pytest.mark.parametrize("name", ["ba60", "ba80_prefer", "k24", "ba100_attached", "dir40", "ba120_vloss"])
+def test_compact_triangle_equals_interleaved(topo, monkeypatch, name):
+    """The compact fill layout (SHD_ROUTE_FILL_LAT16: six pairs per 64-byte line, u16
+    latency widened exactly) against the interleaved doubles: every getter on every pair,
+    the dump, the minimum and the self pairs agree bit for bit; single and sharded fills."""
+    g, z, p = _small(name)
+    A = z[p + "attached"]
+    tabs = []
+    for mode, devs in (("0", (0,)), ("1", (0,)), ("1", (0, 0, 0))):
+        monkeypatch.setenv("SHD_TOPOLOGY_LAT16", mode)
+        t = topo.Topology.from_graph(g, devices=devs)
+        t.attach_all(A)
+        lat, rel = t.table(A)
+        cnt = [t.is_routable(int(a), int(b)) for a in A for b in A]
+        tabs.append((lat, rel, t.min_path_latency(), cnt))
+    for lat, rel, mn, cnt in tabs[1:]:
+        assert np.array_equal(lat, tabs[0][0], equal_nan=True)
+        assert np.array_equal(rel, tabs[0][1], equal_nan=True)
+        assert mn == tabs[0][2] and cnt == tabs[0][3]
+    assert np.array_equal(tabs[0][0], z[p + "lat"])
+
+
+def test_compact_triangle_c3_sharded(topo, monkeypatch):
+    """C3 (9,337 attached) filled in the compact layout over two contexts (rows out of
+    triangle order, each row's lines disjoint) against the interleaved fill, on the
+    golden-sampled rows through the getters."""
+    g = config("c3")
+    T = g.targets()
+    dig = json.load(open(os.path.join(GOLD, "rows_digests.json")))["c3"]
+    S = [r["src"] for r in dig["rows"][::6]]
+    out = []
+    for mode, devs in (("0", (0,)), ("1", (0, 0))):
+        monkeypatch.setenv("SHD_TOPOLOGY_LAT16", mode)
+        t = topo.Topology.from_graph(g, devices=devs)
+        t.attach_all(T)
+        t.fill()
+        out.append((np.array([[t.get_latency(s, int(d)) for d in T] for s in S]),
+                    np.array([[t.get_reliability(s, int(d)) for d in T] for s in S]), t.min_path_latency()))
+        t.close()
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1]) and out[0][2] == out[1][2]

@@ -94,11 +94,13 @@ def main():
         wall = time.perf_counter() - t0
         na = len(T)
         pairs = na * (na + 1) // 2
-        tri_bytes = 16 * pairs
+        tri_bytes = t.triangle_bytes()
         lat = t.get_latency(int(T[0]), int(T[-1]))
         rec = {"config": cfg, "n": g.n, "attached": na, "contexts": len(devs), "new_s": round(t_new, 3),
                "attach_s": round(t_att, 3), "fill_s": round(sec, 4), "fill_wall_s": round(wall, 4),
                "triangle_pairs": pairs, "triangle_bytes": tri_bytes,
+               "layout": "compact u16 lat + f64 rel, 6 pairs per 64-B line" if tri_bytes < 16 * pairs
+                         else "interleaved f64 (lat, rel)", "bytes_per_pair": round(tri_bytes / pairs, 3),
                "host_write_GBps": round(tri_bytes / sec / 1e9, 2), "pairs_per_s": round(pairs / sec),
                "peak_rss_gb_before_fill": round(rss0, 2), "peak_rss_gb": round(rss_gb(), 2),
                "min_path_latency": t.min_path_latency(), "probe_latency": lat}

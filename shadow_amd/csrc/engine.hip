@@ -135,6 +135,7 @@ struct shd_route {
     int vf_lossy = 0;  // some vertex factor is not exactly 1.0 (else every present f_v is a no-op)
     int kd_rone = -1;  // rtab index of exactly 1.0 (-1: none)
     char* d_kd_ws = nullptr;
+    int* d_fwflag = nullptr;  // K4: per pivot, its closed tile is published (fw_restp_kernel)
     unsigned long long* d_kd_stats = nullptr;  // KD liveness counters (shd_route_kd_stats)
     int* d_kd_next = nullptr;  // KD source queue counter
     // host copies for seeded planning (shd_route_plan_*): out-CSR, rtab index per arc and
@@ -2221,9 +2222,26 @@ int shd_route_fw_table_async(shd_route_t* c, void* stream) {
     const int np = c->fw_np, nb = np / FW_T;
     const unsigned blocks = (unsigned)(((size_t)np * np + 255) / 256);
     hipLaunchKernelGGL(fw_init_kernel, dim3(blocks), dim3(256), 0, st, c->d_W, c->n, np, c->d_fwD);
-    // rest kernel: 64 x 64 tiles with 4 x 4 register blocks (default); SHD_ROUTE_FWREST=2 selects
-    // the 128 x 128-region kernel with 8 x 8 blocks (C5 FW table 3.28 ms against 3.06, rocprof A/B)
-    static const int rest1 = !(getenv("SHD_ROUTE_FWREST") && atoi(getenv("SHD_ROUTE_FWREST")) == 2);
+    // rest kernel: 64 x 64 tiles with 4 x 4 register blocks and the next pivot's panels fused in
+    // (default: one launch per pivot); SHD_ROUTE_FWREST=1 the separate panel + rest launches,
+    // 2 the 128 x 128-region rest kernel with 8 x 8 blocks (C5 FW table 3.28 ms against 3.06)
+    const char* fwr = getenv("SHD_ROUTE_FWREST");
+    const int mode = fwr ? atoi(fwr) : 0;
+    if (mode == 0 && nb > 1) {
+        if (!c->d_fwflag) {
+            if (hipMalloc((void**)&c->d_fwflag, sizeof(int) * (size_t)(nb + 1)) != hipSuccess) return SHD_ROUTE_ENOMEM;
+            c->allocs.push_back(c->d_fwflag);
+        }
+        if (hipMemsetAsync(c->d_fwflag, 0, sizeof(int) * (size_t)(nb + 1), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
+        hipLaunchKernelGGL(fw_diag_kernel<FW_T>, dim3(1), dim3(256), 0, st, c->d_fwD, np, 0);
+        hipLaunchKernelGGL(fw_panel_kernel<FW_T>, dim3(nb - 1, 2), dim3(256), 0, st, c->d_fwD, np, 0);
+        for (int kb = 0; kb < nb; kb++)
+            hipLaunchKernelGGL(fw_restp_kernel<FW_T>, dim3((nb - 1) * (nb - 1)), dim3(256), 0, st, c->d_fwD, np, kb,
+                               c->d_fwflag);
+        c->fw_ready = 1;
+        return hip_check(hipGetLastError());
+    }
+    const bool rest1 = mode != 2;
     const int nr = (nb + 1) / 2;
     for (int kb = 0; kb < nb; kb++) {
         // pivot tiles after the first are closed inside the previous fw_rest launch

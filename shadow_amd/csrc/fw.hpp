@@ -261,6 +261,98 @@ __global__ __launch_bounds__(256) void fw_rest_kernel(uint16_t* __restrict__ D, 
     fw_store_block<T>(D, np, ti, tj, r, c, acc);
 }
 
+// fw_rest with the next pivot's panels fused in (one launch per pivot instead of a panel and
+// a rest launch).  1-D grid of (nb - 1)^2 workgroups: workgroup 0 takes the next pivot tile
+// (pn, pn) = (kb + 1, kb + 1), applies pivot kb, closes it and publishes it (stores drained,
+// agent release, flag[pn]); the next (nb - 2)^2 take the tiles outside rows and columns kb, pn;
+// the last 2 (nb - 2) take row pn and column pn: pivot kb's update, then -- once flag[pn] is
+// up (agent acquire) -- the panel product with the closed pivot (row: C = D* (x) C, column:
+// C = C (x) D*), exactly fw_panel_kernel's work for pivot pn.  They are dispatched last, so
+// the pivot's closing workgroup (dispatched first) has long finished when they wait.  The
+// last pivot (pn = nb) has no next pivot: plain rest tiles only.
+template <int T>
+__global__ __launch_bounds__(256) void fw_restp_kernel(uint16_t* __restrict__ D, int np, int kb, int* __restrict__ flag) {
+    constexpr int R = T / 16, H = R / 2;
+    __shared__ __attribute__((aligned(16))) uint16_t At[T * T];
+    __shared__ __attribute__((aligned(16))) uint16_t Bt[T * T];
+    const int nb = np / T, pn = kb + 1;
+    const int w = blockIdx.x;
+    int ti, tj, role = 0;  // 0 plain, 1 the next pivot, 2 row panel pn, 3 column panel pn
+    auto skip = [&](int a, int x0, int x1) {  // a-th index of [0, nb) without x0 < x1
+        if (a >= x0) a++;
+        if (a >= x1) a++;
+        return a;
+    };
+    if (pn < nb) {
+        const int m = nb - 2;
+        if (w == 0) { ti = tj = pn; role = 1; }
+        else if (w - 1 < m * m) { ti = skip((w - 1) / max(m, 1), kb, pn); tj = skip((w - 1) % max(m, 1), kb, pn); }
+        else if (w - 1 - m * m < m) { ti = pn; tj = skip(w - 1 - m * m, kb, pn); role = 2; }
+        else { ti = skip(w - 1 - m * m - m, kb, pn); tj = pn; role = 3; }
+    } else {
+        const int m = nb - 1;
+        ti = w / m; tj = w % m;
+        if (ti >= kb) ti++;
+        if (tj >= kb) tj++;
+    }
+    if (ti >= nb || tj >= nb) return;
+    const int tid = threadIdx.x, r = tid / 16, c = tid % 16;
+    uint32_t acc[R][H];
+    fw_load_block<T>(D, np, ti, tj, r, c, acc);
+    fw_stage<T>(D, np, ti, kb, At, true);
+    fw_stage<T>(D, np, kb, tj, Bt, false);
+    __syncthreads();
+    fw_tile_product<T>(At, Bt, acc, r, c);
+    if (role == 1) {
+        __syncthreads();  // every thread's product is done with At
+#pragma unroll
+        for (int i = 0; i < R; i++) fw_st<H>(At + (R * r + i) * T + R * c, acc[i]);
+        __syncthreads();
+        fw_close<T>(At, acc, r, c);
+        fw_store_block<T>(D, np, ti, tj, r, c, acc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores drained
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&flag[pn], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    if (role >= 2) {
+        // the closed pivot pn: one relaxed poll loop, one agent acquire, then plain loads
+        if (tid == 0) {
+            int spin = 0;
+            while (__hip_atomic_load(&flag[pn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && spin < (1 << 24)) {
+                __builtin_amdgcn_s_sleep(2);
+                spin++;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // (also: every thread's product is done with At / Bt)
+        if (role == 2) {
+            // row panel: C = D* (x) C -- A = D* transposed, B = C as it now stands
+            fw_stage<T>(D, np, pn, pn, At, true);
+#pragma unroll
+            for (int i = 0; i < R; i++) fw_st<H>(Bt + (R * r + i) * T + R * c, acc[i]);
+        } else {
+            // column panel: C = C (x) D* -- A = C transposed, B = D*
+#pragma unroll
+            for (int i = 0; i < R; i++)
+#pragma unroll
+                for (int h = 0; h < H; h++) {
+                    At[(R * c + 2 * h) * T + R * r + i] = (uint16_t)(acc[i][h] & 0xFFFFu);
+                    At[(R * c + 2 * h + 1) * T + R * r + i] = (uint16_t)(acc[i][h] >> 16);
+                }
+            fw_stage<T>(D, np, pn, pn, Bt, false);
+        }
+        __syncthreads();
+        fw_tile_product<T>(At, Bt, acc, r, c);
+    }
+    fw_store_block<T>(D, np, ti, tj, r, c, acc);
+}
+
 // The rest update of pivot kb over 128 x 128 regions (2 x 2 tiles of 64) with 8 x 8
 // register blocks: 256 threads as 16 x 16, thread (r, c) holds rows 8r.. and columns 8c..
 // of the region.  Per k step one 16-byte LDS read of the column panel (transposed: the

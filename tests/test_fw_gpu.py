@@ -202,3 +202,29 @@ def test_c5_direct_table_full(oracle_mod):
     assert np.array_equal(rel.cpu().numpy(), tab["rel"])
     assert np.array_equal(mn.cpu().numpy(), tab["lat"].min(axis=1))
     assert float(out.item()) == tab["min_latency"]
+
+
+@pytest.mark.parametrize("cfg", ["ba700", "c5"])
+def test_fw_fused_panels_equal_separate_launches(monkeypatch, cfg):
+    """The default K4 sequence (each rest launch also closes the next pivot and computes its
+    panels, fw_restp_kernel) against the separate panel + rest launches
+    (SHD_ROUTE_FWREST=1): every SOURCE row of every source bit-identical."""
+    import torch
+    from shadow_amd import route
+    g = internet_like(700, 2, seed=23) if cfg == "ba700" else config("c5")
+    T = np.arange(g.n, dtype=np.int32)
+    dev = torch.device("cuda", 0)
+    d_T = torch.from_numpy(T).to(dev)
+    out = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("SHD_ROUTE_FWREST", mode)
+        eng = route.RouteEngine(g)
+        lat = torch.empty((g.n, g.n), dtype=torch.float64, device=dev)
+        rel = torch.empty_like(lat)
+        mn = torch.empty(g.n, dtype=torch.float64, device=dev)
+        for _ in range(2):  # (a second table on the same context: flags re-armed)
+            eng.fw_table_async()
+            eng.fw_rows_async(d_T, d_T, lat, rel, mn)
+        eng.sync()
+        out.append((lat, rel, mn))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][2], out[1][2])

@@ -2236,8 +2236,8 @@ int shd_route_fw_table_async(shd_route_t* c, void* stream) {
         hipLaunchKernelGGL(fw_diag_kernel<FW_T>, dim3(1), dim3(256), 0, st, c->d_fwD, np, 0);
         hipLaunchKernelGGL(fw_panel_kernel<FW_T>, dim3(nb - 1, 2), dim3(256), 0, st, c->d_fwD, np, 0);
         for (int kb = 0; kb < nb; kb++)
-            hipLaunchKernelGGL(fw_restp_kernel<FW_T>, dim3((nb - 1) * (nb - 1)), dim3(256), 0, st, c->d_fwD, np, kb,
-                               c->d_fwflag);
+            hipLaunchKernelGGL(fw_restp_kernel<FW_T>, dim3((nb - 1) * (nb - 1) + (kb + 1 < nb ? 2 : 0)), dim3(256), 0,
+                               st, c->d_fwD, np, kb, c->d_fwflag);
         c->fw_ready = 1;
         return hip_check(hipGetLastError());
     }

@@ -265,11 +265,13 @@ __global__ __launch_bounds__(256) void fw_rest_kernel(uint16_t* __restrict__ D, 
 // a rest launch).  1-D grid of (nb - 1)^2 workgroups: workgroup 0 takes the next pivot tile
 // (pn, pn) = (kb + 1, kb + 1), applies pivot kb, closes it and publishes it (stores drained,
 // agent release, flag[pn]); the next (nb - 2)^2 take the tiles outside rows and columns kb, pn;
-// the last 2 (nb - 2) take row pn and column pn: pivot kb's update, then -- once flag[pn] is
+// the next 2 (nb - 2) take row pn and column pn: pivot kb's update, then -- once flag[pn] is
 // up (agent acquire) -- the panel product with the closed pivot (row: C = D* (x) C, column:
-// C = C (x) D*), exactly fw_panel_kernel's work for pivot pn.  They are dispatched last, so
-// the pivot's closing workgroup (dispatched first) has long finished when they wait.  The
-// last pivot (pn = nb) has no next pivot: plain rest tiles only.
+// C = C (x) D*), exactly fw_panel_kernel's work for pivot pn; the last two take tiles
+// (pn, kb) and (kb, pn), pivot kb's own panels, which pivot kb leaves as they are: the panel
+// product only.  These are dispatched last, so the pivot's closing workgroup (dispatched
+// first) has long finished when they wait.  The last pivot (pn = nb) has no next pivot:
+// (nb - 1)^2 plain rest tiles only.
 template <int T>
 __global__ __launch_bounds__(256) void fw_restp_kernel(uint16_t* __restrict__ D, int np, int kb, int* __restrict__ flag) {
     constexpr int R = T / 16, H = R / 2;
@@ -288,7 +290,9 @@ __global__ __launch_bounds__(256) void fw_restp_kernel(uint16_t* __restrict__ D,
         if (w == 0) { ti = tj = pn; role = 1; }
         else if (w - 1 < m * m) { ti = skip((w - 1) / max(m, 1), kb, pn); tj = skip((w - 1) % max(m, 1), kb, pn); }
         else if (w - 1 - m * m < m) { ti = pn; tj = skip(w - 1 - m * m, kb, pn); role = 2; }
-        else { ti = skip(w - 1 - m * m - m, kb, pn); tj = pn; role = 3; }
+        else if (w - 1 - m * m < 2 * m) { ti = skip(w - 1 - m * m - m, kb, pn); tj = pn; role = 3; }
+        else if (w - 1 - m * m == 2 * m) { ti = pn; tj = kb; role = 4; }  // row panel, no rest product
+        else { ti = kb; tj = pn; role = 5; }                              // column panel, no rest product
     } else {
         const int m = nb - 1;
         ti = w / m; tj = w % m;
@@ -299,10 +303,14 @@ __global__ __launch_bounds__(256) void fw_restp_kernel(uint16_t* __restrict__ D,
     const int tid = threadIdx.x, r = tid / 16, c = tid % 16;
     uint32_t acc[R][H];
     fw_load_block<T>(D, np, ti, tj, r, c, acc);
-    fw_stage<T>(D, np, ti, kb, At, true);
-    fw_stage<T>(D, np, kb, tj, Bt, false);
-    __syncthreads();
-    fw_tile_product<T>(At, Bt, acc, r, c);
+    if (role < 4) {
+        fw_stage<T>(D, np, ti, kb, At, true);
+        fw_stage<T>(D, np, kb, tj, Bt, false);
+        __syncthreads();
+        fw_tile_product<T>(At, Bt, acc, r, c);
+    } else {
+        role -= 2;  // the panel product alone
+    }
     if (role == 1) {
         __syncthreads();  // every thread's product is done with At
 #pragma unroll

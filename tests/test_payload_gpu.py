@@ -12,10 +12,13 @@ pytestmark = pytest.mark.gpu
 
 
 def _with_self_loops(g: Graph, w):
+    """g with every self-loop replaced by one of latency w (a second loop would make it a
+    multigraph)."""
     v = np.arange(g.n, dtype=np.int32)
-    return Graph(n=g.n, src=np.concatenate([g.src, v]), dst=np.concatenate([g.dst, v]),
-                 latency=np.concatenate([g.latency, np.full(g.n, float(w))]),
-                 packetloss=np.concatenate([g.packetloss, np.full(g.n, 0.01)]), name=g.name + "_loops")
+    keep = g.src != g.dst
+    return Graph(n=g.n, src=np.concatenate([g.src[keep], v]), dst=np.concatenate([g.dst[keep], v]),
+                 latency=np.concatenate([g.latency[keep], np.full(g.n, float(w))]),
+                 packetloss=np.concatenate([g.packetloss[keep], np.full(g.n, 0.01)]), name=g.name + "_loops")
 
 
 def _payload(eng, g, lat16):

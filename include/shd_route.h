@@ -238,12 +238,12 @@ int shd_route_tri_payload_async(shd_route_t* ctx, const double* d_lat, const dou
 
 void* shd_route_host_alloc(size_t bytes);  /* pinned host memory (NULL on failure) */
 
-/* KD liveness counters since the last reset (no reference equivalent): s_sleep rounds the
- * delta-stepping kernel's waves spent waiting on each other -- out[0] compute waves waiting
- * for space in the parent-record ring, out[1] the writer wave on a reserved record not yet
- * written, out[2] a wave on a work-queue entry not yet written; out[3] 0.  A stall (both
- * sides of the ring spinning to their caps) shows as millions; a healthy C3 table is a few
- * thousand at most.  Synchronises the device; reset != 0 zeroes the counters. */
+/* KD liveness counters since the last reset (no reference equivalent): the longest single
+ * wait, in s_sleep rounds, of the delta-stepping kernel's waves on each other -- out[0] a
+ * compute wave for space in the parent-record ring, out[1] the writer wave on a reserved
+ * record not yet written, out[2] a wave on a work-queue entry not yet written; out[3] 0.  A
+ * stall (both sides of the ring spinning to their caps) shows as 2^22; healthy waits are
+ * hundreds.  Synchronises the device; reset != 0 zeroes the counters. */
 int shd_route_kd_stats(shd_route_t* ctx, uint64_t* out, int32_t reset);
 void shd_route_host_free(void* p);
 

@@ -143,8 +143,8 @@ struct DevDelta {
                                         // absent, a no-op in every product: vf is not read)
     int dflags;                         // diagnostic builds: 1 = skip the output-row stores
     unsigned long long* dbg;            // SHD_STAMPS builds: KD_NACC words per source
-    unsigned long long* stats;          // liveness counters (s_sleep rounds): [0] compute waves waiting
-                                        // for writer-ring space, [1] the writer on a reserved record
+    unsigned long long* stats;          // liveness: the longest single wait (s_sleep rounds) of [0] a compute
+                                        // wave for writer-ring space, [1] the writer on a reserved record
                                         // not yet written, [2] a slice on a queue entry not yet written
 };
 
@@ -1508,7 +1508,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
                                && w8 < (1 << 22); w8++)
                             __builtin_amdgcn_s_sleep(1);
                         if (w8 >= (1 << 22)) raise_err(err, SHD_ROUTE_EDEVICE);
-                        if (w8 && g.stats) atomicAdd(&g.stats[0], (unsigned long long)w8);
+                        if (w8 && g.stats) atomicMax(&g.stats[0], (unsigned long long)w8);
                     }
                     rb = __builtin_amdgcn_readfirstlane(rb);
                     if (mine) {
@@ -1565,7 +1565,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
                         int w8 = 0;
                         for (; x == 0xFFFFu && w8 < (1 << 22); w8++) { __builtin_amdgcn_s_sleep(1); x = *slot; }
                         if (x == 0xFFFFu) raise_err(err, SHD_ROUTE_EDEVICE);
-                        if (w8 && g.stats) atomicAdd(&g.stats[2], (unsigned long long)w8);
+                        if (w8 && g.stats) atomicMax(&g.stats[2], (unsigned long long)w8);
                         u = x == 0xFFFFu ? s : (int)x;
                     }
                     const unsigned du0 = act ? ld16(dist, u) : 0u;
@@ -1785,7 +1785,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
                                     rv = *sp;
                                 }
                                 if (w8 >= (1 << 22)) raise_err(err, SHD_ROUTE_EDEVICE);
-                                if (w8 && g.stats) atomicAdd(&g.stats[1], (unsigned long long)w8);
+                                if (w8 && g.stats) atomicMax(&g.stats[1], (unsigned long long)w8);
                                 const uint32_t x = (uint32_t)rv, y = (uint32_t)(rv >> 32);
                                 *sp = 0xFFFFFFFF00000000ull;
                                 const int u = (int)(y & 0xFFFFu);

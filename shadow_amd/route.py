@@ -263,7 +263,7 @@ class RouteEngine:
             "shd_route_tri_payload_async")
 
     def kd_stats(self, reset: bool = True):
-        """shd_route_kd_stats: KD wait counters (s_sleep rounds) since the last reset:
+        """shd_route_kd_stats: the longest KD waits (s_sleep rounds) since the last reset:
         ring space, writer on an unwritten record, slice on an unwritten queue entry."""
         out = np.zeros(4, np.uint64)
         _check(load_library().shd_route_kd_stats(self._h, _p(out), int(reset)), "shd_route_kd_stats")

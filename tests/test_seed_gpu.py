@@ -266,11 +266,10 @@ def test_c3_writer_ring_no_stall(monkeypatch):
     for _ in range(6):
         plan.rows_async(d_tgt, d_lat, d_rel, d_min, dispatch=False)
         eng.sync()
-    # the kernel's own wait counters (s_sleep rounds), box-independent: a stall spins both
-    # sides of the ring to their 2^22 caps (~110 ms each); six healthy launches of the
-    # whole table wait a few thousand rounds in all
+    # the kernel's own longest waits (s_sleep rounds), box-independent: a stall spins both
+    # sides of the ring to their 2^22 caps (~110 ms each); a healthy wait is hundreds
     ring, writer, slot = eng.kd_stats(reset=True)
-    assert ring < 200_000 and writer < 200_000 and slot < 200_000, (ring, writer, slot)
+    assert max(ring, writer, slot) < 1 << 16, (ring, writer, slot)
     row_of = {int(v): i for i, v in enumerate(T)}
     idx = torch.tensor([row_of[r["src"]] for r in dig["rows"]], device=dev)
     lat, rel = d_lat[idx].cpu().numpy(), d_rel[idx].cpu().numpy()

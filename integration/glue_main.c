@@ -13,6 +13,7 @@
 #include "topology.h"
 
 static gdouble g_runahead = -1;
+gint topology_testVertexOf(Topology* top, Address* a);  /* test hook in topology.c */
 void worker_updateMinTimeJump(gdouble minPathLatency) { g_runahead = minPathLatency; }
 
 static double now_s(void) {
@@ -41,6 +42,10 @@ int main(int argc, char** argv) {
     long routable = 0;
     t0 = now_s();
     guint seed2 = 7;
+    /* SHD_GLUE_TRACE=<file>: the first SHD_GLUE_TRACE_N (1000) routable packets as
+     * "src_vertex dst_vertex latency reliability" lines, exact (%.17g) */
+    FILE* trace = getenv("SHD_GLUE_TRACE") ? fopen(getenv("SHD_GLUE_TRACE"), "w") : NULL;
+    const long trace_n = getenv("SHD_GLUE_TRACE_N") ? atol(getenv("SHD_GLUE_TRACE_N")) : 1000;
     for (long k = 0; k < P; k++) {
         Address* s = &a[rand_r(&seed2) % H];
         Address* d = &a[rand_r(&seed2) % H];
@@ -48,6 +53,8 @@ int main(int argc, char** argv) {
         const gdouble L = topology_getLatency(top, s, d);       /* worker.c:275 */
         const gdouble R = topology_getReliability(top, s, d);   /* worker.c:279 */
         topology_incrementPathPacketCounter(top, s, d);
+        if (trace && routable < trace_n)
+            fprintf(trace, "%d %d %.17g %.17g\n", topology_testVertexOf(top, s), topology_testVertexOf(top, d), L, R);
         routable++;
         lat_sum += L;
         if (L < lat_min) lat_min = L;
@@ -55,6 +62,7 @@ int main(int argc, char** argv) {
         if (R > rel_max) rel_max = R;
     }
     const double t_packets = now_s() - t0;
+    if (trace) fclose(trace);
     /* host.c:243: a detached address has no vertex any more -> -1 (topology.c:1973-1985) */
     topology_detach(top, &a[0]);
     const gdouble after = topology_getLatency(top, &a[0], &a[H > 1 ? 1 : 0]);

@@ -80,6 +80,9 @@ static gint _vertex(Topology* top, Address* a) {
     return found ? GPOINTER_TO_INT(p) : -1;
 }
 
+/* test hook (not part of topology.h): the vertex an address is attached to, -1 if none */
+gint topology_testVertexOf(Topology* top, Address* a) { return _vertex(top, a); }
+
 /* The reference reports a new minimum from _topology_storePathInCache on every decrease
  * (topology.c:1383-1385); the eager fill knows the true minimum at the first lookup, so
  * the glue reports it once, from the first looking-up worker thread */

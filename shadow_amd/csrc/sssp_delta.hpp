@@ -1322,10 +1322,29 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
             // A's records overwrite the vertices that do improve.
             // 4 vertices per lane: 8-B distance and 16-B parent-record loads of every seed
             constexpr bool icond = KD_ICOND != 0;
+            // (KD_ICOND 2: the next trip's distances are loaded before this trip's records, so
+            // the records' extra dependent step does not add a round trip per trip)
+            constexpr bool ipipe = KD_ICOND == 2;
+            uint2 dqn[KD_SEEDS];
+            if constexpr (ipipe) {
+#pragma unroll
+                for (int q = 0; q < KD_SEEDS; q++)
+                    dqn[q] = q < nseed ? *reinterpret_cast<const uint2*>(sdrow[q] + min(4 * tid, n & ~3))
+                                       : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+            }
             for (int v0 = 4 * tid; v0 <= n; v0 += 4 * B) {
                 const int vl = min(v0, n & ~3);
                 uint2 dq[KD_SEEDS];
                 uint4 pq[KD_SEEDS];
+                if constexpr (ipipe) {
+#pragma unroll
+                    for (int q = 0; q < KD_SEEDS; q++) {
+                        dq[q] = dqn[q];
+                        pq[q] = make_uint4(KD_NONE, KD_NONE, KD_NONE, KD_NONE);
+                        const int vn = min(v0 + 4 * B, n & ~3);
+                        if (q < nseed) dqn[q] = *reinterpret_cast<const uint2*>(sdrow[q] + vn);
+                    }
+                } else {
 #pragma unroll
                 for (int q = 0; q < KD_SEEDS; q++) {
                     if (q < nseed) {
@@ -1335,6 +1354,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
                         dq[q] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
                         pq[q] = make_uint4(KD_NONE, KD_NONE, KD_NONE, KD_NONE);
                     }
+                }
                 }
                 if constexpr (icond) {
                     // records only of the seeds that attain D0 at one of the 4 vertices (a seed

@@ -2227,7 +2227,7 @@ int shd_route_fw_table_async(shd_route_t* c, void* stream) {
     // 2 the 128 x 128-region rest kernel with 8 x 8 blocks (C5 FW table 3.28 ms against 3.06)
     const char* fwr = getenv("SHD_ROUTE_FWREST");
     const int mode = fwr ? atoi(fwr) : 0;
-    if (mode == 0 && nb > 1) {
+    if ((mode == 0 || mode == 3) && nb > 1) {
         if (!c->d_fwflag) {
             if (hipMalloc((void**)&c->d_fwflag, sizeof(int) * (size_t)(nb + 1)) != hipSuccess) return SHD_ROUTE_ENOMEM;
             c->allocs.push_back(c->d_fwflag);
@@ -2235,9 +2235,19 @@ int shd_route_fw_table_async(shd_route_t* c, void* stream) {
         if (hipMemsetAsync(c->d_fwflag, 0, sizeof(int) * (size_t)(nb + 1), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
         hipLaunchKernelGGL(fw_diag_kernel<FW_T>, dim3(1), dim3(256), 0, st, c->d_fwD, np, 0);
         hipLaunchKernelGGL(fw_panel_kernel<FW_T>, dim3(nb - 1, 2), dim3(256), 0, st, c->d_fwD, np, 0);
-        for (int kb = 0; kb < nb; kb++)
-            hipLaunchKernelGGL(fw_restp_kernel<FW_T>, dim3((nb - 1) * (nb - 1) + (kb + 1 < nb ? 2 : 0)), dim3(256), 0,
-                               st, c->d_fwD, np, kb, c->d_fwflag);
+        int P = 1024;  // mode 3: persistent plain-tile workgroups
+        if (const char* e = getenv("SHD_ROUTE_FWP")) P = std::max(1, atoi(e));
+        for (int kb = 0; kb < nb; kb++) {
+            const int nx = kb + 1 < nb ? 2 : 0;  // the next pivot's panel tiles in row / column kb
+            if (mode == 0) {
+                hipLaunchKernelGGL(fw_restp_kernel<FW_T>, dim3((nb - 1) * (nb - 1) + nx), dim3(256), 0, st, c->d_fwD, np,
+                                   kb, c->d_fwflag);
+            } else {
+                const int m = kb + 1 < nb ? nb - 2 : nb - 1, pp = std::max(1, std::min(P, m * m));
+                const int grid = kb + 1 < nb ? 1 + pp + 2 * m + 2 : pp;
+                hipLaunchKernelGGL(fw_restpp_kernel<FW_T>, dim3(grid), dim3(256), 0, st, c->d_fwD, np, kb, c->d_fwflag, pp);
+            }
+        }
         c->fw_ready = 1;
         return hip_check(hipGetLastError());
     }

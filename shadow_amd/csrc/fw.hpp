@@ -272,34 +272,13 @@ __global__ __launch_bounds__(256) void fw_rest_kernel(uint16_t* __restrict__ D, 
 // product only.  These are dispatched last, so the pivot's closing workgroup (dispatched
 // first) has long finished when they wait.  The last pivot (pn = nb) has no next pivot:
 // (nb - 1)^2 plain rest tiles only.
+// one tile of fw_restp: role 0 plain, 1 the next pivot, 2 / 3 row / column panel of pn
+// after pivot kb's update, 4 / 5 the same without it (tiles of pivot kb's own panels)
 template <int T>
-__global__ __launch_bounds__(256) void fw_restp_kernel(uint16_t* __restrict__ D, int np, int kb, int* __restrict__ flag) {
+__device__ inline void fw_restp_tile(uint16_t* __restrict__ D, int np, int kb, int* __restrict__ flag, int ti, int tj,
+                                     int role, uint16_t* At, uint16_t* Bt) {
     constexpr int R = T / 16, H = R / 2;
-    __shared__ __attribute__((aligned(16))) uint16_t At[T * T];
-    __shared__ __attribute__((aligned(16))) uint16_t Bt[T * T];
-    const int nb = np / T, pn = kb + 1;
-    const int w = blockIdx.x;
-    int ti, tj, role = 0;  // 0 plain, 1 the next pivot, 2 row panel pn, 3 column panel pn
-    auto skip = [&](int a, int x0, int x1) {  // a-th index of [0, nb) without x0 < x1
-        if (a >= x0) a++;
-        if (a >= x1) a++;
-        return a;
-    };
-    if (pn < nb) {
-        const int m = nb - 2;
-        if (w == 0) { ti = tj = pn; role = 1; }
-        else if (w - 1 < m * m) { ti = skip((w - 1) / max(m, 1), kb, pn); tj = skip((w - 1) % max(m, 1), kb, pn); }
-        else if (w - 1 - m * m < m) { ti = pn; tj = skip(w - 1 - m * m, kb, pn); role = 2; }
-        else if (w - 1 - m * m < 2 * m) { ti = skip(w - 1 - m * m - m, kb, pn); tj = pn; role = 3; }
-        else if (w - 1 - m * m == 2 * m) { ti = pn; tj = kb; role = 4; }  // row panel, no rest product
-        else { ti = kb; tj = pn; role = 5; }                              // column panel, no rest product
-    } else {
-        const int m = nb - 1;
-        ti = w / m; tj = w % m;
-        if (ti >= kb) ti++;
-        if (tj >= kb) tj++;
-    }
-    if (ti >= nb || tj >= nb) return;
+    const int pn = kb + 1;
     const int tid = threadIdx.x, r = tid / 16, c = tid % 16;
     uint32_t acc[R][H];
     fw_load_block<T>(D, np, ti, tj, r, c, acc);
@@ -359,6 +338,117 @@ __global__ __launch_bounds__(256) void fw_restp_kernel(uint16_t* __restrict__ D,
         fw_tile_product<T>(At, Bt, acc, r, c);
     }
     fw_store_block<T>(D, np, ti, tj, r, c, acc);
+}
+
+// tile w of a pivot's fw_restp grid ((nb - 1)^2 + 2 when a next pivot exists): role and
+// coordinates (see fw_restp_kernel)
+__device__ inline void fw_restp_map(int w, int nb, int kb, int& ti, int& tj, int& role) {
+    const int pn = kb + 1;
+    auto skip = [&](int a, int x0, int x1) {  // a-th index of [0, nb) without x0 < x1
+        if (a >= x0) a++;
+        if (a >= x1) a++;
+        return a;
+    };
+    role = 0;
+    if (pn < nb) {
+        const int m = nb - 2;
+        if (w == 0) { ti = tj = pn; role = 1; }
+        else if (w - 1 < m * m) { ti = skip((w - 1) / max(m, 1), kb, pn); tj = skip((w - 1) % max(m, 1), kb, pn); }
+        else if (w - 1 - m * m < m) { ti = pn; tj = skip(w - 1 - m * m, kb, pn); role = 2; }
+        else if (w - 1 - m * m < 2 * m) { ti = skip(w - 1 - m * m - m, kb, pn); tj = pn; role = 3; }
+        else if (w - 1 - m * m == 2 * m) { ti = pn; tj = kb; role = 4; }  // row panel, no rest product
+        else { ti = kb; tj = pn; role = 5; }                              // column panel, no rest product
+    } else {
+        const int m = nb - 1;
+        ti = w / m; tj = w % m;
+        if (ti >= kb) ti++;
+        if (tj >= kb) tj++;
+    }
+}
+
+template <int T>
+__global__ __launch_bounds__(256) void fw_restp_kernel(uint16_t* __restrict__ D, int np, int kb, int* __restrict__ flag) {
+    __shared__ __attribute__((aligned(16))) uint16_t At[T * T];
+    __shared__ __attribute__((aligned(16))) uint16_t Bt[T * T];
+    const int nb = np / T;
+    int ti, tj, role;
+    fw_restp_map(blockIdx.x, nb, kb, ti, tj, role);
+    if (ti >= nb || tj >= nb) return;
+    fw_restp_tile<T>(D, np, kb, flag, ti, tj, role, At, Bt);
+}
+
+// fw_restp with persistent plain workgroups (SHD_ROUTE_FWREST=3): workgroup 0 the next
+// pivot, workgroups 1 .. P loop over the plain tiles (t = w - 1 + k P) with the next tile's
+// C block and panel tiles loaded into registers while the current product runs (its
+// staging latency off the critical path), the rest the panel roles as in fw_restp.
+template <int T>
+__global__ __launch_bounds__(256) void fw_restpp_kernel(uint16_t* __restrict__ D, int np, int kb, int* __restrict__ flag,
+                                                        int P) {
+    static_assert(T == 64, "4 x 4 blocks, 4 staging loads per panel and thread");
+    constexpr int R = T / 16, H = R / 2;
+    __shared__ __attribute__((aligned(16))) uint16_t At[T * T];
+    __shared__ __attribute__((aligned(16))) uint16_t Bt[T * T];
+    const int nb = np / T, pn = kb + 1;
+    const int w = blockIdx.x;
+    const int m = pn < nb ? nb - 2 : nb - 1, nplain = m * m;
+    const int base = pn < nb ? 1 : 0;  // first plain tile index in fw_restp_map order
+    int ti, tj, role;
+    if (pn < nb && w == 0) {
+        fw_restp_map(0, nb, kb, ti, tj, role);
+        fw_restp_tile<T>(D, np, kb, flag, ti, tj, role, At, Bt);
+        return;
+    }
+    if (w >= base + P) {  // panel roles
+        fw_restp_map(w - P + nplain, nb, kb, ti, tj, role);
+        if (ti < nb && tj < nb) fw_restp_tile<T>(D, np, kb, flag, ti, tj, role, At, Bt);
+        return;
+    }
+    const int tid = threadIdx.x, r = tid / 16, c = tid % 16;
+    struct Pre { uint2 a[4], b[4], c[R]; };
+    auto load = [&](int t, Pre& x) __attribute__((always_inline)) {
+        int i, j, ro;
+        fw_restp_map(base + t, nb, kb, i, j, ro);
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            const int q = tid + 256 * h;
+            const int rowa = q % T, c4a = (q / T) * 4;            // column panel (i, kb), transposed
+            x.a[h] = *reinterpret_cast<const uint2*>(D + (long long)(i * T + rowa) * np + kb * T + c4a);
+            const int rowb = q / (T / 4), c4b = (q % (T / 4)) * 4;  // row panel (kb, j)
+            x.b[h] = *reinterpret_cast<const uint2*>(D + (long long)(kb * T + rowb) * np + j * T + c4b);
+        }
+#pragma unroll
+        for (int k = 0; k < R; k++) x.c[k] = *reinterpret_cast<const uint2*>(D + (long long)(i * T + R * r + k) * np + j * T + R * c);
+    };
+    Pre cur;
+    int t = w - base;
+    if (t >= nplain) return;
+    load(t, cur);
+    for (;;) {
+        __syncthreads();  // the previous product is done with At / Bt
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            const int q = tid + 256 * h;
+            const int rowa = q % T, c4a = (q / T) * 4;
+            At[(c4a + 0) * T + rowa] = (uint16_t)(cur.a[h].x & 0xFFFFu);
+            At[(c4a + 1) * T + rowa] = (uint16_t)(cur.a[h].x >> 16);
+            At[(c4a + 2) * T + rowa] = (uint16_t)(cur.a[h].y & 0xFFFFu);
+            At[(c4a + 3) * T + rowa] = (uint16_t)(cur.a[h].y >> 16);
+            const int rowb = q / (T / 4), c4b = (q % (T / 4)) * 4;
+            *reinterpret_cast<uint2*>(Bt + rowb * T + c4b) = cur.b[h];
+        }
+        uint32_t acc[R][H];
+#pragma unroll
+        for (int k = 0; k < R; k++) { acc[k][0] = cur.c[k].x; acc[k][1] = cur.c[k].y; }
+        int i, j, ro;
+        fw_restp_map(base + t, nb, kb, i, j, ro);
+        __syncthreads();
+        const int tn = t + P;
+        if (tn < nplain) load(tn, cur);  // in flight during the product
+        fw_tile_product<T>(At, Bt, acc, r, c);
+        fw_store_block<T>(D, np, i, j, r, c, acc);
+        if (tn >= nplain) break;
+        t = tn;
+    }
 }
 
 // The rest update of pivot kb over 128 x 128 regions (2 x 2 tiles of 64) with 8 x 8

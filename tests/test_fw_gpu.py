@@ -207,8 +207,9 @@ def test_c5_direct_table_full(oracle_mod):
 @pytest.mark.parametrize("cfg", ["ba700", "c5"])
 def test_fw_fused_panels_equal_separate_launches(monkeypatch, cfg):
     """The default K4 sequence (each rest launch also closes the next pivot and computes its
-    panels, fw_restp_kernel) against the separate panel + rest launches
-    (SHD_ROUTE_FWREST=1): every SOURCE row of every source bit-identical."""
+    panels, fw_restp_kernel) and its persistent-workgroup form (SHD_ROUTE_FWREST=3, the next
+    tile prefetched during the product; 1024 and 7 workgroups) against the separate panel +
+    rest launches (SHD_ROUTE_FWREST=1): every SOURCE row of every source bit-identical."""
     import torch
     from shadow_amd import route
     g = internet_like(700, 2, seed=23) if cfg == "ba700" else config("c5")
@@ -216,8 +217,9 @@ def test_fw_fused_panels_equal_separate_launches(monkeypatch, cfg):
     dev = torch.device("cuda", 0)
     d_T = torch.from_numpy(T).to(dev)
     out = []
-    for mode in ("0", "1"):
+    for mode, P in (("1", "1024"), ("0", "1024"), ("3", "1024"), ("3", "7")):
         monkeypatch.setenv("SHD_ROUTE_FWREST", mode)
+        monkeypatch.setenv("SHD_ROUTE_FWP", P)
         eng = route.RouteEngine(g)
         lat = torch.empty((g.n, g.n), dtype=torch.float64, device=dev)
         rel = torch.empty_like(lat)
@@ -227,4 +229,5 @@ def test_fw_fused_panels_equal_separate_launches(monkeypatch, cfg):
             eng.fw_rows_async(d_T, d_T, lat, rel, mn)
         eng.sync()
         out.append((lat, rel, mn))
-    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][2], out[1][2])
+    for o in out[1:]:
+        assert torch.equal(out[0][0], o[0]) and torch.equal(out[0][1], o[1]) and torch.equal(out[0][2], o[2])

@@ -276,6 +276,10 @@ static_assert(KD_WCAP == 0 || KD_PREW == 0, "the capped walk's second pass needs
 #ifndef KD_FUSELAT
 #define KD_FUSELAT 0  // phase C: the lat row written inside the pipelined parent copy (identity target lists)
 #endif
+#ifndef KD_LATWALK
+#define KD_LATWALK 0  // phase C: the lat row written by the walks (distances parked in HBM by the copy)
+#endif
+static_assert(KD_LATWALK == 0 || KD_WDYN != 0, "the walks' lat stores prefetch a wave's next block");
 #ifndef KD_ICOND
 #define KD_ICOND 0  // seeded init: a seed's records loaded only for 4-vertex groups where it attains D0
 #endif
@@ -623,9 +627,15 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
     // target in order: positions = vertex ids): the lat row goes out inside the parent copy
     // below, the copy's record loads for the next trip issued before this trip's stores, so
     // neither waits for the other (one in-order vmcnt per wave)
-    const bool fuse_lat = KD_FUSELAT && g.walk && rrow && lrow && tsorted && nt == n &&
+    const bool fuse_lat = KD_FUSELAT && !KD_LATWALK && g.walk && rrow && lrow && tsorted && nt == n &&
                           !(((uintptr_t)lrow >> 3) & 1);
-    if (fuse_lat) {
+    // lat row by the walks (KD_LATWALK, same conditions): the parent copy parks the distances
+    // in the HBM slice, and each walk block stores its targets' lat beside their rel, so the
+    // lat row's stores run under the LDS-bound walks instead of before them
+    const bool walk_lat = KD_LATWALK && g.walk && rrow && lrow && tsorted && nt == n && n >= 64 &&
+                          !(((uintptr_t)lrow >> 3) & 1);
+    KD_GLOBAL uint16_t* const dpark = reinterpret_cast<KD_GLOBAL uint16_t*>(relv) + 2 * (size_t)((n + 7) & ~7);
+    if (fuse_lat || walk_lat) {
     } else if (tsorted) {
         // two adjacent vertices per lane: consecutive positions go out as one 16-B store
         const int lpar = (int)(((uintptr_t)lrow >> 3) & 1);
@@ -683,6 +693,10 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
             uint2 dv[4];
 #pragma unroll
             for (int q = 0; q < 4; q++) dv[q] = *reinterpret_cast<const uint2*>(dist + min(v0 + q * 4 * B, (n - 1) & ~3));
+            if (walk_lat)  // (the group's 4 distances; pads past n land in the parked array's pad)
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (v0 + q * 4 * B < n) *reinterpret_cast<KD_GLOBAL kd_u2*>(dpark + v0 + q * 4 * B) = kd_u2{dv[q].x, dv[q].y};
             // (each thread overwrites only the dist entries it read itself)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
@@ -736,16 +750,16 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
             for (int q = 0; q < 4; q++)
                 pr[q] = *reinterpret_cast<const KD_GLOBAL kd_u4*>(wpr + min(v0 + q * 4 * B, (n - 1) & ~3));
         };
-        if (fuse_lat) {
+        if (fuse_lat || walk_lat) {
             // software-pipelined: trip k + 1's record loads go out before trip k's lat stores
             kd_u4 pa[4], pb[4];
             load_trip(4 * tid, pa);
             for (int v0 = 4 * tid; v0 < n; v0 += 32 * B) {
                 load_trip(v0 + 16 * B, pb);
-                copy_trip(v0, pa, true);
+                copy_trip(v0, pa, fuse_lat);
                 if (v0 + 16 * B >= n) break;
                 load_trip(v0 + 32 * B, pa);
-                copy_trip(v0 + 16 * B, pb, true);
+                copy_trip(v0 + 16 * B, pb, fuse_lat);
             }
         } else {
             for (int v0 = 4 * tid; v0 < n; v0 += 16 * B) {
@@ -754,6 +768,7 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                 copy_trip(v0, pr, false);
             }
         }
+        if (walk_lat) wait_stores();  // the parked distances, visible to every wave's walks
         __syncthreads();
         // Lossless arcs (slot KD_ONE: exactly 1.0) multiply as exact no-ops, so a chain only
         // needs the lossy ones (20% of the arcs on the BASELINE topologies): parv[v] becomes the
@@ -821,8 +836,8 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
         // after NB blocks is listed in ovl (v | j << 16) instead of stored, and the second pass
         // walks the listed chains again in dense waves: a wave then runs for its deepest
         // ordinary chain, not for the deepest chain of any 128 targets (KD_WCAP)
-        auto walk_set = [&](auto NBC, int (&t2)[KD_WQ], int (&jq)[KD_WQ], KD_GLOBAL uint32_t* ovl)
-                            __attribute__((always_inline)) {
+        auto walk_set = [&](auto NBC, int (&t2)[KD_WQ], int (&jq)[KD_WQ], KD_GLOBAL uint32_t* ovl, const bool wlat,
+                            const uint32_t dpair) __attribute__((always_inline)) {
             constexpr int NB = decltype(NBC)::value;
             int cur[KD_WQ];
             uint32_t pk[KD_WQ][NB];
@@ -925,6 +940,32 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                     }
                 }
             }
+            if (wlat) {
+                // lat of this thread's two adjacent targets (identity list: positions = vertices)
+                // from the parked distances, as lat_of computes it
+                double Lq[2];
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const int t = t2[q];
+                    const unsigned d = (dpair >> (16 * q)) & 0xFFFFu;
+                    double Lv = 0.0;
+                    if (t >= 0) {
+                        if (t == s) {
+                            if (isnan(sw_s)) { raise_err(err, SHD_ROUTE_ENOEDGE); Lv = NAN; }
+                            else { Lv = 0.0 + sw_s; lmin = fmin(lmin, Lv); }
+                        } else if (d == 0xFFFFu) { raise_err(err, SHD_ROUTE_EUNREACH); Lv = NAN; }
+                        else { Lv = (double)d; lmin = fmin(lmin, Lv); }
+                    }
+                    Lq[q] = Lv;
+                }
+                // (positions from t2: a chain listed for the second pass has jq = -1 by now, but
+                // its lat is due here)
+                if (KD_OUT) {
+                    if (t2[0] >= 0 && t2[1] == t2[0] + 1)
+                        __builtin_nontemporal_store(kd_d2{Lq[0], Lq[1]}, reinterpret_cast<KD_GLOBAL kd_d2*>(lrow + t2[0]));
+                    else if (t2[0] >= 0) __builtin_nontemporal_store(Lq[0], lrow + t2[0]);
+                }
+            }
         };
         // blocks of KD_WQ x WB targets: the whole workgroup's threads share a block in turn
         // (static), or each wave takes the next block of KD_WQ x 64 from a counter (wdyn: a
@@ -934,12 +975,33 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
         const int li = wdyn ? lane : tid;  // this thread's place in its block
         // (capped first pass: its list over relv's HBM slice, unused by the walks)
         KD_GLOBAL uint32_t* const ovl = KD_WCAP > 0 ? reinterpret_cast<KD_GLOBAL uint32_t*>(relv) : nullptr;
+        // (walk_lat: a wave takes its next block before this one's walks, and loads the next
+        // block's parked distances then, so their wait never includes this block's stores)
+        auto grab = [&]() __attribute__((always_inline)) {
+            int c = 0;
+            if (lane == 0) c = atomicAdd(&sm->wnext, 1);
+            return __builtin_amdgcn_readfirstlane(c) * (KD_WQ * 64);
+        };
+        auto dload = [&](int jb) __attribute__((always_inline)) {
+            const int v = jb + 2 * lane;
+            return jb < lim && v < n ? *reinterpret_cast<const KD_GLOBAL uint32_t*>(dpark + v) : 0xFFFFFFFFu;
+        };
+        int jnext = 0;
+        uint32_t dnext = 0xFFFFFFFFu;
+        if constexpr (KD_LATWALK != 0) {
+            if (walk_lat) { jnext = grab(); dnext = dload(jnext); }
+        }
         for (int blk = 0;; blk++) {
             int jbase;
+            uint32_t dpair = 0xFFFFFFFFu;
             if constexpr (wdyn) {
-                int c = 0;
-                if (lane == 0) c = atomicAdd(&sm->wnext, 1);
-                jbase = __builtin_amdgcn_readfirstlane(c) * (KD_WQ * 64);
+                if (KD_LATWALK != 0 && walk_lat) {
+                    jbase = jnext;
+                    dpair = dnext;
+                    if (jbase < lim) { jnext = grab(); dnext = dload(jnext); }
+                } else {
+                    jbase = grab();
+                }
             } else {
                 jbase = blk * (KD_WQ * BW);
             }
@@ -962,8 +1024,8 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                     t2[q] = j < nt ? tgt[j] : -1;
                 }
             }
-            if constexpr (KD_WCAP > 0) walk_set(std::integral_constant<int, KD_WCAP>{}, t2, jq, ovl);
-            else walk_set(std::integral_constant<int, KD_MAXD / 4>{}, t2, jq, nullptr);
+            if constexpr (KD_WCAP > 0) walk_set(std::integral_constant<int, KD_WCAP>{}, t2, jq, ovl, walk_lat, dpair);
+            else walk_set(std::integral_constant<int, KD_MAXD / 4>{}, t2, jq, nullptr, walk_lat, dpair);
         }
         if constexpr (KD_WCAP > 0) {
             // second pass: the listed chains, 128 per wave-block, walked in full
@@ -983,7 +1045,7 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                     t2[q] = e < novf ? (int)(x & 0xFFFFu) : -1;
                     jq[q] = e < novf ? (int)(x >> 16) : -1;
                 }
-                walk_set(std::integral_constant<int, KD_MAXD / 4>{}, t2, jq, nullptr);
+                walk_set(std::integral_constant<int, KD_MAXD / 4>{}, t2, jq, nullptr, false, 0u);
             }
         }
 #ifdef SHD_STAMPS

@@ -10,7 +10,7 @@ python -c "import json; [print(r['config'], r['layout'], r['fill_s'], r['triangl
 timeout -k 10 300 python -u bench.py --config c5 --steps 10 --no-cpu-baseline > gpurun_out/r4c_c5.json 2> gpurun_out/r4c_c5.err || { tail gpurun_out/r4c_c5.err; exit 1; }
 python -c "import json; d=json.load(open('gpurun_out/r4c_c5.json')); print('C5 K3', d['kernel_ms'], 'FW', d['k4']['fw_table_ms'], 'rows', d['k4']['fw_rows_ms'], d['k4']['rows_verified_vs_oracle'])"
 L=SHD_ROUTE_LIB=shadow_amd/libshd_route
-bash tools/gpu_ab4.sh ${L}_wcap2ds.so ${L}_fl.so ${L}_flw.so ${L}_icond2.so ${L}_flwi.so ${L}_wcap2ds.so ${L}_flwi.so
+bash tools/gpu_ab4.sh ${L}_wcap2ds.so ${L}_fl.so ${L}_flw.so ${L}_lw.so ${L}_icond2.so ${L}_flwi.so ${L}_lwi.so ${L}_wcap2ds.so ${L}_lw.so
 CFG=c3 STEPS=30 bash tools/gpu_ab4.sh "SHD_ROUTE_SEEDS=3" "SHD_ROUTE_KDBLOCK=1024" "SHD_ROUTE_KDBLOCK=1024 SHD_ROUTE_SEEDS=3" "SHD_ROUTE_SEED_ROOTS=2048" "SHD_ROUTE_SEED_DEPTH=6" "SHD_ROUTE_FLAGAT=0.5" ${L}_wcap2ds.so ${L}_icond2.so
 for v in "SHD_ROUTE_FWREST=1" "SHD_ROUTE_FWREST=0" "SHD_ROUTE_FWREST=3" "SHD_ROUTE_FWREST=3 SHD_ROUTE_FWP=2048" "SHD_ROUTE_FWREST=3 SHD_ROUTE_FWP=512"; do
   env $v timeout -k 10 300 python -u bench.py --config c5 --steps 5 --no-cpu-baseline > gpurun_out/r4c_c5v.json 2> gpurun_out/r4c_c5v.err || { tail gpurun_out/r4c_c5v.err; exit 1; }

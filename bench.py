@@ -39,7 +39,7 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
-CFG_INDEX = {"c2": 1, "c3": 2, "c4": 3, "c5": 4, "c2f": 1, "c3f": 2}
+CFG_INDEX = {"c2": 1, "c3": 2, "c4": 3, "c5": 4, "c2f": 1, "c3f": 2, "c4f": 3}
 
 
 def b_src(n, nnz, nt):
@@ -205,7 +205,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=25)  # C4: ~1.2 s timed
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c5", "c2f", "c3f"])
+    ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c5", "c2f", "c3f", "c4f"])
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"])
     ap.add_argument("--allgather", action="store_true", help="strong: all-gather lat+rel shards in every step")
     ap.add_argument("--gather-reps", type=int, default=2, help="strong, N>1: separately timed all-gathers")

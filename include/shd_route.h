@@ -236,7 +236,17 @@ int shd_route_tri_payload_async(shd_route_t* ctx, const double* d_lat, const dou
                                 const int32_t* d_pos, const int64_t* d_off, int32_t nrows, int32_t na, uint32_t flags,
                                 void* d_out_lat, double* d_out_rel, void* stream);
 
-void* shd_route_host_alloc(size_t bytes);  /* pinned host memory (NULL on failure) */
+/* Pinned host memory (NULL on failure), for lr_out above: huge-page-advised anonymous
+ * memory registered with HIP in 256 MiB chunks by background threads.  shd_route_host_alloc
+ * returns once every chunk is registered.  shd_route_host_alloc_lazy returns at once: the
+ * memory may be read and written by the CPU at any time, but until shd_route_host_wait(p)
+ * returns it may be handed to the device only as shd_route_fill_triangle's lr_out, whose
+ * copies wait for each chunk they land in -- so the fill's D2H overlaps the pinning of the
+ * rest (C4's 13.3 GB triangle) instead of following it.  shd_route_host_free takes either. */
+void* shd_route_host_alloc(size_t bytes);
+void* shd_route_host_alloc_lazy(size_t bytes);
+int shd_route_host_wait(void* p);
+void shd_route_host_free(void* p);
 
 /* KD liveness counters since the last reset (no reference equivalent): the longest single
  * wait, in s_sleep rounds, of the delta-stepping kernel's waves on each other -- out[0] a
@@ -245,7 +255,6 @@ void* shd_route_host_alloc(size_t bytes);  /* pinned host memory (NULL on failur
  * stall (both sides of the ring spinning to their caps) shows as 2^22; healthy waits are
  * hundreds.  Synchronises the device; reset != 0 zeroes the counters. */
 int shd_route_kd_stats(shd_route_t* ctx, uint64_t* out, int32_t reset);
-void shd_route_host_free(void* p);
 
 /* K4: all-pairs shortest latencies by blocked min-plus
  * Floyd-Warshall over all vertices, u16 on the device (kept in the context).  Integer

@@ -1654,11 +1654,12 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // default depth cap: about half the rows each workgroup slot runs in turn, so that
         // seed chains are shorter than a slot's queue, and at least 8 (C4: 195 rows per
         // slot, no cap in effect; C3: 9 per slot, cap 8: 3.5 -> 3.1 ms against cap 4)
-        // (seeds per row: three on 1024-thread rows, C4 48.6 -> 48.1 ms; two on 256-thread
-        // rows, whose init pass costs relatively more: C3 3.00 vs 3.07 ms with three)
+        // (seeds per row: three, C4 48.6 -> 48.1 ms; on 256-thread rows, whose init pass costs
+        // relatively more, two measured better in round 2 (C3 3.00 vs 3.07 ms) and three since
+        // the streamed init of round 3 (round 4: C3 2.74 -> 2.67 ms))
         // (multi-GPU ranks: two; a rank's third candidates are mostly two-hop rows, and the
         // extra init pass costs more than they save: 8-way C4 rank 9.6 vs 9.4 ms with three)
-        int kseeds = std::min(KD_SEEDS, c->kd_block >= 1024 && world == 1 ? 3 : 2), nroot_min = c->kd_slots;
+        int kseeds = std::min(KD_SEEDS, world == 1 ? 3 : 2), nroot_min = c->kd_slots;
         int depth = std::max(8, nj / std::max(1, 2 * c->kd_slots));
         if (const char* e = getenv("SHD_ROUTE_SEEDS")) kseeds = std::max(1, std::min(KD_SEEDS, atoi(e)));
         if (const char* e = getenv("SHD_ROUTE_SEED_ROOTS")) nroot_min = std::max(0, atoi(e));
@@ -2226,7 +2227,7 @@ int shd_route_fw_table_async(shd_route_t* c, void* stream) {
     // (default: one launch per pivot); SHD_ROUTE_FWREST=1 the separate panel + rest launches,
     // 2 the 128 x 128-region rest kernel with 8 x 8 blocks (C5 FW table 3.28 ms against 3.06)
     const char* fwr = getenv("SHD_ROUTE_FWREST");
-    const int mode = fwr ? atoi(fwr) : 0;
+    const int mode = fwr ? atoi(fwr) : 3;
     if ((mode == 0 || mode == 3) && nb > 1) {
         if (!c->d_fwflag) {
             if (hipMalloc((void**)&c->d_fwflag, sizeof(int) * (size_t)(nb + 1)) != hipSuccess) return SHD_ROUTE_ENOMEM;
@@ -2392,16 +2393,105 @@ __global__ __launch_bounds__(256) void tri_payload_kernel(const double* __restri
 }
 }  // namespace
 
-extern "C" {
-
-// Pinned host memory for the fill's triangle (C4: 20 GB).  hipHostMalloc faults and pins
-// 4 KiB pages one by one (3.4 s for 20 GiB on the box); anonymous memory advised as
-// transparent huge pages, first-touched by 16 threads and then registered takes 0.15 s
-// for the same D2H rate (tools/micro/pin_bench.cpp).  hipHostMalloc stays the fallback.
+// Pinned host memory for the fill's triangle (C4: 13.3 GB compact, 20 GB interleaved).
+// hipHostMalloc faults and pins 4 KiB pages one by one (3.4 s for 20 GiB on the box);
+// anonymous memory advised as transparent huge pages, populated by several threads and
+// registered takes ~0.15 s for the same D2H rate (tools/micro/pin_bench.cpp).  It is
+// registered in 256 MiB chunks by worker threads, lowest chunk first, so that the fill's
+// copies (shd_route_fill_triangle waits for each chunk it copies into) overlap the pinning
+// of the chunks after them instead of waiting for the whole triangle.  Pages are populated
+// with MADV_POPULATE_WRITE, which never changes their contents (a first-touch store would
+// race with a copy already landing in the chunk).  hipHostMalloc stays the fallback.
 namespace {
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+struct HostMap {
+    char* base = nullptr;  // the mapping (munmap)
+    size_t maplen = 0;
+    char* p = nullptr;     // the caller's pointer (2 MiB aligned)
+    size_t len = 0;
+    size_t chunk = (size_t)256 << 20;
+    int nchunk = 0;
+    std::unique_ptr<std::atomic<int>[]> state;  // per chunk: 0 pending, 1 registered, 2 not registered
+    std::atomic<int> next{0};
+    std::atomic<bool> stop{false};
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<std::thread> th;
+    // wait until every chunk overlapping [off, off + n) is settled (registered or failed)
+    void wait_range(size_t off, size_t n) {
+        if (!n) return;
+        const int c0 = (int)(off / chunk), c1 = (int)std::min<size_t>((off + n - 1) / chunk, nchunk - 1);
+        auto settled = [&] {
+            for (int k = c0; k <= c1; k++)
+                if (state[k].load(std::memory_order_acquire) == 0) return false;
+            return true;
+        };
+        if (settled()) return;
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, settled);
+    }
+    void worker() {
+        for (int k; !stop.load(std::memory_order_relaxed) && (k = next.fetch_add(1)) < nchunk;) {
+            char* a = p + (size_t)k * chunk;
+            const size_t n = std::min(chunk, len - (size_t)k * chunk);
+            (void)madvise(a, n, MADV_POPULATE_WRITE);  // (older kernels: EINVAL, the register faults them)
+            const bool ok = hipHostRegister(a, n, hipHostRegisterPortable) == hipSuccess;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                state[k].store(ok ? 1 : 2, std::memory_order_release);
+            }
+            cv.notify_all();
+        }
+    }
+    ~HostMap() {
+        stop = true;
+        for (auto& t : th) t.join();
+        for (int k = 0; k < nchunk; k++)
+            if (state[k].load() == 1) (void)hipHostUnregister(p + (size_t)k * chunk);
+        if (base) munmap(base, maplen);
+    }
+};
 std::mutex g_host_mu;
-std::map<void*, size_t> g_host_maps;  // registered mappings -> their length
+std::map<char*, std::shared_ptr<HostMap>> g_host_maps;  // by the caller's pointer
+
+std::shared_ptr<HostMap> host_map_of(const void* q) {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    auto it = g_host_maps.upper_bound((char*)q);
+    if (it == g_host_maps.begin()) return nullptr;
+    --it;
+    return (const char*)q < it->first + it->second->len ? it->second : nullptr;
+}
+
+void* host_alloc(size_t bytes, bool lazy) {
+    if (!bytes) bytes = 1;
+    const size_t huge = (size_t)2 << 20;
+    const size_t len = (bytes + huge - 1) & ~(huge - 1);
+    auto m = std::make_shared<HostMap>();
+    void* b = mmap(nullptr, len + huge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (b != MAP_FAILED) {
+        m->base = (char*)b;
+        m->maplen = len + huge;
+        m->p = (char*)(((uintptr_t)b + huge - 1) & ~(uintptr_t)(huge - 1));  // whole huge pages
+        m->len = len;
+        (void)madvise(m->p, len, MADV_HUGEPAGE);
+        m->nchunk = (int)((len + m->chunk - 1) / m->chunk);
+        m->state.reset(new std::atomic<int>[m->nchunk]());
+        const int nth = std::min(m->nchunk, 8);
+        for (int t = 0; t < nth; t++) m->th.emplace_back([mp = m.get()] { mp->worker(); });
+        if (!lazy) m->wait_range(0, len);
+        std::lock_guard<std::mutex> lk(g_host_mu);
+        g_host_maps[m->p] = m;
+        return m->p;
+    }
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) return nullptr;
+    return p;
+}
 }  // namespace
+
+extern "C" {
 
 int shd_route_tri_payload_async(shd_route_t* c, const double* d_lat, const double* d_rel, int64_t ld,
                                 const int32_t* d_pos, const int64_t* d_off, int32_t nrows, int32_t na, uint32_t flags,
@@ -2423,47 +2513,27 @@ int shd_route_tri_payload_async(shd_route_t* c, const double* d_lat, const doubl
     return hip_check(hipGetLastError());
 }
 
-void* shd_route_host_alloc(size_t bytes) {
-    if (!bytes) bytes = 1;
-    const size_t len = (bytes + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
-    void* m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (m != MAP_FAILED) {
-        (void)madvise(m, len, MADV_HUGEPAGE);
-        const int nth = (int)std::max<size_t>(1, std::min<size_t>(16, len >> 28));  // a thread per 256 MiB, <= 16
-        std::vector<std::thread> th;
-        const size_t per = (len / nth + 4095) & ~(size_t)4095;
-        for (int t = 0; t < nth; t++)
-            th.emplace_back([=] {
-                char* b = (char*)m;
-                for (size_t o = per * t; o < std::min(len, per * (t + 1)); o += 4096) b[o] = 0;
-            });
-        for (auto& x : th) x.join();
-        if (hipHostRegister(m, len, hipHostRegisterPortable) == hipSuccess) {
-            std::lock_guard<std::mutex> lk(g_host_mu);
-            g_host_maps[m] = len;
-            return m;
-        }
-        munmap(m, len);
-    }
-    void* p = nullptr;
-    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) return nullptr;
-    return p;
+void* shd_route_host_alloc(size_t bytes) { return host_alloc(bytes, false); }
+
+void* shd_route_host_alloc_lazy(size_t bytes) { return host_alloc(bytes, true); }
+
+int shd_route_host_wait(void* p) {
+    if (!p) return SHD_ROUTE_EINVAL;
+    auto m = host_map_of(p);
+    if (m) m->wait_range(0, m->len);
+    return SHD_ROUTE_OK;
 }
 
 void shd_route_host_free(void* p) {
     if (!p) return;
-    size_t len = 0;
+    std::shared_ptr<HostMap> m;
     {
         std::lock_guard<std::mutex> lk(g_host_mu);
-        auto it = g_host_maps.find(p);
-        if (it != g_host_maps.end()) { len = it->second; g_host_maps.erase(it); }
+        auto it = g_host_maps.find((char*)p);
+        if (it != g_host_maps.end()) { m = std::move(it->second); g_host_maps.erase(it); }
     }
-    if (len) {
-        (void)hipHostUnregister(p);
-        munmap(p, len);
-    } else {
-        (void)hipHostFree(p);
-    }
+    if (!m) (void)hipHostFree(p);
+    // (else the last reference -- a fill still copying holds one -- joins, unregisters, unmaps)
 }
 
 int shd_route_fill_triangle(shd_route_t* c, const int32_t* A, int32_t na, int32_t world, int32_t rank, uint32_t flags,
@@ -2530,6 +2600,22 @@ int shd_route_fill_triangle(shd_route_t* c, const int32_t* A, int32_t na, int32_
     for (int b = 0; b < 2; b++) { (void)hipEventCreateWithFlags(&packed[b], hipEventDisableTiming); (void)hipEventCreateWithFlags(&copied[b], hipEventDisableTiming); }
     int buf = 0;
     bool first[2] = {true, true};
+    // into memory of shd_route_host_alloc_lazy: a copy waits for the chunks it lands in to be
+    // pinned, and never spans two chunks (each is its own registration)
+    const std::shared_ptr<HostMap> hm = host_map_of(lr_out);
+    auto copy_out = [&](char* dst, const char* src, size_t bytes) {
+        while (bytes) {
+            size_t nb = bytes;
+            if (hm) {
+                const size_t o = (size_t)(dst - hm->p);
+                nb = std::min(nb, (o / hm->chunk + 1) * hm->chunk - o);
+                hm->wait_range(o, nb);
+            }
+            if (hipMemcpyAsync(dst, src, nb, hipMemcpyDeviceToHost, xs) != hipSuccess) return false;
+            dst += nb; src += nb; bytes -= nb;
+        }
+        return true;
+    };
     const std::vector<long long>& pk = l16 ? rline : roff;  // packed units: lines or pairs
     const long long stage_units = l16 ? (long long)(16 * stage_pairs / 64) : (long long)stage_pairs;
     for (int r0 = 0; r0 < nr && !rc; buf ^= 1) {
@@ -2554,13 +2640,18 @@ int shd_route_fill_triangle(shd_route_t* c, const int32_t* A, int32_t na, int32_
             if (l16) {
                 while (b < r1 && loff[b] == loff[b - 1] + (na - P->row_pos[b - 1] + 5) / 6) b++;
                 const size_t lines = (size_t)(rline[b] - rline[a]);
-                if (hipMemcpyAsync((char*)lr_out + 64 * loff[a], (char*)dstage[buf].p + 64 * (rline[a] - rline[r0]),
-                                   64 * lines, hipMemcpyDeviceToHost, xs) != hipSuccess) { rc = SHD_ROUTE_EDEVICE; break; }
+                if (!copy_out((char*)lr_out + 64 * loff[a], (char*)dstage[buf].p + 64 * (rline[a] - rline[r0]), 64 * lines)) {
+                    rc = SHD_ROUTE_EDEVICE;
+                    break;
+                }
             } else {
                 while (b < r1 && off[b] == off[b - 1] + (na - P->row_pos[b - 1])) b++;
                 const size_t pairs = (size_t)(roff[b] - roff[a]);
-                if (hipMemcpyAsync(lr_out + 2 * off[a], (double*)dstage[buf].p + 2 * (roff[a] - roff[r0]), 16 * pairs,
-                                   hipMemcpyDeviceToHost, xs) != hipSuccess) { rc = SHD_ROUTE_EDEVICE; break; }
+                if (!copy_out((char*)(lr_out + 2 * off[a]), (char*)((double*)dstage[buf].p + 2 * (roff[a] - roff[r0])),
+                              16 * pairs)) {
+                    rc = SHD_ROUTE_EDEVICE;
+                    break;
+                }
             }
             a = b;
         }

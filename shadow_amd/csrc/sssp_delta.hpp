@@ -259,18 +259,20 @@ constexpr int KD_MAXD = 32;           // phase C path walk: arcs held in registe
 #ifndef KD_PREW
 #define KD_PREW 0                     // waves pre-initialising the next row during the walk (0: off)
 #endif
-// build-time variants (A/B builds, tools/build_var.sh; the defaults are the shipped kernel)
+// build-time variants (A/B builds, tools/build_var.sh; the defaults are the shipped kernel:
+// round 4, C4 45.8 -> 44.2 ms with SDIV 8 + WDYN + WCAP 2 against all three off, C3 2.74 ->
+// 2.76 ms; FUSELAT, LATWALK and ICOND measured 44.9-50.1 ms)
 #ifndef KD_SDIV
-#define KD_SDIV 0   // phase A: a grab takes max(KD_SMIN, queued / KD_SDIV) entries, at most 64 (0: min(64, queued))
+#define KD_SDIV 8   // phase A (1024-thread workgroups): a grab takes max(KD_SMIN, queued / KD_SDIV) entries, at most 64 (0: min(64, queued))
 #endif
 #ifndef KD_SMIN
 #define KD_SMIN 16
 #endif
 #ifndef KD_WDYN
-#define KD_WDYN 0   // phase C: waves take 128-target walk blocks from a counter (0: static blocks)
+#define KD_WDYN 1   // phase C: waves take 128-target walk blocks from a counter (0: static blocks)
 #endif
 #ifndef KD_WCAP
-#define KD_WCAP 0   // phase C: first-pass walks capped at KD_WCAP blocks of 4 arcs, the rest in a second pass (0: one pass)
+#define KD_WCAP 2   // phase C: first-pass walks capped at KD_WCAP blocks of 4 arcs, the rest in a second pass (0: one pass)
 #endif
 static_assert(KD_WCAP == 0 || KD_PREW == 0, "the capped walk's second pass needs every wave");
 #ifndef KD_FUSELAT

@@ -391,8 +391,9 @@ static int fill_locked(shd_topology_t* t) {
         for (int32_t i = 0; i < c->na; i++) c->row16[i + 1] = c->row16[i] + (c->na - i + 5) / 6;
         bytes = 64 * (size_t)c->row16[c->na];
     }
-    /* pinned: the device copies its rows straight into the triangle at full PCIe rate */
-    c->lr = shd_route_host_alloc(bytes ? bytes : 16);
+    /* pinned: the device copies its rows straight into the triangle at full PCIe rate; the
+     * chunks are registered in the background while the rows run and the first chunks copy */
+    c->lr = shd_route_host_alloc_lazy(bytes ? bytes : 16);
     c->cnt = calloc(ntri ? ntri : 1, sizeof(uint32_t));
     if (!c->lr || !c->cnt) { pcache_free(c); return SHD_ROUTE_ENOMEM; }
     int rc = SHD_ROUTE_OK;
@@ -414,6 +415,7 @@ static int fill_locked(shd_topology_t* t) {
             if (jobs[d].min_lat < mn_fill) mn_fill = jobs[d].min_lat;
         }
     }
+    if (!rc) rc = shd_route_host_wait(c->lr);
     if (rc) { pcache_free(c); return rc; }
     /* (s,s) pairs the batch could not store (no self-loop at s): the reference's next
      * (s,s) lookup misses and computes _topology_computeShortestPathToSelf

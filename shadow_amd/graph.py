@@ -159,6 +159,8 @@ CONFIGS = {
     # fractional-latency variants of C2 / C3 (no integer kernel applies)
     "c2f": lambda vloss=False: fractional(internet_like(2000, 5, 1, vloss=vloss, name="c2_ba2k"), 1),
     "c3f": lambda vloss=False: fractional(internet_like(10000, 4, 2, vloss=vloss, hosts=27000, name="c3_ba10k_tor"), 2),
+    "c4f": lambda vloss=False: fractional(internet_like(50000, 10, 3, exact_edges=500000, vloss=vloss,
+                                                        name="c4_as50k"), 3),
 }
 
 

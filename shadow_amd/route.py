@@ -25,6 +25,7 @@ EUNREACH = -5
 EUNSUPPORTED = -6
 DISPATCH = 0x1
 PAYLOAD_LAT16 = 0x1
+FILL_LAT16 = 0x100
 
 
 class RouteError(RuntimeError):
@@ -71,7 +72,7 @@ EXPORTS = (
     "shd_route_plan_create", "shd_route_plan_destroy", "shd_route_plan_get_info", "shd_route_plan_rows",
     "shd_route_rows_planned_async", "shd_route_fw_table_async", "shd_route_fw_rows_async",
     "shd_route_fill_triangle", "shd_route_host_alloc", "shd_route_host_free", "shd_route_tri_payload_async",
-    "shd_route_kd_stats",
+    "shd_route_kd_stats", "shd_route_host_alloc_lazy", "shd_route_host_wait",
 )
 
 _lib = None
@@ -112,6 +113,10 @@ def load_library():
     L.shd_route_host_alloc.restype = P
     L.shd_route_host_alloc.argtypes = [C.c_size_t]
     L.shd_route_host_free.argtypes = [P]
+    L.shd_route_host_alloc_lazy.restype = P
+    L.shd_route_host_alloc_lazy.argtypes = [C.c_size_t]
+    L.shd_route_host_wait.restype = C.c_int
+    L.shd_route_host_wait.argtypes = [P]
     L.shd_route_fw_table_async.restype = C.c_int
     L.shd_route_fw_table_async.argtypes = [P, P]
     L.shd_route_fw_rows_async.restype = C.c_int
@@ -238,14 +243,17 @@ class RouteEngine:
                                                       ptr(d_rel), ptr(d_rowmin), C.c_void_p(stream) if stream else None),
                "shd_route_fw_rows_async")
 
-    def fill_triangle(self, attached, out, world: int = 1, rank: int = 0, dispatch: bool = True):
+    def fill_triangle(self, attached, out, world: int = 1, rank: int = 0, dispatch: bool = True,
+                      lat16: bool = False):
         """shd_route_fill_triangle: this rank's rows of the front end's upper-triangle cache
         over the sorted `attached` vertices into `out` (a PinnedBuffer or any object with
-        .ptr; 16 * na * (na + 1) / 2 bytes).  Returns (min latency written, seconds)."""
+        .ptr; 16 * na * (na + 1) / 2 bytes, or 64 * tri16_lines(na) with lat16: the compact
+        layout).  Returns (min latency written, seconds)."""
         A = np.ascontiguousarray(attached, np.int32)
         mn, sec = C.c_double(), C.c_double()
+        flags = (DISPATCH if dispatch else 0) | (FILL_LAT16 if lat16 else 0)
         rc = load_library().shd_route_fill_triangle(self._h, _p(A), len(A), int(world), int(rank),
-                                                   DISPATCH if dispatch else 0, C.c_void_p(out.ptr),
+                                                   flags, C.c_void_p(out.ptr),
                                                    C.byref(mn), C.byref(sec))
         if rc not in (OK, ENOEDGE, EUNREACH):
             raise RouteError(rc, "shd_route_fill_triangle")
@@ -318,14 +326,29 @@ class RoutePlan:
         _check(rc, "shd_route_rows_planned_async")
 
 
-class PinnedBuffer:
-    """Pinned host memory (shd_route_host_alloc) viewed as float64."""
+def tri16_lines(na: int, i: int | None = None) -> int:
+    """shd_route_tri16_line: first 64-byte line of row i of the compact triangle (i = na, the
+    default: the line count)."""
+    na = int(na)
+    i = na if i is None else int(i)
+    pad = (i // 6) * 15 + sum((6 - (na - t) % 6) % 6 for t in range(i % 6))
+    return (i * na - i * (i - 1) // 2 + pad) // 6
 
-    def __init__(self, nbytes: int):
+
+class PinnedBuffer:
+    """Pinned host memory (shd_route_host_alloc) viewed as float64.  lazy: pinned in the
+    background (shd_route_host_alloc_lazy); hand it to the device only through fill_triangle
+    until wait() returns."""
+
+    def __init__(self, nbytes: int, lazy: bool = False):
         self.nbytes = int(nbytes)
-        self.ptr = load_library().shd_route_host_alloc(self.nbytes)
+        name = "shd_route_host_alloc_lazy" if lazy else "shd_route_host_alloc"
+        self.ptr = getattr(load_library(), name)(self.nbytes)
         if not self.ptr:
-            raise RouteError(ENOMEM, "shd_route_host_alloc")
+            raise RouteError(ENOMEM, name)
+
+    def wait(self):
+        _check(load_library().shd_route_host_wait(C.c_void_p(self.ptr)), "shd_route_host_wait")
 
     def array(self):
         buf = (C.c_double * (self.nbytes // 8)).from_address(self.ptr)

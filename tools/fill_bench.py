@@ -11,6 +11,7 @@ Dijkstra per source on one CPU core.
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
 import resource
@@ -28,15 +29,20 @@ def rss_gb():
 def breakdown(g, T, dev):
     """The same fill straight through the engine (shd_route_fill_triangle), split into:
     pinning the triangle, planning, the rows on the device into HBM, and the whole fill
-    (plan + rows + pack + D2H) twice: the first into freshly pinned pages, then warm."""
+    (plan + rows + pack + D2H) twice: the first into freshly pinned pages, then warm; and
+    the front end's path, a lazily pinned buffer (chunks registered while the rows run and
+    the first chunks copy: shd_route_host_alloc_lazy), timed from the allocation.  The
+    layout is the front end's: compact when the engine reports lat16."""
     import numpy as np
     import torch
     from shadow_amd import route
     eng = route.RouteEngine(g, device=dev)
     A = np.sort(T).astype(np.int32)
     na = len(A)
+    l16 = bool(eng.info["lat16"]) and float(g.latency.max()) < 65535.0
+    nbytes = 64 * route.tri16_lines(na) if l16 else 16 * (na * (na + 1) // 2)
     t0 = time.perf_counter()
-    buf = route.PinnedBuffer(16 * (na * (na + 1) // 2))
+    buf = route.PinnedBuffer(nbytes)
     pin_s = time.perf_counter() - t0
     t0 = time.perf_counter()
     plan = eng.plan(A)
@@ -54,16 +60,22 @@ def breakdown(g, T, dev):
     del lat, rel
     plan.close()
     torch.cuda.empty_cache()
-    _, cold = eng.fill_triangle(A, buf)
-    _, warm = eng.fill_triangle(A, buf)
-    arr = buf.array()
-    probe = float(arr[2 * (na - 1)])  # pair (A[0], A[na-1])
+    _, cold = eng.fill_triangle(A, buf, lat16=l16)
+    _, warm = eng.fill_triangle(A, buf, lat16=l16)
+    ref = np.frombuffer((C.c_char * nbytes).from_address(buf.ptr), np.uint8).copy()
     buf.close()
+    t0 = time.perf_counter()
+    lz = route.PinnedBuffer(nbytes, lazy=True)
+    eng.fill_triangle(A, lz, lat16=l16)
+    lz.wait()
+    lazy_s = time.perf_counter() - t0
+    same = bool(np.array_equal(ref, np.frombuffer((C.c_char * nbytes).from_address(lz.ptr), np.uint8)))
+    lz.close()
     eng.close()
-    return {"pin_s": round(pin_s, 4), "plan_s": round(plan_s, 4), "rows_hbm_s": round(rows_s, 4),
-            "fill_cold_s": round(cold, 4), "fill_warm_s": round(warm, 4),
-            "d2h_GBps_warm": round(16 * (na * (na + 1) // 2) / max(1e-9, warm - plan_s - rows_s) / 1e9, 2),
-            "probe_latency": probe}
+    return {"layout_bytes": nbytes, "pin_s": round(pin_s, 4), "plan_s": round(plan_s, 4),
+            "rows_hbm_s": round(rows_s, 4), "fill_cold_s": round(cold, 4), "fill_warm_s": round(warm, 4),
+            "d2h_GBps_warm": round(nbytes / max(1e-9, warm - plan_s - rows_s) / 1e9, 2),
+            "lazy_alloc_plus_fill_s": round(lazy_s, 4), "lazy_equals_eager": same}
 
 
 def main():

@@ -87,13 +87,14 @@ typedef struct shd_route_info {
     int32_t integer_weights; /* every latency integral and path sums exact in u32 */
     int32_t multigraph;      /* parallel edges present (SURVEY hazard H3) */
     int32_t device;
-    int32_t lds_resident;    /* per-source state fits the 160 KiB LDS */
+    int32_t lds_resident;    /* per-source state fits the 160 KiB LDS (KF above ~12k vertices: 0, KFH) */
     uint64_t device_bytes;   /* resident graph bytes */
     double min_edge_latency;
     int32_t kernel;          /* SSSP kernel: 0 = generic f64, 1 = integer K32 (LDS keys), 2 = KB/KBF
                               * (8 sources per workgroup, C2-class), 4 = KD (delta-stepping, u16
                               * distances, seeded plans), 5 = KF (f64 delta-stepping in LDS: the
-                              * fractional-latency path); 3 = K16 in diagnostic builds only */
+                              * fractional-latency path; with lds_resident 0 its KFH form, vertex
+                              * state in HBM, up to 65535 vertices); 3 = K16 in diagnostic builds only */
     int32_t dist_bound;      /* K32: proven bound on every shortest-path latency (ms) */
     int32_t block;           /* threads per workgroup of the SSSP kernel */
     int32_t reserved;        /* KD: bucket width delta; KB: 1 when path attributes are fused */
@@ -238,11 +239,11 @@ int shd_route_tri_payload_async(shd_route_t* ctx, const double* d_lat, const dou
 
 /* Pinned host memory (NULL on failure), for lr_out above: huge-page-advised anonymous
  * memory registered with HIP in 256 MiB chunks by background threads.  shd_route_host_alloc
- * returns once every chunk is registered.  shd_route_host_alloc_lazy returns at once: the
- * memory may be read and written by the CPU at any time, but until shd_route_host_wait(p)
- * returns it may be handed to the device only as shd_route_fill_triangle's lr_out, whose
- * copies wait for each chunk they land in -- so the fill's D2H overlaps the pinning of the
- * rest (C4's 13.3 GB triangle) instead of following it.  shd_route_host_free takes either. */
+ * returns once every chunk is registered.  shd_route_host_alloc_lazy returns at once: until
+ * shd_route_host_wait(p) returns, the memory may be used only as shd_route_fill_triangle's
+ * lr_out (no CPU reads or writes: the workers first-touch each chunk), whose copies wait for
+ * each chunk they land in -- so the fill's D2H overlaps the pinning of the rest (C4's
+ * 13.3 GB triangle) instead of following it.  shd_route_host_free takes either. */
 void* shd_route_host_alloc(size_t bytes);
 void* shd_route_host_alloc_lazy(size_t bytes);
 int shd_route_host_wait(void* p);

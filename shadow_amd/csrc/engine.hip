@@ -158,6 +158,9 @@ struct shd_route {
     size_t kf_lds = 0;
     double kf_delta = 1.0;
     int kf_nrtab = 0;
+    int kf_h = 0;             // KFH: the per-vertex state in a per-workgroup HBM slice (n > ~12k)
+    char* d_kf_ws = nullptr;
+    size_t kf_ws_stride = 0;
     uint8_t* d_kf_rix = nullptr;
     double* d_kf_rtab = nullptr;
     // K4 (fw.hpp): u16 all-pairs table + dense u16 weights, Np x Np (Np = n rounded to 64)
@@ -735,7 +738,8 @@ const char* shd_route_strerror(int code) {
 // KF eligibility + device arrays (graphs the integer kernels do not take): per in-arc index
 // of its 1 - loss in a table of the distinct values, bucket width, block size.  Fits when
 // the per-source LDS state does and every thread holds at most 16 vertices in the level
-// passes (n <= 16 B).
+// passes (n <= 16 B); above that KFH (n <= 65535: the ring is u16), one 1024-thread
+// workgroup per CU with its vertex state in an HBM slice (C4f: 550 KB per slice).
 int prepare_kf(shd_route* c, const std::vector<int>& row_in, const std::vector<int>& col_in,
                const std::vector<double>& w_in, const std::vector<double>& r_in) {
     const int n = c->n;
@@ -764,8 +768,12 @@ int prepare_kf(shd_route* c, const std::vector<int>& row_in, const std::vector<i
     }
     int blk = 0;
     size_t lds = 0;
+    bool hbm = false;
     if (n <= 16 * 256 && kf_lds_bytes<256>(n) <= kLdsBudget / 4) { blk = 256; lds = kf_lds_bytes<256>(n); }
     else if (n <= 16 * 1024 && kf_lds_bytes<1024>(n) <= kLdsBudget) { blk = 1024; lds = kf_lds_bytes<1024>(n); }
+    else if (n <= 64 * 1024 && kfh_lds_bytes<1024>(n) <= kLdsBudget) { blk = 1024; lds = kfh_lds_bytes<1024>(n); hbm = true; }
+    if (const char* e = getenv("SHD_ROUTE_KFH"))  // (tests: KFH on graphs KF takes)
+        if (atoi(e) && n <= 64 * 1024 && kfh_lds_bytes<1024>(n) <= kLdsBudget) { blk = 1024; lds = kfh_lds_bytes<1024>(n); hbm = true; }
     if (!blk) return SHD_ROUTE_OK;
     // bucket width: the 40th percentile of arc latencies (KF rounds cost far more than the
     // re-expansions wider buckets bring: C3f 15.0 / 13.4 / 13.1 ms at the 12th / 25th / 50th,
@@ -778,11 +786,18 @@ int prepare_kf(shd_route* c, const std::vector<int>& row_in, const std::vector<i
     if (!(delta > 0.0) || std::isinf(delta)) delta = c->min_w > 0 ? c->min_w : 1.0;
     int rc = upload(c, &c->d_kf_rix, rix);
     if (!rc) rc = upload(c, &c->d_kf_rtab, rtab);
-    if (!rc) rc = hip_check(hipFuncSetAttribute(blk == 256 ? (const void*)sssp_f64d_kernel<256> : (const void*)sssp_f64d_kernel<1024>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const void* kfn = hbm ? (const void*)sssp_f64d_kernel<1024, true>
+                          : blk == 256 ? (const void*)sssp_f64d_kernel<256> : (const void*)sssp_f64d_kernel<1024>;
+    if (!rc) rc = hip_check(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (rc) return rc;
     c->kf_block = blk; c->kf_lds = lds; c->kf_delta = delta; c->kf_nrtab = (int)rtab.size();
     c->kf_slots = 256 * std::max(1, std::min((int)(kLdsBudget / lds), 1024 / blk));
+    if (hbm) {
+        c->kf_h = 1;
+        c->kf_ws_stride = kfh_ws_stride<1024>(n);
+        if (hipMalloc((void**)&c->d_kf_ws, c->kf_ws_stride * (size_t)c->kf_slots) != hipSuccess) return SHD_ROUTE_ENOMEM;
+        c->allocs.push_back(c->d_kf_ws);
+    }
     c->sel = 5;
     return SHD_ROUTE_OK;
 }
@@ -952,7 +967,7 @@ int shd_route_get_info(const shd_route_t* c, shd_route_info_t* info) {
     info->integer_weights = c->integer_w;
     info->multigraph = c->multigraph;
     info->device = c->device;
-    info->lds_resident = (c->lds || c->sel) ? 1 : 0;
+    info->lds_resident = ((c->lds || c->sel) && !c->kf_h) ? 1 : 0;  // (KFH: vertex state in HBM)
     info->kernel = c->sel;
     info->dist_bound = c->k32_bound;
     info->block = c->sel == 2 ? KB_BLOCK : c->sel == 3 ? 1024 : c->sel == 4 ? c->kd_block
@@ -1063,12 +1078,15 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         k.rix_in = c->d_kf_rix; k.rtab = c->d_kf_rtab; k.nrtab = c->kf_nrtab;
         k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;
         const int grid = std::min(ns, c->kf_slots);
-        if (c->kf_block == 256)
+        if (c->kf_h)  // (the slices: one per workgroup slot, grid <= kf_slots)
+            hipLaunchKernelGGL((sssp_f64d_kernel<1024, true>), dim3(grid), dim3(1024), c->kf_lds, st, k, d_src, ns, d_tgt,
+                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kf_ws, c->kf_ws_stride);
+        else if (c->kf_block == 256)
             hipLaunchKernelGGL(sssp_f64d_kernel<256>, dim3(grid), dim3(256), c->kf_lds, st, k, d_src, ns, d_tgt, nt,
-                               (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
+                               (long long)ld, d_lat, d_rel, d_row_min, c->d_err, (char*)nullptr, (size_t)0);
         else
             hipLaunchKernelGGL(sssp_f64d_kernel<1024>, dim3(grid), dim3(1024), c->kf_lds, st, k, d_src, ns, d_tgt, nt,
-                               (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
+                               (long long)ld, d_lat, d_rel, d_row_min, c->d_err, (char*)nullptr, (size_t)0);
         return hip_check(hipGetLastError());
     }
     DevGraph g = dev_graph(c);
@@ -2397,15 +2415,14 @@ __global__ __launch_bounds__(256) void tri_payload_kernel(const double* __restri
 // hipHostMalloc faults and pins 4 KiB pages one by one (3.4 s for 20 GiB on the box);
 // anonymous memory advised as transparent huge pages, populated by several threads and
 // registered takes ~0.15 s for the same D2H rate (tools/micro/pin_bench.cpp).  It is
-// registered in 256 MiB chunks by worker threads, lowest chunk first, so that the fill's
-// copies (shd_route_fill_triangle waits for each chunk it copies into) overlap the pinning
-// of the chunks after them instead of waiting for the whole triangle.  Pages are populated
-// with MADV_POPULATE_WRITE, which never changes their contents (a first-touch store would
-// race with a copy already landing in the chunk).  hipHostMalloc stays the fallback.
+// first-touched and registered in 256 MiB chunks by worker threads, lowest chunk first, so
+// that the fill's copies (shd_route_fill_triangle waits for each chunk it copies into)
+// overlap the pinning of the chunks after them instead of waiting for the whole triangle.
+// On the box (tools/micro/pin_overlap.cpp, 8 GiB): 16-thread first-touch 136 GB/s against
+// 30 GB/s for MADV_POPULATE_WRITE, registering touched pages 0.5 GB/ms, and a D2H runs at
+// its full 57 GB/s while other threads touch and register.  (A copy must not span two
+// registrations: the runtime fails it.)  hipHostMalloc stays the fallback.
 namespace {
-#ifndef MADV_POPULATE_WRITE
-#define MADV_POPULATE_WRITE 23
-#endif
 struct HostMap {
     char* base = nullptr;  // the mapping (munmap)
     size_t maplen = 0;
@@ -2436,7 +2453,7 @@ struct HostMap {
         for (int k; !stop.load(std::memory_order_relaxed) && (k = next.fetch_add(1)) < nchunk;) {
             char* a = p + (size_t)k * chunk;
             const size_t n = std::min(chunk, len - (size_t)k * chunk);
-            (void)madvise(a, n, MADV_POPULATE_WRITE);  // (older kernels: EINVAL, the register faults them)
+            for (size_t o = 0; o < n; o += 4096) a[o] = 0;  // (nothing else touches a pending chunk)
             const bool ok = hipHostRegister(a, n, hipHostRegisterPortable) == hipSuccess;
             {
                 std::lock_guard<std::mutex> lk(mu);
@@ -2478,7 +2495,7 @@ void* host_alloc(size_t bytes, bool lazy) {
         (void)madvise(m->p, len, MADV_HUGEPAGE);
         m->nchunk = (int)((len + m->chunk - 1) / m->chunk);
         m->state.reset(new std::atomic<int>[m->nchunk]());
-        const int nth = std::min(m->nchunk, 8);
+        const int nth = std::min(m->nchunk, 12);
         for (int t = 0; t < nth; t++) m->th.emplace_back([mp = m.get()] { mp->worker(); });
         if (!lazy) m->wait_range(0, len);
         std::lock_guard<std::mutex> lk(g_host_mu);

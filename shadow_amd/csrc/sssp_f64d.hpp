@@ -1,7 +1,11 @@
 #pragma once
 // "KF": SOURCE rows for fractional-latency topologies (any positive double latencies) whose
 // per-source state fits LDS (n up to ~12k at 1024 threads, ~3k at four 256-thread workgroups
-// per CU).  One workgroup per source.
+// per CU).  One workgroup per source.  "KFH" (H = true): the same kernel for n up to 65535
+// (C4f: 50k) with the per-vertex state -- f64 distances / relv, u16 parents, u8 reliability
+// indices, 11 B per vertex -- in a per-workgroup HBM slice (most of it lives in L2 / MALL),
+// while the bucket ring, the pending / queued bitmasks and their word minima stay in LDS
+// (2.4 B per vertex), so the rounds' queue work is still LDS work.
 //
 // Replaces igraph_get_shortest_paths_dijkstra (topology.c:1756) +
 // _topology_computePathProperties (topology.c:1407-1523) where the integer kernels (KBF, KD,
@@ -45,6 +49,7 @@ struct DevF64D {
 #ifdef SHD_STAMPS
 #define KF_STAMP(k) do { if (tid == 0 && g.dbg) g.dbg[(size_t)i * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 #define KF_COUNT(k) do { if (tid == 0 && g.dbg) g.dbg[(size_t)i * 16 + (k)] += 1; } while (0)
+#define KF_ADD(k, x) do { if (tid == 0 && g.dbg) g.dbg[(size_t)i * 16 + (k)] += (x); } while (0)
 #define KF_MARK() unsigned long long kf_t = __builtin_amdgcn_s_memtime()
 #define KF_ACC(k) do { if (tid == 0 && g.dbg) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); g.dbg[(size_t)i * 16 + (k)] += t_ - kf_t; kf_t = t_; } } while (0)
 #else
@@ -52,6 +57,7 @@ struct DevF64D {
 #define KF_ACC(k) do { } while (0)
 #define KF_STAMP(k) do { } while (0)
 #define KF_COUNT(k) do { } while (0)
+#define KF_ADD(k, x) do { } while (0)
 #endif
 
 constexpr int KF_HUB = 24;  // phase B: vertices of more in-arcs are done by a whole wave
@@ -96,27 +102,109 @@ struct KFLayout {
 template <int B>
 inline size_t kf_lds_bytes(int n) { return KFLayout<B>::make(n).total; }
 
+// KFH: LDS = small | pend | wmin | inq | ring u16[n] | rtab; HBM slice = dist u64[n] (relv) |
+// par u16[n] | rix u8[n]
 template <int B>
+struct KFHLayout {
+    size_t small, pend, wmin, inq, queue, rtab, total;
+    size_t ws_dist, ws_par, ws_rix, ws_total;
+    __host__ __device__ static KFHLayout make(int n) {
+        KFHLayout L;
+        const size_t nw = (size_t)(n + 63) / 64;
+        size_t o = 0;
+        L.small = o; o += a16(sizeof(KFSmall<B>));
+        L.pend = o;  o += a16(8 * nw);
+        L.wmin = o;  o += a16(8 * nw);
+        L.inq = o;   o += a16(8 * nw);
+        L.queue = o; o += a16(2 * (size_t)n);
+        L.rtab = o;  o += 8 * 256;
+        L.total = o;
+        L.ws_dist = 0;
+        L.ws_par = a16(8 * (size_t)n);
+        L.ws_rix = L.ws_par + a16(2 * (size_t)n);
+        L.ws_total = (L.ws_rix + a16((size_t)n) + 255) & ~(size_t)255;
+        return L;
+    }
+};
+template <int B>
+inline size_t kfh_lds_bytes(int n) { return KFHLayout<B>::make(n).total; }
+template <int B>
+inline size_t kfh_ws_stride(int n) { return KFHLayout<B>::make(n).ws_total; }
+
+// KFH phase C level passes: a thread's vertices v = tid + k B (k < 64, n <= 64 B) pending
+// as bits; per pass each pending vertex reads its parent and factor index and the parent's
+// relv, eight vertices' loads in flight, and is written once its parent is done (the
+// source-first left fold, as the LDS passes).  A value written in a pass may be read in
+// the same pass (every workgroup thread shares the CU's L1, and 64-bit stores are not torn).
+template <int B>
+__device__ __attribute__((always_inline)) int kfh_levels(int n, int s, int tid, int lane, double* relv, const uint16_t* par,
+                                                     const uint8_t* rix, const double* rtl, KFSmall<B>* sm) {
+    unsigned long long rem = 0ull;
+#pragma unroll 1
+    for (int k = 0; k < 64; k++) {
+        const int v = tid + k * B;
+        if (v < n && relv[v] == -1.0) rem |= 1ull << k;
+    }
+    if (tid == 0) sm->flag = 0;
+    __syncthreads();
+    for (int pass = 1;; pass++) {
+        int prog = 0;
+#pragma unroll 1
+        for (int k0 = 0; k0 < 64; k0 += 8) {
+            if (!((rem >> k0) & 0xFFull)) continue;
+            int pq[8];
+            double rp[8], rf[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int v = tid + (k0 + k) * B;
+                const bool live = (rem >> (k0 + k)) & 1ull;
+                pq[k] = live ? (int)par[v] : s;
+                rf[k] = live ? rtl[rix[v]] : 1.0;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) rp[k] = ((rem >> (k0 + k)) & 1ull) ? relv[pq[k]] : -1.0;
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (((rem >> (k0 + k)) & 1ull) && rp[k] != -1.0) {
+                    relv[tid + (k0 + k) * B] = rp[k] * rf[k];
+                    rem &= ~(1ull << (k0 + k));
+                    prog = 1;
+                }
+        }
+        if (__any(prog) && lane == 0) sm->flag = 1;
+        __syncthreads();
+        const int again = sm->flag;
+        __syncthreads();
+        if (tid == 0) sm->flag = 0;
+        if (!again) return pass;
+    }
+}
+
+template <int B, bool H = false>
 __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __restrict__ src, int ns,
                                                       const int* __restrict__ tgt, int nt, long long ld,
                                                       double* __restrict__ lat_out, double* __restrict__ rel_out,
-                                                      double* __restrict__ row_min, int* __restrict__ err) {
+                                                      double* __restrict__ row_min, int* __restrict__ err,
+                                                      char* __restrict__ ws, size_t ws_stride) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int n = g.n, nw = g.nw;
     const KFLayout<B> L = KFLayout<B>::make(n);
-    KFSmall<B>* sm = reinterpret_cast<KFSmall<B>*>(smem + L.small);
-    unsigned long long* dist = reinterpret_cast<unsigned long long*>(smem + L.dist);
-    double* relv = reinterpret_cast<double*>(smem + L.dist);  // phase C, in place of dist
-    unsigned long long* pend = reinterpret_cast<unsigned long long*>(smem + L.pend);
+    const KFHLayout<B> LH = KFHLayout<B>::make(n);
+    char* const wsb = H ? ws + (size_t)blockIdx.x * ws_stride : nullptr;  // KFH: this workgroup's slice
+    KFSmall<B>* sm = reinterpret_cast<KFSmall<B>*>(smem + (H ? LH.small : L.small));
+    unsigned long long* dist = reinterpret_cast<unsigned long long*>(H ? wsb + LH.ws_dist : smem + L.dist);
+    double* relv = reinterpret_cast<double*>(dist);  // phase C, in place of dist
+    unsigned long long* pend = reinterpret_cast<unsigned long long*>(smem + (H ? LH.pend : L.pend));
     // per word a lower bound of its pending distances (bits): a gather opens only the words
     // that can hold work below T
-    unsigned long long* wmin = reinterpret_cast<unsigned long long*>(smem + L.wmin);
-    uint16_t* par = reinterpret_cast<uint16_t*>(smem + L.par);
-    uint8_t* rix = reinterpret_cast<uint8_t*>(smem + L.rix);
-    uint16_t* ring = reinterpret_cast<uint16_t*>(smem + L.queue);
-    unsigned long long* inq = reinterpret_cast<unsigned long long*>(smem + L.inq);  // vertex in the ring
-    int* rowl = reinterpret_cast<int*>(smem + L.rowl);
-    double* rtl = reinterpret_cast<double*>(smem + L.rtab);
+    unsigned long long* wmin = reinterpret_cast<unsigned long long*>(smem + (H ? LH.wmin : L.wmin));
+    uint16_t* par = reinterpret_cast<uint16_t*>(H ? wsb + LH.ws_par : smem + L.par);
+    uint8_t* rix = reinterpret_cast<uint8_t*>(H ? wsb + LH.ws_rix : smem + L.rix);
+    uint16_t* ring = reinterpret_cast<uint16_t*>(smem + (H ? LH.queue : L.queue));
+    unsigned long long* inq = reinterpret_cast<unsigned long long*>(smem + (H ? LH.inq : L.inq));  // vertex in the ring
+    int* rowc = reinterpret_cast<int*>(smem + L.rowl);  // (LDS copy of the out-CSR offsets; KFH reads g.row)
+    const int* rowl = H ? g.row : rowc;
+    double* rtl = reinterpret_cast<double*>(smem + (H ? LH.rtab : L.rtab));
     const int tid = threadIdx.x, lane = tid & 63;
     for (int k = tid; k < 256; k += B) rtl[k] = k < g.nrtab ? g.rtab[k] : NAN;
 
@@ -130,7 +218,8 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
         for (int k = tid; k < nw; k += B) { pend[k] = 0ull; wmin[k] = kInfBits; inq[k] = 0ull; }
         if (tid == 0) { sm->qtail = 0; sm->rhead = 0; sm->ovf = 0; sm->mpend[0] = sm->mpend[1] = kInfBits; }
         int gpar = 0;  // gather parity
-        for (int v = tid; v <= n; v += B) rowl[v] = g.row[v];  // (phase B reuses this LDS)
+        if (!H)
+            for (int v = tid; v <= n; v += B) rowc[v] = g.row[v];  // (phase B reuses this LDS)
         __syncthreads();
         if (tid == 0) {
             dist[s] = 0ull;
@@ -465,6 +554,10 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
         // parents' values at once per pass; a value written during a pass may be read in the
         // same pass (64-bit LDS accesses are not torn), which only finishes chains sooner
         // (parents and factor indices packed: 2 x u16 and 4 x u8 per register)
+        if constexpr (H) {
+            [[maybe_unused]] const int passes = kfh_levels<B>(n, s, tid, lane, relv, par, rix, rtl, sm);
+            KF_ADD(7, passes);
+        } else {
         uint32_t pk2[8], rx4[4];
         unsigned rem = 0;
 #pragma unroll
@@ -509,6 +602,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
             if (tid == 0) sm->flag = 0;
             KF_COUNT(7);
             if (!again) break;
+        }
         }
         KF_STAMP(4);
         for (int j = tid; j < nt; j += B) {

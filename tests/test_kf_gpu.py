@@ -157,3 +157,50 @@ def test_kf_extreme_bucket_widths(route, oracle_mod, monkeypatch, delta):
     assert np.array_equal(lat, olat)
     assert np.array_equal(rel, orel)
     assert np.array_equal(mn, olat.min(axis=1))
+
+
+# ---- KFH: the vertex state in an HBM slice (n above KF's LDS limit; C4f) ----------------
+
+def test_kfh_equals_kf_rows(route, monkeypatch):
+    # KFH forced on C2f (which KF takes): every row bit-identical to KF's, three launches
+    g = config("c2f")
+    tgt = g.targets()
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    e0 = route.RouteEngine(g)
+    assert e0.info["kernel"] == 5 and e0.info["lds_resident"] == 1
+    l0, r0, m0 = e0.rows(tgt, tgt, dispatch=False)
+    monkeypatch.setenv("SHD_ROUTE_KFH", "1")
+    e1 = route.RouteEngine(g)
+    assert e1.info["kernel"] == 5 and e1.info["lds_resident"] == 0
+    for _ in range(3):
+        lat, rel, mn = e1.rows(tgt, tgt, dispatch=False)
+        assert np.array_equal(lat, l0) and np.array_equal(rel, r0) and np.array_equal(mn, m0)
+
+
+def test_kfh_vertex_loss_directed(route, oracle_mod, monkeypatch):
+    g = fractional(internet_like(3000, 3, 5, vloss=True, hosts=2500, name="kfh_vl"), 3)
+    monkeypatch.setenv("SHD_ROUTE_KFH", "1")
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 5 and eng.info["lds_resident"] == 0
+    tgt = g.targets()
+    src = tgt[::41]
+    lat, rel, mn = eng.rows(src, tgt, dispatch=False)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(src, tgt, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    np.testing.assert_allclose(rel, orel, rtol=REL_TOL, atol=0)
+
+
+def test_kfh_20k_vertices(route, oracle_mod, monkeypatch):
+    # above KF's LDS limit: KFH by default, sampled rows bit-exact against the oracle
+    g = fractional(internet_like(20000, 4, 6, name="kfh_20k"), 5)
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    monkeypatch.delenv("SHD_ROUTE_KFH", raising=False)
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 5 and eng.info["lds_resident"] == 0
+    tgt = g.targets()
+    src = np.concatenate([tgt[:3], tgt[::977], tgt[-2:]]).astype(np.int32)
+    lat, rel, mn = eng.rows(src, tgt, dispatch=False)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(src, tgt, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(rel, orel)
+    assert np.array_equal(mn, olat.min(axis=1))

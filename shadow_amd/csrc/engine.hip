@@ -1076,6 +1076,8 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         k.row = c->d_row; k.col = c->d_col; k.w = c->d_w;
         k.row_in = c->d_row_in; k.col_in = c->d_col_in; k.w_in = c->d_w_in;
         k.rix_in = c->d_kf_rix; k.rtab = c->d_kf_rtab; k.nrtab = c->kf_nrtab;
+        k.hring = 0;
+        if (const char* e = getenv("SHD_ROUTE_KFH_RING")) k.hring = std::max(0, atoi(e));  // (tests: a small ring)
         k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;
         const int grid = std::min(ns, c->kf_slots);
         if (c->kf_h)  // (the slices: one per workgroup slot, grid <= kf_slots)

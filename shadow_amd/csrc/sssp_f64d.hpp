@@ -41,6 +41,7 @@ struct DevF64D {
     const uint8_t* __restrict__ rix_in;  // index of each in-arc's 1 - loss in rtab
     const double* __restrict__ rtab;     // distinct 1 - loss values (<= 254)
     int nrtab;
+    int hring;                           // KFH: ring entries cap (0: what LDS holds; tests)
     const double* __restrict__ vf;
     const double* __restrict__ self_w;
     const double* __restrict__ self_r;
@@ -102,11 +103,13 @@ struct KFLayout {
 template <int B>
 inline size_t kf_lds_bytes(int n) { return KFLayout<B>::make(n).total; }
 
-// KFH: LDS = small | pend | wmin | inq | ring u16[n] | rtab; HBM slice = dist u64[n] (relv) |
-// par u16[n] | rix u8[n]
+// KFH: LDS = small | pend | wmin | inq | key u16[n] | ring u16[R] | rtab, the ring taking
+// what LDS is left (R <= n; C4f: 19.6k entries); HBM slice = dist u64[n] (relv) | par u16[n]
+// | rix u8[n]
 template <int B>
 struct KFHLayout {
-    size_t small, pend, wmin, inq, queue, rtab, total;
+    size_t small, pend, wmin, inq, key, queue, rtab, total;
+    unsigned ring;  // ring entries
     size_t ws_dist, ws_par, ws_rix, ws_total;
     __host__ __device__ static KFHLayout make(int n) {
         KFHLayout L;
@@ -116,7 +119,11 @@ struct KFHLayout {
         L.pend = o;  o += a16(8 * nw);
         L.wmin = o;  o += a16(8 * nw);
         L.inq = o;   o += a16(8 * nw);
-        L.queue = o; o += a16(2 * (size_t)n);
+        L.key = o;   o += a16(2 * (size_t)n + 2);
+        L.queue = o;
+        const size_t room = o + 8 * 256 + 64 * 2 <= kLdsBudget ? (kLdsBudget - o - 8 * 256) / 2 : 64;
+        L.ring = (unsigned)(room < (size_t)n ? room & ~(size_t)63 : (size_t)n);
+        o += a16(2 * (size_t)L.ring);
         L.rtab = o;  o += 8 * 256;
         L.total = o;
         L.ws_dist = 0;
@@ -130,6 +137,35 @@ template <int B>
 inline size_t kfh_lds_bytes(int n) { return KFHLayout<B>::make(n).total; }
 template <int B>
 inline size_t kfh_ws_stride(int n) { return KFHLayout<B>::make(n).ws_total; }
+
+// KFH distance keys: a u16 per vertex in LDS, monotone in the f64 distance (0 below 1 ms,
+// then 12 mantissa bits per binade up to ~65 s, 65535 above and for +inf), kept equal to
+// key(dist) by an LDS min after every improving atomicMin.  Keys only fall, so a stale key
+// is larger than the true one, and key(nd) > key[v] proves nd > dist[v]: a relaxation is
+// dropped there without touching HBM.  Phase B bounds a neighbour's distance by its key's
+// interval [lo, hi) and loads it only when fl(lo + w) <= d[v] <= fl(hi + w) can hold.
+__device__ inline unsigned kf_key(unsigned long long b) {
+    constexpr unsigned long long one = 0x3FF0000000000000ull;
+    return b < one ? 0u : (unsigned)min((b - one) >> 40, 65534ull) + 1u;
+}
+__device__ inline double kf_key_lo(unsigned k) {
+    return k == 0 ? 0.0 : as_d(0x3FF0000000000000ull + ((unsigned long long)(k - 1) << 40));
+}
+__device__ inline double kf_key_hi(unsigned k) {
+    return k == 0 ? 1.0 : k >= 65535 ? (double)INFINITY : as_d(0x3FF0000000000000ull + ((unsigned long long)k << 40));
+}
+__device__ inline void kf_key_min(uint16_t* keyl, int v, unsigned k) {
+    unsigned* w = reinterpret_cast<unsigned*>(keyl) + (v >> 1);
+    const int sh = (v & 1) * 16;
+    unsigned old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (;;) {
+        if (((old >> sh) & 0xFFFFu) <= k) return;
+        const unsigned nw = (old & ~(0xFFFFu << sh)) | (k << sh);
+        const unsigned prev = atomicCAS(w, old, nw);
+        if (prev == old) return;
+        old = prev;
+    }
+}
 
 // KFH phase C level passes: a thread's vertices v = tid + k B (k < 64, n <= 64 B) pending
 // as bits; per pass each pending vertex reads its parent and factor index and the parent's
@@ -205,6 +241,8 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
     int* rowc = reinterpret_cast<int*>(smem + L.rowl);  // (LDS copy of the out-CSR offsets; KFH reads g.row)
     const int* rowl = H ? g.row : rowc;
     double* rtl = reinterpret_cast<double*>(smem + (H ? LH.rtab : L.rtab));
+    uint16_t* keyl = reinterpret_cast<uint16_t*>(smem + LH.key);  // (KFH only)
+    const unsigned R = H ? (g.hring > 0 ? min(LH.ring, (unsigned)g.hring) : LH.ring) : (unsigned)n;  // ring entries
     const int tid = threadIdx.x, lane = tid & 63;
     for (int k = tid; k < 256; k += B) rtl[k] = k < g.nrtab ? g.rtab[k] : NAN;
 
@@ -215,6 +253,8 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
             continue;
         }
         for (int v = tid; v < n; v += B) dist[v] = kInfBits;
+        if (H)
+            for (int v = tid; v < (n + 1) / 2; v += B) reinterpret_cast<unsigned*>(keyl)[v] = 0xFFFFFFFFu;
         for (int k = tid; k < nw; k += B) { pend[k] = 0ull; wmin[k] = kInfBits; inq[k] = 0ull; }
         if (tid == 0) { sm->qtail = 0; sm->rhead = 0; sm->ovf = 0; sm->mpend[0] = sm->mpend[1] = kInfBits; }
         int gpar = 0;  // gather parity
@@ -225,6 +265,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
             dist[s] = 0ull;
             pend[s >> 6] = 1ull << (s & 63);
             wmin[s >> 6] = 0ull;
+            if (H) keyl[s] = 0;
         }
         double T = g.delta;
         __syncthreads();
@@ -288,10 +329,20 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                     for (unsigned long long b = take; b;) {
                         const int bi = __ffsll((long long)b) - 1;
                         b &= b - 1;
-                        ring[pos++ % (unsigned)n] = (uint16_t)((k << 6) + bi);
+                        if (!H || pos - qhead < R) {
+                            ring[pos % R] = (uint16_t)((k << 6) + bi);
+                        } else {  // (KFH: the ring is full; the vertex stays pending, its word's
+                                  // bound 0 until the next gather recomputes it)
+                            pend[k] |= 1ull << bi;
+                            atomicAnd(&inq[k], ~(1ull << bi));
+                            wmin[k] = 0ull;
+                        }
+                        pos++;
                     }
                 }
                 __syncthreads();
+                if (H && tid == 0 && (unsigned)sm->qtail - qhead > R) sm->qtail = (int)(qhead + R);
+                if (H) __syncthreads();
                 KF_COUNT(10);
                 KF_ACC(8);
                 continue;  // (an empty gather -- a loose lower bound -- recomputes T)
@@ -316,11 +367,13 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                 KF_ACC(9);
                 const int q = c + lane;
                 int u = 0, beg = 0, deg = 0;
+                double dun = 0.0;  // (KFH: the entry's distance, one HBM load per entry)
                 if (q < qn) {
-                    u = ring[(qhead + (unsigned)q) % (unsigned)n];
+                    u = ring[(qhead + (unsigned)q) % R];
                     atomicAnd(&inq[u >> 6], ~(1ull << (u & 63)));  // (may be queued again below)
                     beg = rowl[u];
                     deg = rowl[u + 1] - beg;
+                    if (H) dun = as_d(dist[u]);
                 }
                 const int incl = kd_wave_incl_sum(deg);
                 const int total = __builtin_amdgcn_readlane(incl, 63);
@@ -349,12 +402,13 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                     }
                     __builtin_amdgcn_wave_barrier();  // (the marks are read before the next trip clears them)
                     int aq[4], uq[4], vq[4];
-                    double wq[4];
+                    double wq[4], duq[4];
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         const int p = p0 + r * 64 + lane;
                         const int ob = __shfl(beg, lo[r], 64), oe = __shfl(excl, lo[r], 64);
                         uq[r] = __shfl(u, lo[r], 64);
+                        if (H) duq[r] = __shfl(dun, lo[r], 64);
                         aq[r] = p < total ? ob + (p - oe) : -1;
                     }
                     KF_ACC(13);
@@ -366,15 +420,26 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                     }
                     if (tid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     KF_ACC(14);
+                    // (KFH: the key filter, then the candidates' HBM atomics issued together)
+                    unsigned long long hold[4];
+                    if constexpr (H) {
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const unsigned long long nb = as_u(duq[r] + wq[r]);
+                            const bool cand = aq[r] >= 0 && kf_key(nb) <= keyl[vq[r]];
+                            hold[r] = cand ? atomicMin(&dist[vq[r]], nb) : 0ull;
+                        }
+                    }
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         if (aq[r] < 0) continue;
                         const int v = vq[r];
-                        const double nd = as_d(dist[uq[r]]) + wq[r];
+                        const double nd = (H ? duq[r] : as_d(dist[uq[r]])) + wq[r];
                         const unsigned long long nb = as_u(nd);
-                        if (nb < dist[v]) {
-                            const unsigned long long old = atomicMin(&dist[v], nb);
+                        if (H || nb < dist[v]) {
+                            const unsigned long long old = H ? hold[r] : atomicMin(&dist[v], nb);
                             if (nb < old) {
+                                if (H) kf_key_min(keyl, v, kf_key(nb));
                                 const unsigned long long bit = 1ull << (v & 63);
                                 if (nd < T) {  // this bucket: straight back into the ring
                                     if (!(atomicOr(&inq[v >> 6], bit) & bit)) {
@@ -383,7 +448,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                                         // late): a push past them is dropped and flagged, and the
                                         // round's end moves the whole ring to the pending bitmask
                                         const unsigned at = (unsigned)atomicAdd(&sm->qtail, 1);
-                                        if (at - qhead < (unsigned)n) ring[at % (unsigned)n] = (uint16_t)v;
+                                        if (at - qhead < R) ring[at % R] = (uint16_t)v;
                                         else sm->ovf = 1;
                                     }
                                 } else {
@@ -418,6 +483,15 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
         // workgroup, for hundreds of trips) are listed and done by whole waves below.
         if (tid == 0) sm->qtail = 0;  // (hub list length; the ring is free now)
         __syncthreads();
+        // a neighbour's distance for the tightness test (KFH: INFINITY -- never tight -- when
+        // its key interval rules the arc out, so most in-arcs cost no HBM load)
+        auto dnb = [&](int u, double w, double dv) __attribute__((always_inline)) {
+            if constexpr (H) {
+                const unsigned ku = keyl[u];
+                if (!(kf_key_lo(ku) + w <= dv && dv <= kf_key_hi(ku) + w)) return (double)INFINITY;
+            }
+            return as_d(dist[u]);
+        };
         for (int v0 = tid; v0 < n; v0 += 2 * B) {
             int vv[2], a0[2], a1[2], bu[2], ba[2];
             double dv[2], bd[2];
@@ -430,19 +504,23 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                 a0[h] = scan ? g.row_in[vv[h]] : 0;
                 a1[h] = scan ? g.row_in[vv[h] + 1] : 0;
                 if (a1[h] - a0[h] > KF_HUB) {
-                    ring[atomicAdd(&sm->qtail, 1)] = (uint16_t)vv[h];
-                    a1[h] = a0[h];
-                    vv[h] = -1 - vv[h];  // (written by the wave below)
+                    const int hs = atomicAdd(&sm->qtail, 1);
+                    if (!H || hs < (int)R) {  // (KFH: a full list leaves the hub to its thread)
+                        ring[hs] = (uint16_t)vv[h];
+                        a1[h] = a0[h];
+                        vv[h] = -1 - vv[h];  // (written by the wave below)
+                    }
                 }
                 bd[h] = INFINITY; bu[h] = 0x7fffffff; ba[h] = -1;
             }
-            for (int t0 = 0; t0 < max(a1[0] - a0[0], a1[1] - a0[1]); t0 += 4) {
-                int uq[2][4];
-                double wq[2][4];
+            constexpr int KBW = H ? 8 : 4;  // in-arcs per vertex and step (KFH: more HBM loads in flight)
+            for (int t0 = 0; t0 < max(a1[0] - a0[0], a1[1] - a0[1]); t0 += KBW) {
+                int uq[2][KBW];
+                double wq[2][KBW];
 #pragma unroll
                 for (int h = 0; h < 2; h++)
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
+                    for (int q = 0; q < KBW; q++) {
                         const int a = min(a0[h] + t0 + q, max(a1[h] - 1, 0));
                         uq[h][q] = g.col_in[a];
                         wq[h][q] = g.w_in[a];
@@ -450,9 +528,9 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
 #pragma unroll
                 for (int h = 0; h < 2; h++)
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
+                    for (int q = 0; q < KBW; q++) {
                         if (a0[h] + t0 + q >= a1[h]) continue;
-                        const double du = as_d(dist[uq[h][q]]);
+                        const double du = dnb(uq[h][q], wq[h][q], dv[h]);
                         if (du + wq[h][q] == dv[h] && (du < bd[h] || (du == bd[h] && uq[h][q] < bu[h]))) {
                             bd[h] = du; bu[h] = uq[h][q]; ba[h] = a0[h] + t0 + q;
                         }
@@ -474,7 +552,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
             // hubs: 16 lanes per hub (four hubs per wave at a time), 4 in-arcs per lane and
             // step with the loads in flight, then the lexicographic (d[u], u, arc) minimum
             // over the hub's 16 lanes
-            const int nhub = sm->qtail;
+            const int nhub = min(sm->qtail, (int)R);
             const int sub = lane >> 4, sl = lane & 15;
             for (int h0 = (tid >> 6) * 4; h0 < nhub; h0 += (B / 64) * 4) {
                 const int h = h0 + sub;
@@ -497,7 +575,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                     for (int q = 0; q < 4; q++) {
                         const int a = t + 16 * q;
                         if (a >= a1) continue;
-                        const double du = as_d(dist[uq[q]]);
+                        const double du = dnb(uq[q], wq[q], dv);
                         if (du + wq[q] == dv && (du < bd || (du == bd && (uq[q] < bu || (uq[q] == bu && a < ba))))) {
                             bd = du; bu = uq[q]; ba = a;
                         }

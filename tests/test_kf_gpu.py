@@ -177,6 +177,26 @@ def test_kfh_equals_kf_rows(route, monkeypatch):
         assert np.array_equal(lat, l0) and np.array_equal(rel, r0) and np.array_equal(mn, m0)
 
 
+@pytest.mark.parametrize("ring", ["64", "700"])
+def test_kfh_small_ring(route, oracle_mod, monkeypatch, ring):
+    # KFH's ring holds what LDS leaves (C4f: 19.6k of 50k vertices): a gather that finds more
+    # vertices below the bucket bound than the ring holds leaves the rest pending, a push
+    # past it moves the ring to the pending bitmask, a hub list past it leaves the hubs to
+    # their threads.  A 64 / 700-entry ring on C2f (2000 vertices) takes all three paths
+    g = config("c2f")
+    monkeypatch.setenv("SHD_ROUTE_KFH", "1")
+    monkeypatch.setenv("SHD_ROUTE_KFH_RING", ring)
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 5 and eng.info["lds_resident"] == 0
+    tgt = g.targets()
+    src = tgt[::13]
+    lat, rel, mn = eng.rows(src, tgt, dispatch=False)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(src, tgt, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(rel, orel)
+    assert np.array_equal(mn, olat.min(axis=1))
+
+
 def test_kfh_vertex_loss_directed(route, oracle_mod, monkeypatch):
     g = fractional(internet_like(3000, 3, 5, vloss=True, hosts=2500, name="kfh_vl"), 3)
     monkeypatch.setenv("SHD_ROUTE_KFH", "1")

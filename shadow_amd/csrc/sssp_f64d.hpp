@@ -68,7 +68,7 @@ struct KFSmall {
     int qtail;     // ring entries queued (mod n); phase B: hub list length
     int rhead;     // slices of the round taken
     int flag;
-    int ovf;       // a push of this round found no free ring slot (the ring is dropped after it)
+    int ovf[2];    // a push of this round found no free ring slot (the ring is dropped after it), by round parity
     unsigned long long wmark[B / 64][4];  // per wave: start marks of a trip's four windows
     unsigned long long mpend[2];  // lower bound of the pending distances (bits), by gather parity
     unsigned long long rmin;
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
         if (H)
             for (int v = tid; v < (n + 1) / 2; v += B) reinterpret_cast<unsigned*>(keyl)[v] = 0xFFFFFFFFu;
         for (int k = tid; k < nw; k += B) { pend[k] = 0ull; wmin[k] = kInfBits; inq[k] = 0ull; }
-        if (tid == 0) { sm->qtail = 0; sm->rhead = 0; sm->ovf = 0; sm->mpend[0] = sm->mpend[1] = kInfBits; }
+        if (tid == 0) { sm->qtail = 0; sm->rhead = 0; sm->ovf[0] = sm->ovf[1] = 0; sm->mpend[0] = sm->mpend[1] = kInfBits; }
         int gpar = 0;  // gather parity
         if (!H)
             for (int v = tid; v <= n; v += B) rowc[v] = g.row[v];  // (phase B reuses this LDS)
@@ -277,7 +277,8 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
         // below T queues it straight back, so a bucket's rounds need no gather.  Vertices
         // improved to T or above wait in the pending bitmask with per-word lower bounds;
         // only an empty ring (the bucket done) opens the next bucket by one gather.
-        unsigned qhead = 0;  // ring entries [qhead, sm->qtail) are queued (mod n)
+        unsigned qhead = 0;  // ring entries [qhead, sm->qtail) are queued (mod R)
+        int rpar = 0;        // round parity (the overflow flag of the round)
         for (;;) {
             KF_MARK();
             if (qhead == (unsigned)sm->qtail) {
@@ -354,6 +355,8 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
             KF_COUNT(6);
             const int qn = (int)(qend - qhead);
             __syncthreads();  // every wave has read the round's end before any wave queues more
+            // (the other parity's flag was read by every thread before this barrier)
+            if (tid == 0) sm->ovf[rpar ^ 1] = 0;
             // waves pull 64-entry slices of the round's entries (no block barrier inside a
             // round); a slice's arcs are spread over its lanes, 4 positions per lane and trip,
             // owners by a binary search over the slice's lane offsets (ds_bpermute), the 8
@@ -449,7 +452,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                                         // round's end moves the whole ring to the pending bitmask
                                         const unsigned at = (unsigned)atomicAdd(&sm->qtail, 1);
                                         if (at - qhead < R) ring[at % R] = (uint16_t)v;
-                                        else sm->ovf = 1;
+                                        else sm->ovf[rpar] = 1;
                                     }
                                 } else {
                                     atomicOr(&pend[v >> 6], bit);
@@ -463,7 +466,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
             __syncthreads();
             if (tid == 0) sm->rhead = 0;  // (every wave has left the loop above)
             qhead = qend;
-            if (sm->ovf) {  // (uniform) ring overflow: its vertices (inq) become pending, the ring empty
+            if (sm->ovf[rpar]) {  // (uniform) ring overflow: its vertices (inq) become pending, the ring empty
                 for (int k = tid; k < nw; k += B) {
                     const unsigned long long b = inq[k];
                     if (b) { pend[k] |= b; wmin[k] = 0ull; inq[k] = 0ull; }  // (0: a valid lower bound)
@@ -471,8 +474,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                 qhead = (unsigned)sm->qtail;
                 KF_COUNT(15);
             }
-            __syncthreads();
-            if (tid == 0) sm->ovf = 0;  // (every thread has read it)
+            rpar ^= 1;
             KF_ACC(9);
         }
 

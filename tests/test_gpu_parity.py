@@ -206,5 +206,9 @@ def test_kernel_selection(route):
     g2.latency = g2.latency + 0.25  # fractional -> KF (LDS-resident f64 delta-stepping)
     assert route.RouteEngine(g2).info["kernel"] == 5
     g3 = internet_like(20000, 2, seed=3)
-    g3.latency = g3.latency + 0.25  # fractional, past KF's LDS -> the generic f64 kernel
-    assert route.RouteEngine(g3).info["kernel"] == 0
+    g3.latency = g3.latency + 0.25  # fractional, past KF's LDS -> KFH (vertex state in HBM)
+    e3 = route.RouteEngine(g3)
+    assert e3.info["kernel"] == 5 and e3.info["lds_resident"] == 0
+    g4 = internet_like(70000, 2, seed=3)
+    g4.latency = g4.latency + 0.25  # past KFH's u16 ring ids -> the generic f64 kernel
+    assert route.RouteEngine(g4).info["kernel"] == 0

@@ -13,8 +13,9 @@ tests)
   timeout -k 10 180 python -u __graft_entry__.py smoke || exit 1
   ;;
 bench)
-  for cfg in c4 c3 c2 c5 c3f c2f; do
+  for cfg in c4 c3 c2 c5 c3f c2f c4f; do
     extra="--no-cpu-baseline"; steps=20
+    [ $cfg = c4f ] && steps=3
     [ $cfg = c4 ] && extra=""
     [ $cfg = c5 ] && extra=""
     SHD_ROUTE_PLAN_DEBUG=1 timeout -k 10 400 python -u bench.py --config $cfg --steps $steps --warmup 5 $extra > gpurun_out/r4_bench_$cfg.json 2> gpurun_out/r4_bench_$cfg.err || { echo BENCH $cfg FAILED; tail gpurun_out/r4_bench_$cfg.err; exit 1; }

@@ -19,6 +19,7 @@ ks c4 --config c4 --steps 5 --warmup 1
 ks c5 --config c5 --steps 5 --warmup 1
 ks c3f --config c3f --steps 3 --warmup 1
 ks c2f --config c2f --steps 10 --warmup 2
+ks c4f --config c4f --steps 2 --warmup 1
 pmc() {  # cfg counter bench-args...
   local cfg=$1 ctr=$2; shift 2
   timeout -s KILL 120 rocprofv3 --pmc $ctr -d gpurun_out/prof_$tag/pmc_$cfg/$ctr -o run --output-format csv \

@@ -285,6 +285,12 @@ static_assert(KD_LATWALK == 0 || KD_WDYN != 0, "the walks' lat stores prefetch a
 #ifndef KD_ICOND
 #define KD_ICOND 0  // seeded init: a seed's records loaded only for 4-vertex groups where it attains D0
 #endif
+#ifndef KD_SEEDANY
+#define KD_SEEDANY 0   // with KD_SEEDSPIN: wait for any one seed (not the first) before the bounded polls
+#endif
+#ifndef KD_SEEDSPIN
+#define KD_SEEDSPIN 8  // seeded init: polls (s_sleep 8 each) of a second or third seed's flag before it is dropped (0: wait; round 4: C3 2.68 -> 2.53 ms, C4 44.7 -> 44.4)
+#endif
 constexpr int KD_PRESPIN = 32;        // pre-init: polls of a seed's flag (s_sleep 8 each) before giving up
 constexpr int KD_WQ = 2;              // phase C path walk: targets per thread (4 measured 1% slower at C4: its registers put 39 VGPRs of the output function in callee-saved ranges, saved to scratch and restored around every row; 2: 13)
 constexpr int KD_ONE = 254;           // phase C: rtab slot holding 1.0 (the source's own step)
@@ -1355,29 +1361,56 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
                 *reinterpret_cast<uint4*>(dist + v0) = *reinterpret_cast<const uint4*>(dstg + v0);
         } else if (seeded) {
             uint32_t* const wpr = wpr_of();
-            SEED_VIEW();
             // the seeds' rows are ready: one relaxed poll of each flag, one agent-scope
-            // acquire (this CU's L1 invalidated), then every wave reads them with plain loads
+            // acquire (this CU's L1 invalidated), then every wave reads them with plain loads.
+            // With KD_SEEDSPIN > 0 a seed after the first that is not ready within that many
+            // polls is dropped from the job (any subset of the seeds gives exact rows: the
+            // fix-up phases start from whichever upper bounds D0 holds)
             if (tid == 0) {
 #ifdef SHD_STAMPS
                 const unsigned long long w0 = __builtin_amdgcn_s_memtime();
 #endif
-                for (int q = 0; q < nseed; q++) {
+                const int ns0 = sm->job.nseed;
+                if (KD_SEEDANY && KD_SEEDSPIN > 0) {  // (first any ready seed, then the bounded polls)
+                    for (int spin = 0;; spin++) {
+                        bool any = false;
+                        for (int q = 0; q < ns0; q++)
+                            any = any || __hip_atomic_load(&g.done[sm->job.seed[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                        if (any) break;
+                        if (spin >= (1 << 22)) { raise_err(err, SHD_ROUTE_EDEVICE); break; }
+                        __builtin_amdgcn_s_sleep(8);
+                    }
+                }
+                int kept = 0;
+                for (int q = 0; q < ns0; q++) {
+                    const int* const flag = &g.done[sm->job.seed[q]];
+                    const int cap = ((q == 0 && !KD_SEEDANY) || KD_SEEDSPIN == 0) ? (1 << 22) : KD_SEEDSPIN;
                     int spin = 0;
-                    while (__hip_atomic_load(&g.done[sslot[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-                           spin < (1 << 22)) {
+                    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && spin < cap) {
                         __builtin_amdgcn_s_sleep(8);
                         spin++;
                     }
                     if (spin >= (1 << 22)) raise_err(err, SHD_ROUTE_EDEVICE);
+                    if (spin >= cap && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+                        continue;  // (KD_SEEDSPIN: dropped)
+                    if (kept != q) {
+                        sm->job.seed[kept] = sm->job.seed[q];
+                        sm->job.u[kept] = sm->job.u[q];
+                        sm->job.wr[kept] = sm->job.wr[q];
+                        sm->job.rec[kept] = sm->job.rec[q];
+                    }
+                    kept++;
                 }
+                sm->job.nseed = kept;
 #ifdef SHD_STAMPS
                 sm->acc[31] += __builtin_amdgcn_s_memtime() - w0;
+                sm->acc[36] += ns0 - kept;
 #endif
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
+            SEED_VIEW();
             // one streaming pass, 8 vertices per lane (16-B loads of every seed's distances
             // and parent records): D0(v) = min_j w(s,u_j) + d_{u_j}(v), saturating at 0xFFFF
             // (= unreached), into LDS; and the parent record a vertex keeps if it never

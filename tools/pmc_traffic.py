@@ -10,7 +10,7 @@ import os
 import sys
 
 HOT = ("sssp_batch_kernel", "sssp_batch_rows_kernel", "path_attr_kernel", "sssp_k32_kernel", "sssp_rows_kernel", "sssp_k16", "sssp_delta_kernel",
-       "direct_rows_kernel", "fw_rest", "fw_diag", "fw_panel", "fw_parent", "fw_rows", "fw_inlist")
+       "direct_rows_kernel", "sssp_f64d_kernel", "fw_rest", "fw_diag", "fw_panel", "fw_parent", "fw_rows", "fw_inlist")
 
 
 def load(path):

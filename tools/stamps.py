@@ -105,7 +105,8 @@ if eng.info["kernel"] == 4:
     print(f"  wave0 per group: owners {d[:, 30].mean() / ng:.0f}  owners+loads {d[:, 27].mean() / ng:.0f}  process {d[:, 28].mean() / ng:.0f} (relax {d[:, 29].mean() / ng:.0f}) cyc")
     print(f"  queue overflow/source: pushes to pending {d[:, 14].mean():.0f}  gathered past capacity {d[:, 15].mean():.0f}")
     print(f"  drain of the previous row's stores {d[:, 9].mean():.0f}")
-    print(f"  seeded init {d[:, 29].mean():.0f} (seed wait {d[:, 31].mean():.0f})  A' copy {d[:, 27].mean():.0f}  A' events {d[:, 28].mean():.0f} cyc/source")
+    print(f"  seeded init {d[:, 29].mean():.0f} (seed wait {d[:, 31].mean():.0f}, {100 * d[:, 31].mean() / max(d[:, 29].mean(), 1):.0f}% of it; "
+          f"seeds dropped {d[:, 36].mean():.3f}/row)  A' copy {d[:, 27].mean():.0f}  A' events {d[:, 28].mean():.0f} cyc/source")
     for k, nm in [(11, "minreduce"), (8, "gather"), (9, "prep"), (10, "expand"), (16, "B.short"), (17, "B.long"),
                   (18, "lat row+drain"), (19, "par copy"), (13, "C.compute")]:
         print(f"  A.{nm:10s} mean {d[:, k].mean():10.0f} cyc  ({d[:, k].mean() / max(d[:, 5].mean(), 1):.0f}/sweep)")

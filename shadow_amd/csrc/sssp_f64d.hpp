@@ -68,7 +68,8 @@ struct KFSmall {
     int qtail;     // ring entries queued (mod n); phase B: hub list length
     int rhead;     // slices of the round taken
     int flag;
-    int ovf[2];    // a push of this round found no free ring slot (the ring is dropped after it), by round parity
+    int ovf;       // a push of this round found no free ring slot (the ring is dropped after it); 256-thread
+                   // workgroups: bit p for a round of parity p
     unsigned long long wmark[B / 64][4];  // per wave: start marks of a trip's four windows
     unsigned long long mpend[2];  // lower bound of the pending distances (bits), by gather parity
     unsigned long long rmin;
@@ -256,7 +257,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
         if (H)
             for (int v = tid; v < (n + 1) / 2; v += B) reinterpret_cast<unsigned*>(keyl)[v] = 0xFFFFFFFFu;
         for (int k = tid; k < nw; k += B) { pend[k] = 0ull; wmin[k] = kInfBits; inq[k] = 0ull; }
-        if (tid == 0) { sm->qtail = 0; sm->rhead = 0; sm->ovf[0] = sm->ovf[1] = 0; sm->mpend[0] = sm->mpend[1] = kInfBits; }
+        if (tid == 0) { sm->qtail = 0; sm->rhead = 0; sm->ovf = 0; sm->mpend[0] = sm->mpend[1] = kInfBits; }
         int gpar = 0;  // gather parity
         if (!H)
             for (int v = tid; v <= n; v += B) rowc[v] = g.row[v];  // (phase B reuses this LDS)
@@ -356,7 +357,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
             const int qn = (int)(qend - qhead);
             __syncthreads();  // every wave has read the round's end before any wave queues more
             // (the other parity's flag was read by every thread before this barrier)
-            if (tid == 0) sm->ovf[rpar ^ 1] = 0;
+            if (B < 1024 && tid == 0) sm->ovf &= ~(1 << (rpar ^ 1));
             // waves pull 64-entry slices of the round's entries (no block barrier inside a
             // round); a slice's arcs are spread over its lanes, 4 positions per lane and trip,
             // owners by a binary search over the slice's lane offsets (ds_bpermute), the 8
@@ -452,7 +453,8 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                                         // round's end moves the whole ring to the pending bitmask
                                         const unsigned at = (unsigned)atomicAdd(&sm->qtail, 1);
                                         if (at - qhead < R) ring[at % R] = (uint16_t)v;
-                                        else sm->ovf[rpar] = 1;
+                                        else if (B < 1024) atomicOr(&sm->ovf, 1 << rpar);
+                                        else sm->ovf = 1;
                                     }
                                 } else {
                                     atomicOr(&pend[v >> 6], bit);
@@ -466,7 +468,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
             __syncthreads();
             if (tid == 0) sm->rhead = 0;  // (every wave has left the loop above)
             qhead = qend;
-            if (sm->ovf[rpar]) {  // (uniform) ring overflow: its vertices (inq) become pending, the ring empty
+            if (B < 1024 ? (sm->ovf >> rpar) & 1 : sm->ovf) {  // (uniform) ring overflow: its vertices (inq) become pending, the ring empty
                 for (int k = tid; k < nw; k += B) {
                     const unsigned long long b = inq[k];
                     if (b) { pend[k] |= b; wmin[k] = 0ull; inq[k] = 0ull; }  // (0: a valid lower bound)
@@ -474,7 +476,14 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                 qhead = (unsigned)sm->qtail;
                 KF_COUNT(15);
             }
+            // (the flag's reset: 256-thread rows clear the other parity's bit at the next
+            // round's start, which spares a barrier per round: C2f 0.72 -> 0.45 ms; 1024-thread
+            // rows keep the barrier, measured faster there: C3f 10.4 against 10.6-10.7 ms)
             rpar ^= 1;
+            if (B >= 1024) {
+                __syncthreads();
+                if (tid == 0) sm->ovf = 0;  // (every thread has read it)
+            }
             KF_ACC(9);
         }
 

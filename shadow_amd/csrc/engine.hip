@@ -1611,11 +1611,42 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         std::iota(pos.begin(), pos.end(), 0);
         by_rank(pos);
         std::vector<int> fpar(ns, -1), flvl(ns, 0), sub(ns, 1);
+        // each row's best seed (the forest's parent): on the device, one wave per row (the
+        // plan's seed-choice kernel with k = 1: ~1 ms with the copies at C4, against ~6 ms
+        // of host CSR scans on every rank); SHD_ROUTE_GPUCHOICE=0 keeps the host scan
+        std::vector<int> bu(ns, -1);
+        bool dev_forest = !(getenv("SHD_ROUTE_GPUCHOICE") && atoi(getenv("SHD_ROUTE_GPUCHOICE")) == 0) &&
+                          c->d_kd_orec != nullptr;
+        if (dev_forest) {
+            std::vector<uint8_t> av(n);
+            for (int v = 0; v < n; v++) av[v] = first[v] >= 0;
+            DevBuf dcl, drk, dav, dsq, dout;
+            std::vector<PlanChoice> ho(ns);
+            dev_forest = !dcl.alloc(sizeof(double) * n) && !drk.alloc(sizeof(int) * n) && !dav.alloc(n) &&
+                         !dsq.alloc(sizeof(int) * ns) && !dout.alloc(sizeof(PlanChoice) * ns) &&
+                         hipMemcpy(dcl.p, c->close.data(), sizeof(double) * n, hipMemcpyHostToDevice) == hipSuccess &&
+                         hipMemcpy(drk.p, rk.data(), sizeof(int) * n, hipMemcpyHostToDevice) == hipSuccess &&
+                         hipMemcpy(dav.p, av.data(), n, hipMemcpyHostToDevice) == hipSuccess &&
+                         hipMemcpy(dsq.p, src, sizeof(int) * ns, hipMemcpyHostToDevice) == hipSuccess;
+            if (dev_forest) {
+                hipLaunchKernelGGL(plan_choice_kernel, dim3((ns + 3) / 4), dim3(256), 0, 0, c->d_row, c->d_kd_orec,
+                                   (const double*)dcl.p, (const int*)drk.p, (const uint8_t*)dav.p, (const int*)dsq.p, ns,
+                                   1, 0, 0, alpha, (PlanChoice*)dout.p);
+                dev_forest = hipGetLastError() == hipSuccess &&
+                             hipMemcpy(ho.data(), dout.p, sizeof(PlanChoice) * ns, hipMemcpyDeviceToHost) == hipSuccess;
+            }
+            if (dev_forest)
+                for (int p = 0; p < ns; p++) bu[p] = ho[p].m > 0 ? ho[p].u[0] : -1;
+        }
+        if (!dev_forest)
+            for (int p = 0; p < ns; p++) {
+                int a;
+                bu[p] = best_seeds(p, [&](int u) { return first[u] >= 0; }, 1, &a) ? c->h_col[a] : -1;
+            }
         int maxl = 0;
         for (int p : pos) {
-            int a;
-            if (best_seeds(p, [&](int u) { return first[u] >= 0; }, 1, &a)) {
-                fpar[p] = first[c->h_col[a]];
+            if (bu[p] >= 0) {
+                fpar[p] = first[bu[p]];
                 flvl[p] = flvl[fpar[p]] + 1;
             }
             maxl = std::max(maxl, flvl[p]);

@@ -108,6 +108,28 @@ def test_plans_independent_of_host_workers(oracle_mod, kd):
     assert np.array_equal(lat, olat) and np.array_equal(rel, orel)
 
 
+@pytest.mark.parametrize("cfg,world", [("c2", 3), ("c3", 8)])
+def test_partition_forest_device_equals_host(kd, cfg, world):
+    """A multi-GPU plan's seed forest (every row's best seed, which decides the partition) is
+    computed on the device by default; SHD_ROUTE_GPUCHOICE=0 computes it (and the seed
+    choices) with the host scan.  Every rank's rows and plan shape must be the same."""
+    from shadow_amd import route
+    g = config(cfg)
+    T = g.targets()
+    eng = route.RouteEngine(g)
+    dev = []
+    for r in range(world):
+        p = eng.plan(T, world, r)
+        dev.append((p.info, p.positions.copy()))
+        p.close()
+    kd.setenv("SHD_ROUTE_GPUCHOICE", "0")
+    for r in range(world):
+        p = eng.plan(T, world, r)
+        assert p.info == dev[r][0]
+        assert np.array_equal(p.positions, dev[r][1])
+        p.close()
+
+
 def test_directed_plan_falls_back(oracle_mod, kd):
     from shadow_amd import route
     g = _graph("dir")

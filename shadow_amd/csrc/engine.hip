@@ -777,9 +777,11 @@ int prepare_kf(shd_route* c, const std::vector<int>& row_in, const std::vector<i
     if (!blk) return SHD_ROUTE_OK;
     // bucket width: the 40th percentile of arc latencies (KF rounds cost far more than the
     // re-expansions wider buckets bring: C3f 15.0 / 13.4 / 13.1 ms at the 12th / 25th / 50th,
-    // C2f 0.60 / 0.55 / 0.57 ms)
+    // C2f 0.60 / 0.55 / 0.57 ms); KFH the 10th, where a re-expansion is HBM traffic (C4f, the
+    // width in ms: 15 / 25 / 35 / 50 / 70 / ~100 (40th) / 200: 822 / 815 / 822 / 835 / 842 /
+    // 886 / 1061 ms)
     std::vector<double> ws(w_in.begin(), w_in.end());
-    const size_t k = ws.size() * 40 / 100;
+    const size_t k = ws.size() * (hbm ? 10 : 40) / 100;
     std::nth_element(ws.begin(), ws.begin() + k, ws.end());
     double delta = ws[k];
     if (const char* e = getenv("SHD_ROUTE_KFDELTA")) delta = atof(e);

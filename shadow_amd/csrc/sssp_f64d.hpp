@@ -62,6 +62,9 @@ struct DevF64D {
 #endif
 
 constexpr int KF_HUB = 24;  // phase B: vertices of more in-arcs are done by a whole wave
+#ifndef KFH_HUB
+#define KFH_HUB KF_HUB  // (KFH's threshold; C4f 12 / 24 / 48 / 96: 830 / 814 / 860 / 905 ms)
+#endif
 
 template <int B>
 struct KFSmall {
@@ -514,7 +517,7 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                 const bool scan = ok && vv[h] != s && dv[h] < INFINITY;
                 a0[h] = scan ? g.row_in[vv[h]] : 0;
                 a1[h] = scan ? g.row_in[vv[h] + 1] : 0;
-                if (a1[h] - a0[h] > KF_HUB) {
+                if (a1[h] - a0[h] > (H ? KFH_HUB : KF_HUB)) {
                     const int hs = atomicAdd(&sm->qtail, 1);
                     if (!H || hs < (int)R) {  // (KFH: a full list leaves the hub to its thread)
                         ring[hs] = (uint16_t)vv[h];

@@ -238,12 +238,18 @@ int shd_route_tri_payload_async(shd_route_t* ctx, const double* d_lat, const dou
                                 void* d_out_lat, double* d_out_rel, void* stream);
 
 /* Pinned host memory (NULL on failure), for lr_out above: huge-page-advised anonymous
- * memory registered with HIP in 256 MiB chunks by background threads.  shd_route_host_alloc
- * returns once every chunk is registered.  shd_route_host_alloc_lazy returns at once: until
- * shd_route_host_wait(p) returns, the memory may be used only as shd_route_fill_triangle's
- * lr_out (no CPU reads or writes: the workers first-touch each chunk), whose copies wait for
- * each chunk they land in -- so the fill's D2H overlaps the pinning of the rest (C4's
- * 13.3 GB triangle) instead of following it.  shd_route_host_free takes either. */
+ * memory first-touched in 256 MiB chunks by background threads.  shd_route_host_alloc
+ * returns once the whole buffer is touched and registered with HIP as ONE registration
+ * (any copy may span it; hipHostMalloc if the registration fails).
+ * shd_route_host_alloc_lazy returns at once and registers each 256 MiB chunk separately:
+ * until shd_route_host_wait(p) returns, the memory may be used only as
+ * shd_route_fill_triangle's lr_out (no CPU reads or writes: the workers first-touch each
+ * chunk), whose copies wait for each chunk they land in -- so the fill's D2H overlaps the
+ * pinning of the rest (C4's 13.3 GB triangle) instead of following it.  A caller's own
+ * hipMemcpy into lazy memory must not span a 256 MiB chunk boundary (the runtime fails a
+ * copy across two registrations).  shd_route_host_wait returns SHD_ROUTE_EDEVICE when a
+ * chunk could not be registered (it stays pageable: usable, slower).  shd_route_host_free
+ * takes either. */
 void* shd_route_host_alloc(size_t bytes);
 void* shd_route_host_alloc_lazy(size_t bytes);
 int shd_route_host_wait(void* p);

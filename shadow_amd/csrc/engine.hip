@@ -2295,11 +2295,11 @@ int shd_route_fw_table_async(shd_route_t* c, void* stream) {
             const int nx = kb + 1 < nb ? 2 : 0;  // the next pivot's panel tiles in row / column kb
             if (mode == 0) {
                 hipLaunchKernelGGL(fw_restp_kernel<FW_T>, dim3((nb - 1) * (nb - 1) + nx), dim3(256), 0, st, c->d_fwD, np,
-                                   kb, c->d_fwflag);
+                                   kb, c->d_fwflag, c->d_err);
             } else {
                 const int m = kb + 1 < nb ? nb - 2 : nb - 1, pp = std::max(1, std::min(P, m * m));
                 const int grid = kb + 1 < nb ? 1 + pp + 2 * m + 2 : pp;
-                hipLaunchKernelGGL(fw_restpp_kernel<FW_T>, dim3(grid), dim3(256), 0, st, c->d_fwD, np, kb, c->d_fwflag, pp);
+                hipLaunchKernelGGL(fw_restpp_kernel<FW_T>, dim3(grid), dim3(256), 0, st, c->d_fwD, np, kb, c->d_fwflag, pp, c->d_err);
             }
         }
         c->fw_ready = 1;
@@ -2466,6 +2466,9 @@ struct HostMap {
     size_t chunk = (size_t)256 << 20;
     int nchunk = 0;
     std::unique_ptr<std::atomic<int>[]> state;  // per chunk: 0 pending, 1 registered, 2 not registered
+    bool whole = false;    // eager form: chunks are only first-touched (state 1 = touched), then
+                           // the whole range is registered once, so any copy may span it
+    bool whole_reg = false;
     std::atomic<int> next{0};
     std::atomic<bool> stop{false};
     std::mutex mu;
@@ -2489,7 +2492,7 @@ struct HostMap {
             char* a = p + (size_t)k * chunk;
             const size_t n = std::min(chunk, len - (size_t)k * chunk);
             for (size_t o = 0; o < n; o += 4096) a[o] = 0;  // (nothing else touches a pending chunk)
-            const bool ok = hipHostRegister(a, n, hipHostRegisterPortable) == hipSuccess;
+            const bool ok = whole || hipHostRegister(a, n, hipHostRegisterPortable) == hipSuccess;
             {
                 std::lock_guard<std::mutex> lk(mu);
                 state[k].store(ok ? 1 : 2, std::memory_order_release);
@@ -2500,8 +2503,12 @@ struct HostMap {
     ~HostMap() {
         stop = true;
         for (auto& t : th) t.join();
-        for (int k = 0; k < nchunk; k++)
-            if (state[k].load() == 1) (void)hipHostUnregister(p + (size_t)k * chunk);
+        if (whole) {
+            if (whole_reg) (void)hipHostUnregister(p);
+        } else {
+            for (int k = 0; k < nchunk; k++)
+                if (state[k].load() == 1) (void)hipHostUnregister(p + (size_t)k * chunk);
+        }
         if (base) munmap(base, maplen);
     }
 };
@@ -2530,12 +2537,22 @@ void* host_alloc(size_t bytes, bool lazy) {
         (void)madvise(m->p, len, MADV_HUGEPAGE);
         m->nchunk = (int)((len + m->chunk - 1) / m->chunk);
         m->state.reset(new std::atomic<int>[m->nchunk]());
+        m->whole = !lazy;
         const int nth = std::min(m->nchunk, 12);
         for (int t = 0; t < nth; t++) m->th.emplace_back([mp = m.get()] { mp->worker(); });
-        if (!lazy) m->wait_range(0, len);
-        std::lock_guard<std::mutex> lk(g_host_mu);
-        g_host_maps[m->p] = m;
-        return m->p;
+        bool ok = true;
+        if (!lazy) {
+            // touched in parallel, then one registration (a caller's single large copy into
+            // the buffer must not span two registrations); on failure, hipHostMalloc below
+            m->wait_range(0, len);
+            m->whole_reg = ok = hipHostRegister(m->p, len, hipHostRegisterPortable) == hipSuccess;
+        }
+        if (ok) {
+            std::lock_guard<std::mutex> lk(g_host_mu);
+            g_host_maps[m->p] = m;
+            return m->p;
+        }
+        m.reset();  // (joins the touch workers and unmaps)
     }
     void* p = nullptr;
     if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) return nullptr;
@@ -2572,7 +2589,13 @@ void* shd_route_host_alloc_lazy(size_t bytes) { return host_alloc(bytes, true); 
 int shd_route_host_wait(void* p) {
     if (!p) return SHD_ROUTE_EINVAL;
     auto m = host_map_of(p);
-    if (m) m->wait_range(0, m->len);
+    if (!m) return SHD_ROUTE_OK;
+    m->wait_range(0, m->len);
+    // a chunk the runtime refused to register stays pageable: copies into it still work,
+    // slower, and the caller is told
+    if (!m->whole)
+        for (int k = 0; k < m->nchunk; k++)
+            if (m->state[k].load(std::memory_order_acquire) == 2) return SHD_ROUTE_EDEVICE;
     return SHD_ROUTE_OK;
 }
 

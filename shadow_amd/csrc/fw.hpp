@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void fw_rest_kernel(uint16_t* __restrict__ D, 
 // after pivot kb's update, 4 / 5 the same without it (tiles of pivot kb's own panels)
 template <int T>
 __device__ inline void fw_restp_tile(uint16_t* __restrict__ D, int np, int kb, int* __restrict__ flag, int ti, int tj,
-                                     int role, uint16_t* At, uint16_t* Bt) {
+                                     int role, uint16_t* At, uint16_t* Bt, int* __restrict__ err) {
     constexpr int R = T / 16, H = R / 2;
     const int pn = kb + 1;
     const int tid = threadIdx.x, r = tid / 16, c = tid % 16;
@@ -314,6 +314,9 @@ __device__ inline void fw_restp_tile(uint16_t* __restrict__ D, int np, int kb, i
                 __builtin_amdgcn_s_sleep(2);
                 spin++;
             }
+            // a pivot never published (a lost or stalled closing workgroup): the product
+            // below would read an open tile, so the launch reports a device error
+            if (spin >= (1 << 24)) raise_err(err, SHD_ROUTE_EDEVICE);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -367,14 +370,15 @@ __device__ inline void fw_restp_map(int w, int nb, int kb, int& ti, int& tj, int
 }
 
 template <int T>
-__global__ __launch_bounds__(256) void fw_restp_kernel(uint16_t* __restrict__ D, int np, int kb, int* __restrict__ flag) {
+__global__ __launch_bounds__(256) void fw_restp_kernel(uint16_t* __restrict__ D, int np, int kb, int* __restrict__ flag,
+                                                       int* __restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint16_t At[T * T];
     __shared__ __attribute__((aligned(16))) uint16_t Bt[T * T];
     const int nb = np / T;
     int ti, tj, role;
     fw_restp_map(blockIdx.x, nb, kb, ti, tj, role);
     if (ti >= nb || tj >= nb) return;
-    fw_restp_tile<T>(D, np, kb, flag, ti, tj, role, At, Bt);
+    fw_restp_tile<T>(D, np, kb, flag, ti, tj, role, At, Bt, err);
 }
 
 // fw_restp with persistent plain workgroups (SHD_ROUTE_FWREST=3): workgroup 0 the next
@@ -383,7 +387,7 @@ __global__ __launch_bounds__(256) void fw_restp_kernel(uint16_t* __restrict__ D,
 // staging latency off the critical path), the rest the panel roles as in fw_restp.
 template <int T>
 __global__ __launch_bounds__(256) void fw_restpp_kernel(uint16_t* __restrict__ D, int np, int kb, int* __restrict__ flag,
-                                                        int P) {
+                                                        int P, int* __restrict__ err) {
     static_assert(T == 64, "4 x 4 blocks, 4 staging loads per panel and thread");
     constexpr int R = T / 16, H = R / 2;
     __shared__ __attribute__((aligned(16))) uint16_t At[T * T];
@@ -395,12 +399,12 @@ __global__ __launch_bounds__(256) void fw_restpp_kernel(uint16_t* __restrict__ D
     int ti, tj, role;
     if (pn < nb && w == 0) {
         fw_restp_map(0, nb, kb, ti, tj, role);
-        fw_restp_tile<T>(D, np, kb, flag, ti, tj, role, At, Bt);
+        fw_restp_tile<T>(D, np, kb, flag, ti, tj, role, At, Bt, err);
         return;
     }
     if (w >= base + P) {  // panel roles
         fw_restp_map(w - P + nplain, nb, kb, ti, tj, role);
-        if (ti < nb && tj < nb) fw_restp_tile<T>(D, np, kb, flag, ti, tj, role, At, Bt);
+        if (ti < nb && tj < nb) fw_restp_tile<T>(D, np, kb, flag, ti, tj, role, At, Bt, err);
         return;
     }
     const int tid = threadIdx.x, r = tid / 16, c = tid % 16;

@@ -892,7 +892,10 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                         if (more) {
                             const int at = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-                            ovl[at] = (uint32_t)t2[q] | ((uint32_t)jq[q] << 16);
+                            // sorted targets: vertex | position << 16 (both < n <= 65535);
+                            // a caller's list: the full 32-bit position (the vertex is
+                            // tgt[position]), since such a list may exceed 65535 entries
+                            ovl[at] = tsorted ? (uint32_t)t2[q] | ((uint32_t)jq[q] << 16) : (uint32_t)jq[q];
                             jq[q] = -1;  // stored by the second pass
                         }
                     }
@@ -981,8 +984,11 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
         constexpr bool wdyn = KD_WDYN != 0;
         const int WB = wdyn ? 64 : BW;
         const int li = wdyn ? lane : tid;  // this thread's place in its block
-        // (capped first pass: its list over relv's HBM slice, unused by the walks)
-        KD_GLOBAL uint32_t* const ovl = KD_WCAP > 0 ? reinterpret_cast<KD_GLOBAL uint32_t*>(relv) : nullptr;
+        // (capped first pass: its list over relv's HBM slice, unused by the walks; the slice
+        // holds 2n entries, and a list gets at most one per target position, so a caller's
+        // unsorted list longer than 2n (duplicates) walks uncapped in one pass instead)
+        KD_GLOBAL uint32_t* const ovl =
+            KD_WCAP > 0 && (tsorted || nt <= 2 * n) ? reinterpret_cast<KD_GLOBAL uint32_t*>(relv) : nullptr;
         // (walk_lat: a wave takes its next block before this one's walks, and loads the next
         // block's parked distances then, so their wait never includes this block's stores)
         auto grab = [&]() __attribute__((always_inline)) {
@@ -1032,10 +1038,10 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                     t2[q] = j < nt ? tgt[j] : -1;
                 }
             }
-            if constexpr (KD_WCAP > 0) walk_set(std::integral_constant<int, KD_WCAP>{}, t2, jq, ovl, walk_lat, dpair);
+            if (KD_WCAP > 0 && ovl) walk_set(std::integral_constant<int, (KD_WCAP > 0 ? KD_WCAP : 1)>{}, t2, jq, ovl, walk_lat, dpair);
             else walk_set(std::integral_constant<int, KD_MAXD / 4>{}, t2, jq, nullptr, walk_lat, dpair);
         }
-        if constexpr (KD_WCAP > 0) {
+        if (KD_WCAP > 0 && ovl) {
             // second pass: the listed chains, 128 per wave-block, walked in full
             wait_stores();  // (the list, in HBM, visible to every wave)
             __syncthreads();
@@ -1050,8 +1056,13 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                 for (int q = 0; q < KD_WQ; q++) {
                     const int e = e0 + q * 64 + lane;
                     const uint32_t x = e < novf ? ovl[e] : 0xFFFFFFFFu;
-                    t2[q] = e < novf ? (int)(x & 0xFFFFu) : -1;
-                    jq[q] = e < novf ? (int)(x >> 16) : -1;
+                    if (tsorted) {
+                        t2[q] = e < novf ? (int)(x & 0xFFFFu) : -1;
+                        jq[q] = e < novf ? (int)(x >> 16) : -1;
+                    } else {
+                        jq[q] = e < novf ? (int)x : -1;
+                        t2[q] = e < novf ? tgt[x] : -1;
+                    }
                 }
                 walk_set(std::integral_constant<int, KD_MAXD / 4>{}, t2, jq, nullptr, false, 0u);
             }

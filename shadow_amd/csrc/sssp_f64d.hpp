@@ -71,6 +71,7 @@ struct KFSmall {
     int qtail;     // ring entries queued (mod n); phase B: hub list length
     int rhead;     // slices of the round taken
     int flag;
+    int pflag[3];  // level passes: pass r raises slot r % 3 and clears slot (r + 1) % 3
     int ovf;       // a push of this round found no free ring slot (the ring is dropped after it); 256-thread
                    // workgroups: bit p for a round of parity p
     unsigned long long wmark[B / 64][4];  // per wave: start marks of a trip's four windows
@@ -185,7 +186,7 @@ __device__ __attribute__((always_inline)) int kfh_levels(int n, int s, int tid, 
         const int v = tid + k * B;
         if (v < n && relv[v] == -1.0) rem |= 1ull << k;
     }
-    if (tid == 0) sm->flag = 0;
+    if (tid < 3) sm->pflag[tid] = 0;
     __syncthreads();
     for (int pass = 1;; pass++) {
         int prog = 0;
@@ -211,11 +212,12 @@ __device__ __attribute__((always_inline)) int kfh_levels(int n, int s, int tid, 
                     prog = 1;
                 }
         }
-        if (__any(prog) && lane == 0) sm->flag = 1;
+        // (parity-indexed: the slot cleared here was last read before the previous barrier,
+        // so no wave of the next pass can have its raise overwritten)
+        if (__any(prog) && lane == 0) sm->pflag[pass % 3] = 1;
+        if (tid == 0) sm->pflag[(pass + 1) % 3] = 0;
         __syncthreads();
-        const int again = sm->flag;
-        __syncthreads();
-        if (tid == 0) sm->flag = 0;
+        const int again = sm->pflag[pass % 3];
         if (!again) return pass;
     }
 }
@@ -360,7 +362,8 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
             const int qn = (int)(qend - qhead);
             __syncthreads();  // every wave has read the round's end before any wave queues more
             // (the other parity's flag was read by every thread before this barrier)
-            if (B < 1024 && tid == 0) sm->ovf &= ~(1 << (rpar ^ 1));
+            // (an atomic and: waves already in this round may be setting this parity's bit)
+            if (B < 1024 && tid == 0) atomicAnd(&sm->ovf, ~(1 << (rpar ^ 1)));
             // waves pull 64-entry slices of the round's entries (no block barrier inside a
             // round); a slice's arcs are spread over its lanes, 4 positions per lane and trip,
             // owners by a binary search over the slice's lane offsets (ds_bpermute), the 8
@@ -665,9 +668,9 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                 if (relv[v] == -1.0) rem |= 1u << k;
             }
         }
-        if (tid == 0) sm->flag = 0;
+        if (tid < 3) sm->pflag[tid] = 0;
         __syncthreads();
-        for (;;) {
+        for (int pass = 1;; pass++) {
             int prog = 0;
 #pragma unroll
             for (int k0 = 0; k0 < 16; k0 += 8) {
@@ -687,11 +690,11 @@ __global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __re
                         prog = 1;
                     }
             }
-            if (__any(prog) && lane == 0) sm->flag = 1;
+            // (parity-indexed flags, as kfh_levels: one barrier per pass, no lost raise)
+            if (__any(prog) && lane == 0) sm->pflag[pass % 3] = 1;
+            if (tid == 0) sm->pflag[(pass + 1) % 3] = 0;
             __syncthreads();
-            const int again = sm->flag;
-            __syncthreads();  // every thread has read the flag before it is cleared
-            if (tid == 0) sm->flag = 0;
+            const int again = sm->pflag[pass % 3];
             KF_COUNT(7);
             if (!again) break;
         }

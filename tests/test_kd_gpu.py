@@ -109,3 +109,25 @@ def test_kd_sources_subset(oracle_mod, kd, cfg):
     olat, orel, _, _ = og.source_rows(S, T, oracle_mod.TIE_MINKEY)
     assert np.array_equal(lat, olat)
     assert np.array_equal(rel, orel)
+
+
+@pytest.mark.parametrize("nt", [1000, 70000])
+def test_kd_unsorted_duplicate_targets(oracle_mod, kd, nt):
+    """A caller's target list that is unsorted and repeats vertices: on the
+    chain graph most chains outlive the capped first walk and go through the second pass's
+    list.  nt = 1000 (<= 2n) lists them by 32-bit position; nt = 70000 (> 2n, and past
+    the 16 bits the sorted list's entries spend on a position) walks uncapped in one pass."""
+    from shadow_amd import route
+    g = _chain(600, 41)
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 4
+    og = oracle_mod.OracleGraph(g)
+    rng = np.random.default_rng(nt)
+    T = rng.integers(0, g.n, size=nt).astype(np.int32)
+    S = np.array([0, 299, 599, 17], np.int32)
+    lat, rel, mn = eng.rows(S, T, dispatch=False)
+    allv = np.arange(g.n, dtype=np.int32)
+    olat, orel, _, _ = og.source_rows(S, allv, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat[:, T])
+    assert np.array_equal(rel, orel[:, T])
+    assert np.array_equal(mn, olat[:, T].min(axis=1))

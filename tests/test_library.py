@@ -59,3 +59,30 @@ def test_front_end_exports():
     lib = ctypes.CDLL(topology.LIB_PATH)
     for sym in declared:
         assert hasattr(lib, sym), sym
+
+
+def _dyn_exports(path, prefix):
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return sorted({ln.split()[-1] for ln in out.splitlines() if ln.split() and ln.split()[-1].startswith(prefix)})
+
+
+def test_cmake_hip_target(tmp_path):
+    """integration/CMakeLists.txt (enable_language(HIP), CMAKE_HIP_ARCHITECTURES gfx950) the
+    way Shadow's build would take it (reference src/main/CMakeLists.txt:103-108): configure
+    and build out of tree; the engine carries a gfx950 code object and exports exactly the
+    C-ABI of include/shd_route.h, the front end that of include/shd_topology.h."""
+    import shutil
+    import subprocess
+    from shadow_amd import route, topology
+    if not shutil.which("cmake") or not os.path.exists("/opt/rocm/lib/llvm/bin/clang++"):
+        pytest.skip("cmake or the ROCm clang is not installed")
+    b = tmp_path / "cmake"
+    subprocess.run(["cmake", "-S", os.path.join(ROOT, "integration"), "-B", str(b)], check=True,
+                   capture_output=True)
+    subprocess.run(["cmake", "--build", str(b), "-j8"], check=True, capture_output=True)
+    eng, front = str(b / "libshd_route.so"), str(b / "libshd_topology.so")
+    assert _dyn_exports(eng, "shd_route_") == sorted(route.EXPORTS)
+    assert _dyn_exports(front, "shd_") == sorted(topology.EXPORTS)
+    assert b"gfx950" in open(eng, "rb").read()
+    assert os.path.exists(b / "glue_test") or not os.path.exists("/opt/conda/lib/libglib-2.0.so")

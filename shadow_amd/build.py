@@ -46,8 +46,7 @@ def needs_build() -> bool:
 
 
 def build_diag(verbose: bool = False) -> str:
-    """Diagnostic build with per-phase s_memtime stamps (tools/stamps.py) and the retired K16
-    kernel (SHD_ROUTE_KERNEL=k16); never shipped."""
+    """Diagnostic build with per-phase s_memtime stamps (tools/stamps.py); never shipped."""
     out = os.path.join(HERE, "libshd_route_diag.so")
     cmd = [HIPCC, *FLAGS, "-DSHD_STAMPS", "-DSHD_DIAG", "-o", out, *SOURCES]
     if verbose:

@@ -17,9 +17,6 @@
 #include "sssp_k32.hpp"
 #include "sssp_batch.hpp"
 #include "path_attr.hpp"
-#ifdef SHD_DIAG
-#include "sssp_k16.hpp"  // K16: superseded by KD, kept for the diagnostic build only
-#endif
 #include "sssp_delta.hpp"
 #include "direct_fw.hpp"
 #include "fw.hpp"
@@ -117,14 +114,13 @@ struct shd_route {
     double* d_kbf_rtab = nullptr;     // distinct reliabilities
     uint32_t* d_keys = nullptr;     // key rows scratch (ns x n u32), grown on demand
     size_t keys_cap = 0;
-    // K16 large-graph kernel (sssp_k16.hpp)
-    int k16 = 0, k16_slots = 0;
-    size_t k16_lds = 0, k16_stride = 0;
-    uint32_t* d_k16_oarc = nullptr;
-    char* d_k16_ws = nullptr;
     // KD delta-stepping kernel (sssp_delta.hpp)
     int kd = 0, kd_block = 1024, kd_slots = 0, kd_delta = 1, kd_qcap = 0;
     size_t kd_lds = 0, kd_stride = 0;
+    // the planner's unseeded hub rows on 256-thread contexts (C3): 1024-thread workgroups,
+    // one row per CU, cut the latency of that launch (each row is unseeded and alone)
+    int kd_hub_block = 0, kd_hub_qcap = 0, kd_hub_delta = 1;
+    size_t kd_hub_lds = 0;
     int* d_kd_lstart = nullptr;   // light in-CSR offsets (n+1)
     uint32_t* d_kd_orec = nullptr;  // out-arc records v | w << 16
     uint16_t* d_kd_oridx = nullptr; // rtab index per out-arc
@@ -152,7 +148,7 @@ struct shd_route {
     long long lm_rs = 0;
     uint16_t* d_lm_drow = nullptr;  // the landmark rows in the row-store format (device)
     uint32_t* d_lm_prow = nullptr;
-    int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 3 K16, 4 KD, 5 KF
+    int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 4 KD, 5 KF (3: the retired K16)
     // KF (fractional latencies, LDS-resident f64 delta-stepping)
     int kf_block = 0, kf_slots = 0;
     size_t kf_lds = 0;
@@ -395,34 +391,13 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)AL.total));
         if (rc) return rc;
     }
-    // packed in-arcs (u << 16 | w), rows sorted by (-w, u, eid): KB and K16
+    // packed in-arcs (u << 16 | w), rows sorted by (-w, u, eid): KB
     {
         std::vector<uint32_t> packed(((size_t)c->nnz + 3) / 4 * 4, 0u);
         for (int q = 0; q < c->nnz; q++) packed[q] = ((uint32_t)cin[q] << 16) | (uint32_t)w[order[q]];
         rc = upload(c, &c->d_kb_arc, packed);
         if (rc) return rc;
     }
-#ifdef SHD_DIAG
-    // K16: u16 distances in LDS, one 1024-thread workgroup per source
-    const bool want_k16 = force && !strcmp(force, "k16");
-    {
-        std::vector<uint32_t> oarc(c->nnz);
-        for (int a = 0; a < c->nnz; a++) oarc[a] = ((uint32_t)col[a] << 16) | (uint32_t)w[a];
-        rc = upload(c, &c->d_k16_oarc, oarc);
-        if (rc) return rc;
-    }
-    if (want_k16 && k16_lds_bytes(n) <= kLdsBudget) {
-        c->k16_stride = k16_ws_stride(n);
-        c->k16_slots = 256;  // one 1024-thread workgroup per CU
-        if (hipMalloc((void**)&c->d_k16_ws, c->k16_stride * (size_t)c->k16_slots) != hipSuccess) return SHD_ROUTE_ENOMEM;
-        c->allocs.push_back(c->d_k16_ws);
-        c->k16_lds = k16_lds_bytes(n);
-        rc = hip_check(hipFuncSetAttribute((const void*)sssp_k16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)c->k16_lds));
-        if (rc) return rc;
-        c->k16 = 1;
-    }
-#endif
     // KD delta-stepping: bucket width ~ the 12th percentile of arc latencies (>= 1), so
     // ~12% of arcs are light; light in-arcs are the tail of each (-w)-sorted in-row
     const bool want_kd = !force || !strcmp(force, "kd") || !strcmp(force, "auto");
@@ -548,6 +523,25 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 }
                 if (rc) return rc;
                 c->kd = 1; c->kd_block = blk; c->kd_lds = lds; c->kd_delta = delta; c->kd_qcap = qcap;
+                if (blk < 1024 && !getenv("SHD_ROUTE_DELTA") && !getenv("SHD_ROUTE_QCAP")) {
+                    // hub rows in 1024-thread workgroups: that block's queue and bucket width
+                    const size_t hb = kd_lds_bytes<1024>(n, 0);
+                    if (hb + 2 * 512 <= kLdsBudget) {
+                        const int hq = (int)std::min<size_t>((size_t)n, (kLdsBudget - hb - 64) / 2) & ~7;
+                        const size_t hl = kd_lds_bytes<1024>(n, hq);
+                        std::vector<int> ws2(c->nnz);
+                        for (int a = 0; a < c->nnz; a++) ws2[a] = (int)w[a];
+                        const size_t k12 = (size_t)c->nnz * 12 / 100;
+                        std::nth_element(ws2.begin(), ws2.begin() + k12, ws2.end());
+                        if (hl <= kLdsBudget &&
+                            hipFuncSetAttribute((const void*)kd_plan_rows_kernel<1024>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)hl) == hipSuccess) {
+                            c->kd_hub_block = 1024; c->kd_hub_qcap = hq; c->kd_hub_lds = hl;
+                            c->kd_hub_delta = std::max(1, ws2[k12]);
+                        }
+                    }
+                    if (const char* e = getenv("SHD_ROUTE_HUB1024")) if (atoi(e) == 0) c->kd_hub_block = 0;
+                }
                 c->kd_walk = kd_dispatch(blk, [&](auto B) { return kd_walk_fits<decltype(B)::value>(n, qcap, c->kd_nrtab); }) ? 1 : 0;
                 if (const char* e = getenv("SHD_ROUTE_KDWALK")) c->kd_walk = c->kd_walk && atoi(e) != 0;
             }
@@ -660,7 +654,7 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
             if (const char* e = getenv("SHD_ROUTE_KBGRID")) c->kb_grid_cap = std::max(1, atoi(e));
         }
     }
-    c->sel = c->kb ? 2 : c->kd ? 4 : c->k32 ? 1 : c->k16 ? 3 : 0;  // KB (C2-class), else KD (C3/C4-class)
+    c->sel = c->kb ? 2 : c->kd ? 4 : c->k32 ? 1 : 0;  // KB (C2-class), else KD (C3/C4-class)
     return SHD_ROUTE_OK;
 }
 
@@ -677,6 +671,8 @@ DevDelta kd_args(const shd_route* c) {
 #ifdef SHD_STAMPS
     if (const char* e = getenv("SHD_ROUTE_DFLAGS")) k.dflags = atoi(e);
 #endif
+    k.seed_drop = 0;
+    if (const char* e = getenv("SHD_ROUTE_SEEDDROP")) k.seed_drop = atoi(e) & ~1;
 
     k.jobs = nullptr; k.drow = nullptr; k.drow_out = nullptr; k.prow = nullptr; k.rstride = 0; k.evcap = c->n;
     k.done = nullptr;
@@ -690,15 +686,19 @@ DevDelta kd_args(const shd_route* c) {
 // one KD launch of ns sources (k.jobs: planned jobs, else d_src); `next` is zeroed
 int kd_launch(shd_route* c, DevDelta k, int* next, const int32_t* d_src, int ns, const int32_t* d_tgt, int nt,
               int64_t ld, double* d_lat, double* d_rel, double* d_row_min, hipStream_t st, bool planner = false,
-              char* ws = nullptr, int max_grid = 0) {
+              char* ws = nullptr, int max_grid = 0, bool hub = false) {
     if (ns <= 0) return SHD_ROUTE_OK;
     k.next = next;
     if (!ws) ws = c->d_kd_ws;
     const int grid = std::min(ns, max_grid > 0 ? std::min(max_grid, c->kd_slots) : c->kd_slots);
-    kd_dispatch(c->kd_block, [&](auto B) {
+    // (hub: the planner's rows in 1024-thread workgroups where the context's are smaller)
+    const bool big = hub && planner && c->kd_hub_block > 0;
+    size_t lds = c->kd_lds;
+    if (big) { k.rc = c->kd_hub_qcap; k.delta = c->kd_hub_delta; lds = c->kd_hub_lds; }
+    kd_dispatch(big ? c->kd_hub_block : c->kd_block, [&](auto B) {
         constexpr int b = decltype(B)::value;
         if (planner)
-            hipLaunchKernelGGL(kd_plan_rows_kernel<b>, dim3(grid), dim3(b), c->kd_lds, st, k, d_src, ns, d_tgt,
+            hipLaunchKernelGGL(kd_plan_rows_kernel<b>, dim3(grid), dim3(b), lds, st, k, d_src, ns, d_tgt,
                                nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, ws, c->kd_stride);
         else
             hipLaunchKernelGGL(sssp_delta_kernel<b>, dim3(grid), dim3(b), c->kd_lds, st, k, d_src, ns, d_tgt,
@@ -1043,17 +1043,6 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         if (hipMemsetAsync(c->d_kd_next, 0, sizeof(int), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
         return kd_launch(c, k, c->d_kd_next, d_src, ns, d_tgt, nt, ld, d_lat, d_rel, d_row_min, st);
     }
-#ifdef SHD_DIAG
-    if (c->sel == 3 && !(dispatch && c->prefer_direct)) {
-        DevK16 k;
-        k.n = c->n; k.bound = c->k32_bound; k.row = c->d_row; k.oarc = c->d_k16_oarc; k.row_in = c->d_k32_row_in;
-        k.iarc = c->d_kb_arc; k.r_in = c->d_k32_r_in; k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r;
-        const int grid = std::min(ns, c->k16_slots);
-        hipLaunchKernelGGL(sssp_k16_kernel, dim3(grid), dim3(K16_BLOCK), c->k16_lds, st, k, d_src, ns, d_tgt, nt,
-                           (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_k16_ws, c->k16_stride);
-        return hip_check(hipGetLastError());
-    }
-#endif
     if (c->sel == 1 && !(dispatch && c->prefer_direct)) {
         DevK32 k;
         k.n = c->n; k.bound = c->k32_bound; k.row = c->d_row; k.arc = c->d_arc; k.row_in = c->d_k32_row_in;
@@ -1124,13 +1113,63 @@ namespace {
 // two-hop rows s -> x -> u (deg x <= hop_deg) by (w(s,x) + w(x,u) + closeness(u), u, record).
 // Arcs from the packed out-records (u | w << 16 | ridx << 24).  Entries [0, m) are
 // neighbour seeds, [m, m + nh) two-hop seeds (w = w(s,x) + w(x,u), record (x,u)).
+// Up to PC_CAND neighbour candidates are listed in order (ncand of them asked for), so
+// that the sequential pass, whose usable set is a subset of `avail` (the seed-chain depth
+// cap), finds the exact top-kseeds usable ones in the list instead of rescanning the CSR
+// row on the host (C3: 928 host recomputations, ~2 ms of the 4.1 ms plan).
+constexpr int PC_CAND = 6;
 struct PlanChoice {
     int m, nh;
-    int u[3], w[3];
-    uint32_t rec[3];
-    int pad;
+    int u[PC_CAND], w[PC_CAND];
+    uint32_t rec[PC_CAND];
+    int pad[2];
 };
-static_assert(KD_SEEDS <= 3, "PlanChoice holds three seeds");
+static_assert(KD_SEEDS <= 3 && 2 * KD_SEEDS <= PC_CAND, "PlanChoice holds the candidates");
+
+// A root's landmark seeds on the device (shd_route_plan_create): one wave per root row s, the
+// host rule -- the klm landmarks nearest s by (d_L(s), landmark index) (undirected graphs:
+// d_L(s) = d(s, L)), each with the record of L's own vertex in s's tree: the last arc (x, L)
+// of the s -> L path in L's tree, found by walking L's parent records up from s.
+struct LmChoice {
+    int m;
+    int l[3], d[3];
+    uint32_t rec[3];
+    int pad[2];
+};
+__global__ void plan_landmark_kernel(const uint16_t* __restrict__ drow, const uint32_t* __restrict__ prow, long long rs,
+                                     const int* __restrict__ lmv, int nland, const int* __restrict__ srcq, int nq, int klm,
+                                     int n, LmChoice* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (q >= nq) return;  // the whole wave
+    const int s = srcq[q];
+    LmChoice o;
+    o.m = 0; o.pad[0] = o.pad[1] = 0;
+    for (int k = 0; k < 3; k++) { o.l[k] = 0; o.d[k] = 0; o.rec[k] = 0u; }
+    uint32_t prev = 0u;  // picks come in increasing (d, l) order: the next one is past prev
+    for (int k = 0; k < klm && k < 3; k++) {
+        uint32_t best = 0xFFFFFFFFu;
+        for (int l = lane; l < nland; l += 64) {
+            const uint32_t d = drow[(long long)l * rs + s];
+            const uint32_t key = (d << 16) | (uint32_t)l;
+            if (d != 0xFFFFu && (k == 0 || key > prev) && key < best) best = key;
+        }
+        for (int off = 32; off > 0; off >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, off));
+        if (best == 0xFFFFFFFFu) break;
+        prev = best;
+        const int l = (int)(best & 0xFFFFu), L = lmv[l];
+        uint32_t rec = KD_SRC_MARK;
+        if (L != s) {
+            const uint32_t* lp = prow + (long long)l * rs;
+            int x = s;
+            for (int hop = 0; hop < n && (int)(lp[x] & 0xFFFFu) != L; hop++) x = (int)(lp[x] & 0xFFFFu);
+            rec = (uint32_t)x | (lp[x] & 0xFFFF0000u);
+        }
+        o.l[k] = l; o.d[k] = (int)(best >> 16); o.rec[k] = rec;
+        o.m = k + 1;
+    }
+    if (lane == 0) out[q] = o;
+}
 
 // lexicographic minimum of (x, u, t) over the wave (t: a tie-breaking key, arc or record)
 __device__ inline void wave_min3(double& x, int& u, uint32_t& t) {
@@ -1148,22 +1187,31 @@ __device__ inline void wave_min3(double& x, int& u, uint32_t& t) {
 __global__ void plan_choice_kernel(const int* __restrict__ row, const uint32_t* __restrict__ orec,
                                    const double* __restrict__ close, const int* __restrict__ rk,
                                    const uint8_t* __restrict__ avail, const int* __restrict__ srcq, int nq, int kseeds,
-                                   int two_hop, int hop_deg, double alpha, PlanChoice* __restrict__ out) {
+                                   int two_hop, int hop_deg, double alpha, int ncand, PlanChoice* __restrict__ out) {
     const int lane = threadIdx.x & 63;
     const int q = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (q >= nq) return;  // the whole wave
     const int s = srcq[q], rks = rk[s], a0 = row[s], a1 = row[s + 1];
-    int su[3] = {-1, -1, -1}, sw[3] = {0, 0, 0};
-    uint32_t sr[3] = {0u, 0u, 0u};
+    int su[PC_CAND], sw[PC_CAND];
+    uint32_t sr[PC_CAND];
+#pragma unroll
+    for (int k = 0; k < PC_CAND; k++) { su[k] = -1; sw[k] = 0; sr[k] = 0u; }
+    auto picked = [&](int u) {
+        bool p = false;
+#pragma unroll
+        for (int k = 0; k < PC_CAND; k++) p = p || u == su[k];
+        return p;
+    };
+    ncand = max(kseeds, min(ncand, PC_CAND));
     int m = 0;
-    for (; m < kseeds; m++) {
+    for (; m < ncand; m++) {
         double bx = INFINITY;
         int bu = INT_MAX;
         uint32_t ba = UINT_MAX;
         for (int a = a0 + lane; a < a1; a += 64) {
             const uint32_t r = orec[a];
             const int u = (int)(r & 0xFFFFu);
-            if (u == s || u == su[0] || u == su[1] || u == su[2] || !avail[u] || rk[u] >= rks) continue;
+            if (u == s || picked(u) || !avail[u] || rk[u] >= rks) continue;
             const double x = (double)((r >> 16) & 0xFFu) + alpha * close[u];
             if (x < bx || (x == bx && (u < bu || (u == bu && (uint32_t)a < ba)))) { bx = x; bu = u; ba = (uint32_t)a; }
         }
@@ -1192,7 +1240,7 @@ __global__ void plan_choice_kernel(const int* __restrict__ row, const uint32_t* 
                     const uint32_t rb = orec[b];
                     const int u = (int)(rb & 0xFFFFu);
                     if (u == s || u == x || rk[u] >= rks || !avail[u]) continue;
-                    if (u == su[0] || u == su[1] || u == su[2] || u == hu[0] || u == hu[1] || u == hu[2]) continue;
+                    if (picked(u) || u == hu[0] || u == hu[1] || u == hu[2]) continue;
                     const int wb = (int)((rb >> 16) & 0xFFu);
                     const double cost = (double)wa + (double)wb + close[u];
                     const uint32_t rec = (uint32_t)x | ((rb >> 24) << 16) | ((uint32_t)wb << 24);
@@ -1216,8 +1264,9 @@ __global__ void plan_choice_kernel(const int* __restrict__ row, const uint32_t* 
     }
     if (lane == 0) {
         PlanChoice o;
-        o.m = m; o.nh = nh; o.pad = 0;
-        for (int k = 0; k < 3; k++) {
+        o.m = m; o.nh = nh;
+        o.pad[0] = o.pad[1] = 0;
+        for (int k = 0; k < PC_CAND; k++) {
             const bool v = k < m + nh;
             o.u[k] = v ? su[k] : 0; o.w[k] = v ? sw[k] : 0; o.rec[k] = v ? sr[k] : 0u;
         }
@@ -1388,6 +1437,10 @@ struct shd_route_plan {
 
 namespace {
 
+// landmark-only plans: at most this many rows per workgroup slot, and their landmark count
+constexpr double PLAN_LMALL_RPS = 1.5;
+constexpr int PLAN_LMALL_COUNT = 512;
+
 // host threads of a plan (the box's CPU quota is 16)
 int plan_threads() {
     int nth = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
@@ -1408,7 +1461,7 @@ HostPool* host_pool() {
 // is copied back into d_out / p_out.  Blocks: the planner runs once per context, before any
 // planned launch.
 int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, DevBuf& dp, std::vector<uint16_t>& hd,
-                      std::vector<uint32_t>& hp) {
+                      int ncopy) {
     const int k = (int)verts.size(), n = c->n;
     if (k == 0) return SHD_ROUTE_OK;
     const auto h0 = std::chrono::steady_clock::now();
@@ -1420,9 +1473,11 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, D
         std::memset(&jobs[q], 0, sizeof(KDJob));
         jobs[q].row = -1; jobs[q].s = verts[q]; jobs[q].store = q; jobs[q].nseed = 0;
     }
-    // the launch's own per-workgroup scratch (at most 64 workgroups): the context's is left to
-    // its rows launches, so none of those can share it even if one is still in flight
-    const int grid = std::min(k, 64);
+    // the launch's own per-workgroup scratch (at most 256 workgroups, one per CU: each row is
+    // unseeded, so k rows on fewer workgroups would take k / grid row latencies): the
+    // context's is left to its rows launches, so none of those can share it even if one is
+    // still in flight
+    const int grid = std::min(k, 256);
     DevBuf dj, dn, dw;
     if (dj.alloc(sizeof(KDJob) * k) || dd.alloc(sizeof(uint16_t) * (size_t)rs * k) ||
         dp.alloc(sizeof(uint32_t) * (size_t)rs * k) || dn.alloc(sizeof(int) * (1 + (size_t)k)) ||
@@ -1441,15 +1496,17 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, D
     g.drow = (const uint16_t*)dd.p; g.drow_out = (uint16_t*)dd.p; g.prow = (uint32_t*)dp.p; g.rstride = rs;
     g.done = (int*)dn.p + 1;
     if ((rc = kd_launch(c, g, (int*)dn.p, nullptr, k, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, true,
-                        (char*)dw.p, grid)))
+                        (char*)dw.p, grid, true)))
         return rc;
     if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
     if ((rc = take_err(c))) return rc;
     h_launch = hs();
-    hd.resize((size_t)rs * k);
-    hp.resize((size_t)rs * k);
-    if (hipMemcpy(hd.data(), dd.p, sizeof(uint16_t) * hd.size(), hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(hp.data(), dp.p, sizeof(uint32_t) * hp.size(), hipMemcpyDeviceToHost) != hipSuccess)
+    // only the rows the host reads (the closeness rows' distances): the landmark rows stay on
+    // the device, where the plan's landmark-seed kernel reads them (copying 512 rows of C3 to
+    // pageable memory took 6 ms); ensure_lm_host copies them for the host fallback
+    ncopy = std::min(ncopy, k);
+    hd.resize((size_t)rs * ncopy);
+    if (ncopy && hipMemcpy(hd.data(), dd.p, sizeof(uint16_t) * hd.size(), hipMemcpyDeviceToHost) != hipSuccess)
         return SHD_ROUTE_EDEVICE;
     h_copy = hs();
     if (getenv("SHD_ROUTE_PLAN_DEBUG"))
@@ -1475,11 +1532,10 @@ int ensure_hub_rows(shd_route* c, int k) {
     });
     std::vector<int> lv(ord.begin(), ord.begin() + k);
     std::vector<uint16_t> hd;
-    std::vector<uint32_t> hp;
     DevBuf dd, dp;
-    int rc = device_store_rows(c, lv, dd, dp, hd, hp);
-    if (rc) return rc;
     const int L = std::min(k, 16);
+    int rc = device_store_rows(c, lv, dd, dp, hd, L);
+    if (rc) return rc;
     const long long rs = kd_row_stride(n);
     c->close.assign(n, 0.0);
     for (int v = 0; v < n; v++) {
@@ -1495,12 +1551,26 @@ int ensure_hub_rows(shd_route* c, int k) {
     c->d_lm_drow = (uint16_t*)dd.p; dd.p = nullptr;
     c->d_lm_prow = (uint32_t*)dp.p; dp.p = nullptr;
     c->lm_v = lv;
-    c->lm_hd = std::move(hd);
-    c->lm_hp = std::move(hp);
+    c->lm_hd.clear();  // (host copies on demand: ensure_lm_host)
+    c->lm_hp.clear();
     c->lm_rs = rs;
     return SHD_ROUTE_OK;
 }
 int ensure_landmarks(shd_route* c, int k) { return ensure_hub_rows(c, k); }
+
+// the landmark rows on the host (the plan's host fallback for landmark seeds)
+int ensure_lm_host(shd_route* c) {
+    const size_t cnt = (size_t)c->lm_rs * c->lm_v.size();
+    if (c->lm_hd.size() == cnt && c->lm_hp.size() == cnt) return SHD_ROUTE_OK;
+    c->lm_hd.resize(cnt);
+    c->lm_hp.resize(cnt);
+    if (hipMemcpy(c->lm_hd.data(), c->d_lm_drow, sizeof(uint16_t) * cnt, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(c->lm_hp.data(), c->d_lm_prow, sizeof(uint32_t) * cnt, hipMemcpyDeviceToHost) != hipSuccess) {
+        c->lm_hd.clear(); c->lm_hp.clear();
+        return SHD_ROUTE_EDEVICE;
+    }
+    return SHD_ROUTE_OK;
+}
 
 }  // namespace
 
@@ -1527,6 +1597,24 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     // landmark rows (below): 16 for 1024-thread plans, 64 for 256-thread ones; computed in the
     // same device launch as the closeness rows (ensure_hub_rows)
     int nland = c->multigraph ? 0 : std::min(c->kd_block >= 1024 ? 16 : 64, n);
+    // Landmark-only plans (round 5): when a rank has few rows per workgroup slot, seed chains
+    // make its time a few serial row latencies (C3 8-way: 1.2 rows per slot, 3-4 levels, 28% of
+    // linear); every row then seeds from its 3 nearest of PLAN_LMALL_COUNT landmark rows
+    // instead (all at level 0: no waits, no chains).  Multi-GPU ranks with chains take 256
+    // landmarks for their roots (C4 8-way 9.08 -> 8.77 ms with 3 landmark seeds each; 256 hub
+    // rows cost the plan what 16 do: one unseeded row per CU, in parallel).
+    double lmall_rps = PLAN_LMALL_RPS;
+    if (const char* e = getenv("SHD_ROUTE_LMALL")) lmall_rps = atof(e);
+    // (256-thread contexts, n <= 16384: PLAN_LMALL_COUNT landmarks are >= 3% of the vertices,
+    // and the 3 nearest bound a row better than its neighbour rows: C3 1 GPU 2.51 -> 2.30 ms
+    // with 512, 8-way 1.12 -> 0.65 ms)
+    int lmall_small = 1;
+    if (const char* e = getenv("SHD_ROUTE_LMALL_SMALL")) lmall_small = atoi(e);
+    const bool lm_all = !c->multigraph && c->kd_slots > 0 &&
+                        ((lmall_small && c->kd_block < 1024 && n >= 4 * PLAN_LMALL_COUNT) ||
+                         (double)ns / world <= lmall_rps * (double)c->kd_slots);
+    if (lm_all) nland = std::min(n, PLAN_LMALL_COUNT);
+    else if (world > 1 && !c->multigraph) nland = std::min(n, 256);
     if (const char* e = getenv("SHD_ROUTE_LANDMARKS")) nland = c->multigraph ? 0 : std::max(0, std::min(atoi(e), n));
     if (want) {
         const int rc = ensure_hub_rows(c, nland);
@@ -1599,7 +1687,14 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     };
     // ---- which positions this rank computes: output rows + helper rows ----------------
     std::vector<int> job_pos, job_row;
-    if (!want || world == 1) {
+    if (want && world > 1 && lm_all) {
+        // landmark-only plans seed from no other row: a rank takes every world-th position
+        // (row costs vary with the vertex's place in the graph: a stride spreads them), no
+        // helper rows
+        for (int p = rank; p < ns; p += world) {
+            job_row.push_back((int)P->row_pos.size()); P->row_pos.push_back(p); job_pos.push_back(p);
+        }
+    } else if (!want || world == 1) {
         // a contiguous block of the caller's list (world 1: all of it)
         const int blk = (ns + world - 1) / world, lo = std::min(ns, rank * blk), hi = std::min(ns, lo + blk);
         for (int p = lo; p < hi; p++) { P->row_pos.push_back(p); job_pos.push_back(p); job_row.push_back(p - lo); }
@@ -1633,7 +1728,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             if (dev_forest) {
                 hipLaunchKernelGGL(plan_choice_kernel, dim3((ns + 3) / 4), dim3(256), 0, 0, c->d_row, c->d_kd_orec,
                                    (const double*)dcl.p, (const int*)drk.p, (const uint8_t*)dav.p, (const int*)dsq.p, ns,
-                                   1, 0, 0, alpha, (PlanChoice*)dout.p);
+                                   1, 0, 0, alpha, 1, (PlanChoice*)dout.p);
                 dev_forest = hipGetLastError() == hipSuccess &&
                              hipMemcpy(ho.data(), dout.p, sizeof(PlanChoice) * ns, hipMemcpyDeviceToHost) == hipSuccess;
             }
@@ -1712,12 +1807,14 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // the streamed init of round 3 (round 4: C3 2.74 -> 2.67 ms))
         // (multi-GPU ranks: two; a rank's third candidates are mostly two-hop rows, and the
         // extra init pass costs more than they save: 8-way C4 rank 9.6 vs 9.4 ms with three)
-        int kseeds = std::min(KD_SEEDS, world == 1 ? 3 : 2), nroot_min = c->kd_slots;
+        int kseeds = std::min(KD_SEEDS, world == 1 ? 3 : 2), nroot_min = lm_all && nland > 0 ? nj : c->kd_slots;
         int depth = std::max(8, nj / std::max(1, 2 * c->kd_slots));
         if (const char* e = getenv("SHD_ROUTE_SEEDS")) kseeds = std::max(1, std::min(KD_SEEDS, atoi(e)));
         if (const char* e = getenv("SHD_ROUTE_SEED_ROOTS")) nroot_min = std::max(0, atoi(e));
         if (const char* e = getenv("SHD_ROUTE_SEED_DEPTH")) depth = std::max(1, atoi(e));
-        int klm = kseeds;  // landmark seeds of a root row
+        // landmark seeds of a root row: three (C4 8-way roots 9.08 -> 8.83 ms with 64
+        // landmarks; landmark-only C3 plans 0.79 -> 0.70 ms at 8-way)
+        int klm = KD_SEEDS;
         if (const char* e = getenv("SHD_ROUTE_LMSEEDS")) klm = std::max(1, std::min(KD_SEEDS, atoi(e)));
         // seeds of each job: the kseeds neighbours u (jobs of this rank, smaller rank, level
         // below the cap) with the smallest w(s,u) + closeness(u), i.e. the likely gateways
@@ -1834,6 +1931,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // 8.5-8.9 against 13.2 ms on one box); SHD_ROUTE_GPUCHOICE=0 keeps them on the host
         const double th0 = since();
         bool dev_choice = nchunk > 0 && !(getenv("SHD_ROUTE_GPUCHOICE") && atoi(getenv("SHD_ROUTE_GPUCHOICE")) == 0);
+        std::vector<PlanChoice> dch;  // device candidate lists of the seedable rows, in queue order
         if (dev_choice) {
             auto device_choices = [&]() -> bool {
                 const int nqs = nq - nroot_min;
@@ -1852,18 +1950,12 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                     return false;
                 hipLaunchKernelGGL(plan_choice_kernel, dim3((nqs + 3) / 4), dim3(256), 0, 0, c->d_row, c->d_kd_orec,
                                    (const double*)dcl.p, (const int*)drk.p, (const uint8_t*)dav.p, (const int*)dsq.p, nqs,
-                                   kseeds, two_hop ? 1 : 0, hop_deg, alpha, (PlanChoice*)dout.p);
-                std::vector<PlanChoice> ho(nqs);
+                                   kseeds, two_hop ? 1 : 0, hop_deg, alpha, PC_CAND, (PlanChoice*)dout.p);
+                dch.resize(nqs);
                 if (hipGetLastError() != hipSuccess ||
-                    hipMemcpy(ho.data(), dout.p, sizeof(PlanChoice) * nqs, hipMemcpyDeviceToHost) != hipSuccess)
+                    hipMemcpy(dch.data(), dout.p, sizeof(PlanChoice) * nqs, hipMemcpyDeviceToHost) != hipSuccess) {
+                    dch.clear();
                     return false;
-                for (int i = 0; i < nqs; i++) {
-                    Choice& C = pre[nroot_min + i];
-                    const PlanChoice& o = ho[i];
-                    C.m = o.m;
-                    C.nh = o.nh;
-                    for (int k = 0; k < o.m; k++) { C.u[k] = o.u[k]; C.w[k] = o.w[k]; C.rec[k] = o.rec[k]; }
-                    for (int k = 0; k < o.nh; k++) C.hop[k] = Hop{0.0, o.u[o.m + k], o.w[o.m + k], o.rec[o.m + k]};
                 }
                 return true;
             };
@@ -1872,6 +1964,29 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 nextq.store(nq);
                 for (int k = 0; k < nchunk; k++) chunk_done[k].store(1, std::memory_order_relaxed);
             }
+        }
+        // the roots' landmark seeds on the device (a host loop over the landmark rows took
+        // ~2 us per root: strided distance reads and a parent walk per landmark seed)
+        std::vector<LmChoice> lmc;
+        if (nland > 0 && nroot_min > 0 && c->d_lm_drow &&
+            !(getenv("SHD_ROUTE_GPUCHOICE") && atoi(getenv("SHD_ROUTE_GPUCHOICE")) == 0)) {
+            const int nr0 = std::min(nroot_min, nq);
+            std::vector<int> sq(nr0);
+            for (int i = 0; i < nr0; i++) sq[i] = src[order[i]];
+            std::vector<int> lv(c->lm_v.begin(), c->lm_v.begin() + nland);
+            DevBuf dsq, dlv, dout;
+            bool ok = !dsq.alloc(sizeof(int) * nr0) && !dlv.alloc(sizeof(int) * nland) && !dout.alloc(sizeof(LmChoice) * nr0) &&
+                      hipMemcpy(dsq.p, sq.data(), sizeof(int) * nr0, hipMemcpyHostToDevice) == hipSuccess &&
+                      hipMemcpy(dlv.p, lv.data(), sizeof(int) * nland, hipMemcpyHostToDevice) == hipSuccess;
+            if (ok) {
+                hipLaunchKernelGGL(plan_landmark_kernel, dim3((nr0 + 3) / 4), dim3(256), 0, 0, c->d_lm_drow, c->d_lm_prow,
+                                   (long long)c->lm_rs, (const int*)dlv.p, nland, (const int*)dsq.p, nr0, klm, n,
+                                   (LmChoice*)dout.p);
+                lmc.resize(nr0);
+                ok = hipGetLastError() == hipSuccess &&
+                     hipMemcpy(lmc.data(), dout.p, sizeof(LmChoice) * nr0, hipMemcpyDeviceToHost) == hipSuccess;
+            }
+            if (!ok) lmc.clear();
         }
         HostPool* pool = dev_choice ? nullptr : host_pool();
         std::unique_lock<std::mutex> lease(g_pool_use, std::try_to_lock);
@@ -1892,6 +2007,8 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             pool_wait();
         }
         int nlev = 1, q = 0;
+        int n_direct[KD_SEEDS + 1] = {0}, n_twohop = 0;  // SHD_ROUTE_PLAN_DEBUG: seed kinds
+        std::unique_ptr<KDJob[]> byjob(new KDJob[nj]);
         t_loop0 = since();
         for (int j = 0; j < nj; j++) {
             const int p = job_pos[j], s = src[p];
@@ -1904,7 +2021,30 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             }
             Choice ch;
             ch.m = ch.nh = 0;
-            if (seedable) {
+            if (seedable && dev_choice) {
+                // the first kseeds usable entries of the device's ordered candidate list are the
+                // host rule's choice over the usable rows, when the list held kseeds usable ones
+                // or every available neighbour (o.m < PC_CAND); a two-hop fill stands when every
+                // listed neighbour was usable (same exclusions, same count) and so are its picks
+                const PlanChoice& o = dch[qi - nroot_min];
+                int got = 0;
+                bool direct_all = true;
+                for (int k = 0; k < o.m && got < kseeds; k++) {
+                    if (fl[o.u[k]] >= 0) { ch.u[got] = o.u[k]; ch.w[got] = o.w[k]; ch.rec[got] = o.rec[k]; got++; }
+                    else direct_all = false;
+                }
+                ch.m = got;
+                bool exact = got == kseeds || o.m < PC_CAND;
+                if (exact && got < kseeds && two_hop) {
+                    bool hop_ok = o.m < kseeds && direct_all;
+                    for (int k = 0; k < o.nh && hop_ok; k++) hop_ok = fl[o.u[o.m + k]] >= 0;
+                    if (hop_ok) {
+                        ch.nh = o.nh;
+                        for (int k = 0; k < o.nh; k++) ch.hop[k] = Hop{0.0, o.u[o.m + k], o.w[o.m + k], o.rec[o.m + k]};
+                    } else exact = false;
+                }
+                if (!exact) { ch.m = ch.nh = 0; choose(p, [&](int u) { return fl[u] >= 0; }, ch); n_recomp++; }
+            } else if (seedable) {
                 bool ok = true;
                 const Choice& pc = pre[qi];
                 for (int k = 0; k < pc.m; k++) ok = ok && fl[pc.u[k]] >= 0;
@@ -1913,7 +2053,15 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 else { choose(p, [&](int u) { return fl[u] >= 0; }, ch); n_recomp++; }
             }
             int m = ch.m;
-            if (!seedable && nland > 0) {
+            if (seedable) { n_direct[std::min(ch.m, KD_SEEDS)]++; if (ch.nh) n_twohop++; }
+            if (!seedable && nland > 0 && qi < (int)lmc.size()) {
+                const LmChoice& o = lmc[qi];
+                for (int k = 0; k < o.m; k++) {
+                    su[j][k] = c->lm_v[o.l[k]]; wr[j][k] = o.d[k]; srec[j][k] = (int)o.rec[k]; lmseed[j][k] = o.l[k];
+                }
+                nsd[j] = o.m;
+            } else if (!seedable && nland > 0) {
+                if (ensure_lm_host(c)) return SHD_ROUTE_EDEVICE;
                 // nearest landmarks by d(s, L) (undirected: d_L(s)), up to klm (default kseeds)
                 std::vector<std::pair<double, int>> lc;
                 for (int l = 0; l < nland; l++) {
@@ -1953,6 +2101,19 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             if (!nsd[j]) P->nroots++;
             nlev = std::max(nlev, lvl[j] + 1);
             if (first[src[p]] == j && lvl[j] + 1 < depth) fl[src[p]] = p;
+            {
+                // the job record, in job order (the schedule below copies it into queue order:
+                // one cache line per job instead of five scattered per-job arrays); its own
+                // store slot and landmark slots (-1 - l: after every kept row's slot) are
+                // final only after this pass
+                KDJob& J = byjob[j];
+                std::memset(&J, 0, sizeof(J));
+                J.row = job_row[j]; J.s = s; J.store = -1; J.nseed = nsd[j];
+                for (int k = 0; k < nsd[j]; k++) {
+                    J.seed[k] = lmseed[j][k] >= 0 ? -1 - lmseed[j][k] : slot[seedjob[j][k]];
+                    J.u[k] = su[j][k]; J.wr[k] = wr[j][k]; J.rec[k] = srec[j][k];
+                }
+            }
         }
         pool_wait();
         t_hop = since() - th0;
@@ -2046,15 +2207,14 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             long long fcur = 0;
             // each job is written into the launch's job array as it is scheduled (queue order)
             jobs.resize(nj);
+            const double t_jobs = since();
             int qi = 0;
             auto emit = [&](int j) {
                 KDJob& J = jobs[qi++];
-                std::memset(&J, 0, sizeof(J));
-                J.row = job_row[j]; J.s = src[job_pos[j]]; J.store = slot[j]; J.nseed = nsd[j];
-                for (int k = 0; k < nsd[j]; k++) {
-                    J.seed[k] = lmseed[j][k] >= 0 ? P->nslots + lmseed[j][k] : slot[seedjob[j][k]];
-                    J.u[k] = su[j][k]; J.wr[k] = wr[j][k]; J.rec[k] = srec[j][k];
-                }
+                J = byjob[j];
+                J.store = slot[j];
+                for (int k = 0; k < J.nseed; k++)
+                    if (J.seed[k] < 0) J.seed[k] = P->nslots + (-1 - J.seed[k]);
             };
             long long cur = -1;
             size_t pos = 0;
@@ -2089,6 +2249,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             }
             t_sched = since();
             if (getenv("SHD_ROUTE_PLAN_DEBUG")) {
+                fprintf(stderr, "  schedule: job array ready %.2f ms (%d jobs, ticks to %lld)\n", 1e3 * t_jobs, nj, cur);
                 int hist[KD_SEEDS + 1] = {0};
                 for (int j = 0; j < nj; j++) hist[nsd[j]]++;
                 fprintf(stderr, "plan world %d rank %d: jobs %d levels %d seeds:", world, rank, nj, nlev);
@@ -2098,6 +2259,12 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                         1e3 * t_close, 1e3 * t_rk, 1e3 * t_order, 1e3 * t_land, 1e3 * t_hop, 1e3 * t_seeds, 1e3 * t_sched);
                 fprintf(stderr, "  seq loop start %.2f (recomputed %d), store thread started %.2f, deps done %.2f\n", 1e3 * t_loop0, n_recomp,
                         1e3 * t_alloc, 1e3 * t_deps);
+                int nlm = 0;
+                for (int j = 0; j < nj; j++) nlm += nsd[j] > 0 && lmseed[j][0] >= 0;
+                fprintf(stderr, "  seed kinds: landmark-seeded roots %d; neighbour-seeded rows by direct seeds:", nlm);
+                for (int k = 0; k <= KD_SEEDS; k++) fprintf(stderr, " %d:%d", k, n_direct[k]);
+                fprintf(stderr, " (with two-hop seeds %d; at most one direct seed: %.1f%% of the other rows)\n", n_twohop,
+                        100.0 * (n_direct[0] + n_direct[1]) / std::max(1, nj - nlm));
             }
         }
         if (store_th.joinable()) store_th.join();

@@ -142,6 +142,8 @@ struct DevDelta {
     int has_vf;                         // some vertex factor other than 1.0 (else every f_v is 1.0 or
                                         // absent, a no-op in every product: vf is not read)
     int dflags;                         // diagnostic builds: 1 = skip the output-row stores
+    int seed_drop;                      // tests (SHD_ROUTE_SEEDDROP): bit q drops seed q >= 1 of every
+                                        // seeded job, as an unready seed is dropped (KD_SEEDSPIN)
     unsigned long long* dbg;            // SHD_STAMPS builds: KD_NACC words per source
     unsigned long long* stats;          // liveness: the longest single wait (s_sleep rounds) of [0] a compute
                                         // wave for writer-ring space, [1] the writer on a reserved record
@@ -193,13 +195,9 @@ struct KDSmall {
     int wnext2, novf;   // phase C capped walks (KD_WCAP): next block of the second pass, chains listed
     KDJob job;          // the current job (kept in LDS: read where needed, not held in
                         // registers across phase A, whose expansion needs all of them)
-    // Pre-init (planned launches, B >= 1024): the next job is taken at the start of this
-    // row's output phases, and while most waves walk this row's paths the last KD_PREW
-    // waves stream the next row's seeds (HBM) into its parent records and a staged D0
+    // planned launches: the next job is taken at the start of this row's output phases
     KDJob njob;         // the next job (valid when njb >= 0)
     int njb;            // its queue index (-1: not taken; the loop takes one as usual)
-    int npre;           // the next row's records and staged D0 are written (set after phase C)
-    int npre_ok;        // pre-init waves that completed
     int wpar;           // which of the two per-workgroup record slices the current row uses
     const KDJob* jobs;  // (the launch's job list, queue counter, row store and flags, for the
     int* qnext;         //  non-inlined output phases)
@@ -208,7 +206,6 @@ struct KDSmall {
     long long rstride;
     int* done;
     uint32_t* wsl[2];   // the two record slices of this workgroup
-    uint16_t* dstage;   // staged D0 of the next row (u16 x (n + 8))
     int ns;
 #ifdef SHD_STAMPS
     unsigned long long acc[KD_NACC];
@@ -256,12 +253,11 @@ struct KDLayout {
     }
 };
 constexpr int KD_MAXD = 32;           // phase C path walk: arcs held in registers
-#ifndef KD_PREW
-#define KD_PREW 0                     // waves pre-initialising the next row during the walk (0: off)
-#endif
 // build-time variants (A/B builds, tools/build_var.sh; the defaults are the shipped kernel:
 // round 4, C4 45.8 -> 44.2 ms with SDIV 8 + WDYN + WCAP 2 against all three off, C3 2.74 ->
-// 2.76 ms; FUSELAT, LATWALK and ICOND measured 44.9-50.1 ms)
+// 2.76 ms; the losing variants -- lat row fused into the parent copy or the walks, records
+// loaded only where a seed attains D0, pre-init of the next row under the walks -- measured
+// 44.9-50.1 ms and were removed in round 5)
 #ifndef KD_SDIV
 #define KD_SDIV 8   // phase A (1024-thread workgroups): a grab takes max(KD_SMIN, queued / KD_SDIV) entries, at most 64 (0: min(64, queued))
 #endif
@@ -274,24 +270,9 @@ constexpr int KD_MAXD = 32;           // phase C path walk: arcs held in registe
 #ifndef KD_WCAP
 #define KD_WCAP 2   // phase C: first-pass walks capped at KD_WCAP blocks of 4 arcs, the rest in a second pass (0: one pass)
 #endif
-static_assert(KD_WCAP == 0 || KD_PREW == 0, "the capped walk's second pass needs every wave");
-#ifndef KD_FUSELAT
-#define KD_FUSELAT 0  // phase C: the lat row written inside the pipelined parent copy (identity target lists)
-#endif
-#ifndef KD_LATWALK
-#define KD_LATWALK 0  // phase C: the lat row written by the walks (distances parked in HBM by the copy)
-#endif
-static_assert(KD_LATWALK == 0 || KD_WDYN != 0, "the walks' lat stores prefetch a wave's next block");
-#ifndef KD_ICOND
-#define KD_ICOND 0  // seeded init: a seed's records loaded only for 4-vertex groups where it attains D0
-#endif
-#ifndef KD_SEEDANY
-#define KD_SEEDANY 0   // with KD_SEEDSPIN: wait for any one seed (not the first) before the bounded polls
-#endif
 #ifndef KD_SEEDSPIN
 #define KD_SEEDSPIN 8  // seeded init: polls (s_sleep 8 each) of a second or third seed's flag before it is dropped (0: wait; round 4: C3 2.68 -> 2.53 ms, C4 44.7 -> 44.4)
 #endif
-constexpr int KD_PRESPIN = 32;        // pre-init: polls of a seed's flag (s_sleep 8 each) before giving up
 constexpr int KD_WQ = 2;              // phase C path walk: targets per thread (4 measured 1% slower at C4: its registers put 39 VGPRs of the output function in callee-saved ranges, saved to scratch and restored around every row; 2: 13)
 constexpr int KD_ONE = 254;           // phase C: rtab slot holding 1.0 (the source's own step)
 constexpr int KD_NAN = 255;           // phase C: rtab slot holding NaN (unreachable vertices)
@@ -303,17 +284,15 @@ constexpr int kd_rr() { return B >= 1024 ? KD_RR : 256; }
 // parent | ridx << 16 (| w << 24, packed arcs) of the parent arc (KD_SRC_MARK for the source)
 // | tie events
 // {p | ridx << 16 | w << 24, v} x n (seeded rows) | a second record slice u32[n + 8] (rows
-// alternate between the two, so the next row's pre-init never writes the records the current
-// row may still read) | staged D0 u16[n + 8].  Seeded rows use relv as u32 keys.
+// alternate between the two).  Seeded rows use relv as u32 keys.
 __host__ __device__ inline size_t kd_ws_stride(int n) {
     return a16(sizeof(double) * n) + a16(sizeof(uint32_t) * (n + 8)) + a16(8 * (size_t)n) + 256 +
-           a16(sizeof(uint32_t) * (n + 8)) + a16(sizeof(uint16_t) * (n + 8));
+           a16(sizeof(uint32_t) * (n + 8));
 }
-// the second record slice and the staged D0 (pre-init), after relv | wpr | events
+// the second record slice, after relv | wpr | events
 __host__ __device__ inline size_t kd_ws_wpr1(int n) {
     return a16(sizeof(double) * n) + a16(sizeof(uint32_t) * (n + 8)) + a16(8 * (size_t)n) + 256;
 }
-__host__ __device__ inline size_t kd_ws_dstage(int n) { return kd_ws_wpr1(n) + a16(sizeof(uint32_t) * (n + 8)); }
 __host__ __device__ inline long long kd_row_stride(int n) { return ((long long)n + 2 + 7) & ~7ll; }
 
 // LDS-only workgroup barrier: outstanding global stores (output rows) stay in flight.
@@ -482,108 +461,6 @@ __device__ inline int kd_next_source(int* ctr, int* slot, int tid, bool all_queu
     return i;
 }
 
-// Pre-init of the next job (sm->njob), by the threads pt = 0 .. PT-1 of the last KD_PREW waves
-// while the other waves walk the current row's paths (LDS-bound; this is HBM-bound): the
-// seeded init's stream (the seeded branch of kd_rows_body) with D0 written to the staged
-// array instead of LDS, the parent records to the next row's own record array (its store
-// slot, or the record slice the current row does not use).  All or nothing: a wave whose
-// seeds are not ready after a short poll leaves it to the next row's own init.
-template <int B>
-__device__ inline void kd_preinit(const int n, const int pt, const int PT, int* __restrict__ err) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    KDSmall* sm = reinterpret_cast<KDSmall*>(smem);
-    const int lane = threadIdx.x & 63;
-    const int nseed = __builtin_amdgcn_readfirstlane(sm->njob.nseed);
-    const int s = __builtin_amdgcn_readfirstlane(sm->njob.s);
-    int* const done = sm->done;
-    int ok = 1;
-    if (lane == 0) {
-        for (int q = 0; q < nseed && ok; q++) {
-            const int sl = sm->njob.seed[q];
-            int spin = 0;
-            while (__hip_atomic_load(&done[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && spin < KD_PRESPIN) {
-                __builtin_amdgcn_s_sleep(8);
-                spin++;
-            }
-            ok = spin < KD_PRESPIN;
-        }
-        if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!__builtin_amdgcn_readfirstlane(ok)) return;
-    const int st = __builtin_amdgcn_readfirstlane(sm->njob.store);
-    uint32_t* const wpr = st >= 0 ? sm->prow + (size_t)st * sm->rstride : sm->wsl[sm->wpar ^ 1];
-    uint16_t* const dstg = sm->dstage;
-    int su[KD_SEEDS];
-    unsigned wsu[KD_SEEDS], rsu[KD_SEEDS];
-    const uint16_t* sdrow[KD_SEEDS];
-    const uint32_t* sprow[KD_SEEDS];
-#pragma unroll
-    for (int q = 0; q < KD_SEEDS; q++) {
-        const int sl = __builtin_amdgcn_readfirstlane(q < nseed ? sm->njob.seed[q] : 0);
-        wsu[q] = (unsigned)__builtin_amdgcn_readfirstlane(q < nseed ? sm->njob.wr[q] : 0) & 0xFFFFu;
-        su[q] = __builtin_amdgcn_readfirstlane(q < nseed ? sm->njob.u[q] : -1);
-        rsu[q] = (unsigned)__builtin_amdgcn_readfirstlane(q < nseed ? sm->njob.rec[q] : 0);
-        sdrow[q] = sm->drow + (size_t)sl * sm->rstride;
-        sprow[q] = sm->prow + (size_t)sl * sm->rstride;
-    }
-    // two groups of 4 vertices per lane and trip, all 4 * KD_SEEDS loads issued first (four
-    // waves alone must keep enough bytes in flight to finish within the walk)
-    auto load = [&](int v0, uint2 (&dq)[KD_SEEDS], uint4 (&pq)[KD_SEEDS]) __attribute__((always_inline)) {
-        const int vl = min(v0, n & ~3);
-#pragma unroll
-        for (int q = 0; q < KD_SEEDS; q++) {
-            if (q < nseed) {
-                const kd_u2 d2 = *(const KD_GLOBAL kd_u2*)(sdrow[q] + vl);
-                const kd_u4 p4 = *(const KD_GLOBAL kd_u4*)(sprow[q] + vl);
-                dq[q] = make_uint2(d2.x, d2.y);
-                pq[q] = make_uint4(p4.x, p4.y, p4.z, p4.w);
-            } else {
-                dq[q] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-                pq[q] = make_uint4(KD_NONE, KD_NONE, KD_NONE, KD_NONE);
-            }
-        }
-    };
-    auto comb = [&](int v0, const uint2 (&dq)[KD_SEEDS], const uint4 (&pq)[KD_SEEDS]) __attribute__((always_inline)) {
-        uint32_t dw[2], rw[4];
-#pragma unroll
-        for (int h = 0; h < 4; h++) {
-            const int v = v0 + h;
-            unsigned dbest = 0xFFFFu, kbest = 0xFFFFFFFFu;
-            uint32_t rbest = KD_NONE;
-#pragma unroll
-            for (int q = 0; q < KD_SEEDS; q++) {
-                const uint32_t d2 = (h < 2) ? dq[q].x : dq[q].y;
-                const unsigned d = (h & 1) ? (d2 >> 16) : (d2 & 0xFFFFu);
-                const unsigned c = q < nseed ? min(0xFFFFu, wsu[q] + d) : 0xFFFFFu;
-                const uint32_t p = kd_comp(pq[q], h);
-                const uint32_t r = v == su[q] ? rsu[q] : p;
-                const uint32_t k = __builtin_amdgcn_perm(~r, r, 0x07010002u);  // (255-w) | p | ridx
-                if (c < dbest || (c == dbest && k < kbest)) { dbest = c; kbest = k; rbest = r; }
-            }
-            if (v >= n) dbest = 0xFFFFu;
-            if (v == s) rbest = KD_SRC_MARK;
-            if (h & 1) dw[h >> 1] |= dbest << 16;
-            else dw[h >> 1] = dbest;
-            rw[h] = rbest;
-        }
-        *(KD_GLOBAL kd_u2*)(dstg + v0) = kd_u2{dw[0], dw[1]};
-        *(KD_GLOBAL kd_u4*)(wpr + v0) = kd_u4{rw[0], rw[1], rw[2], rw[3]};
-    };
-    for (int v0 = 4 * pt; v0 <= n; v0 += 8 * PT) {
-        const int v1 = v0 + 4 * PT;
-        uint2 da[KD_SEEDS], db[KD_SEEDS];
-        uint4 pa[KD_SEEDS], pb[KD_SEEDS];
-        load(v0, da, pa);
-        load(v1, db, pb);
-        comb(v0, da, pa);
-        if (v1 <= n) comb(v1, db, pb);
-    }
-    wait_stores();
-    if (lane == 0) atomicAdd(&sm->npre_ok, 1);
-    (void)err;
-}
-
 // Phases C/D of one row (lat row, parent copy, reliability by walks or level sweeps, rel
 // row, row min), called once per row.  Not inlined, on purpose: see the call site.
 template <int B>
@@ -631,20 +508,7 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
         else { Lv = (double)dist[t]; lmin = fmin(lmin, Lv); }
         return Lv;
     };
-    // fused lat row (KD_FUSELAT, the walk path over an identity target list, i.e. every vertex a
-    // target in order: positions = vertex ids): the lat row goes out inside the parent copy
-    // below, the copy's record loads for the next trip issued before this trip's stores, so
-    // neither waits for the other (one in-order vmcnt per wave)
-    const bool fuse_lat = KD_FUSELAT && !KD_LATWALK && g.walk && rrow && lrow && tsorted && nt == n &&
-                          !(((uintptr_t)lrow >> 3) & 1);
-    // lat row by the walks (KD_LATWALK, same conditions): the parent copy parks the distances
-    // in the HBM slice, and each walk block stores its targets' lat beside their rel, so the
-    // lat row's stores run under the LDS-bound walks instead of before them
-    const bool walk_lat = KD_LATWALK && g.walk && rrow && lrow && tsorted && nt == n && n >= 64 &&
-                          !(((uintptr_t)lrow >> 3) & 1);
-    KD_GLOBAL uint16_t* const dpark = reinterpret_cast<KD_GLOBAL uint16_t*>(relv) + 2 * (size_t)((n + 7) & ~7);
-    if (fuse_lat || walk_lat) {
-    } else if (tsorted) {
+    if (tsorted) {
         // two adjacent vertices per lane: consecutive positions go out as one 16-B store
         const int lpar = (int)(((uintptr_t)lrow >> 3) & 1);
         for (int v = 2 * tid; v < (i >= 0 ? n : 0); v += 2 * B) {
@@ -666,7 +530,7 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
     }
     wait_stores();  // wpr of phase B visible to the whole workgroup
     // planned launches: the next job is taken here (queue order is unchanged: a job is still
-    // taken after every job it seeds from), so the pre-init waves below can stream its seeds
+    // taken after every job it seeds from)
     const bool queued = sm->jobs != nullptr;
     if (tid == 0) {
         sm->deep = 0; sm->rmin = kInfBits; sm->wnext = 0; sm->wnext2 = 0; sm->novf = 0;
@@ -676,7 +540,7 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
     const int njb = queued ? __builtin_amdgcn_readfirstlane(sm->njb) : -1;
     if (tid < 16 && njb >= 0) {
         const int x = njb < sm->ns ? ((const KD_GLOBAL int*)(sm->jobs + njb))[tid] : (tid == 3 ? 0 : -1);
-        reinterpret_cast<int*>(&sm->njob)[tid] = x;  // (past the end: nseed = 0, no pre-init)
+        reinterpret_cast<int*>(&sm->njob)[tid] = x;  // (past the end: nseed = 0)
     }
 
     KD_ACC(18);
@@ -697,21 +561,16 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
         // vertices per trip: C4 takes 4 trips instead of the 7 of one 4-B load per vertex)
         // (wpr rows hold n + 8 records, dist n + 1 entries padded to 16 B: the last group's
         // reads stay inside; its writes past n are dropped)
-        auto copy_trip = [&](const int v0, const kd_u4 (&pr)[4], const bool with_lat) __attribute__((always_inline)) {
+        auto copy_trip = [&](const int v0, const kd_u4 (&pr)[4]) __attribute__((always_inline)) {
             uint2 dv[4];
 #pragma unroll
             for (int q = 0; q < 4; q++) dv[q] = *reinterpret_cast<const uint2*>(dist + min(v0 + q * 4 * B, (n - 1) & ~3));
-            if (walk_lat)  // (the group's 4 distances; pads past n land in the parked array's pad)
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    if (v0 + q * 4 * B < n) *reinterpret_cast<KD_GLOBAL kd_u2*>(dpark + v0 + q * 4 * B) = kd_u2{dv[q].x, dv[q].y};
             // (each thread overwrites only the dist entries it read itself)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int vb = v0 + q * 4 * B;
                 if (vb >= n) continue;
                 uint32_t pw[2] = {0u, 0u}, rw = 0u;
-                double Lq[4];
 #pragma unroll
                 for (int h = 0; h < 4; h++) {
                     const int v = vb + h;
@@ -725,28 +584,12 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                                         : ri == (uint32_t)rone ? (uint32_t)KD_ONE : ri;
                     pw[h >> 1] |= pv << (16 * (h & 1));
                     rw |= rx << (8 * h);
-                    if (with_lat) {  // lat_of(v) from the distance in hand
-                        double Lv = 0.0;
-                        if (v < n) {
-                            if (src_v) {
-                                if (isnan(sw_s)) { raise_err(err, SHD_ROUTE_ENOEDGE); Lv = NAN; }
-                                else { Lv = 0.0 + sw_s; lmin = fmin(lmin, Lv); }
-                            } else if (unr) { raise_err(err, SHD_ROUTE_EUNREACH); Lv = NAN; }
-                            else { Lv = (double)d; lmin = fmin(lmin, Lv); }
-                        }
-                        Lq[h] = Lv;
-                    }
                 }
                 if (vb + 4 <= n) {
-                    if (with_lat && KD_OUT) {
-                        __builtin_nontemporal_store(kd_d2{Lq[0], Lq[1]}, reinterpret_cast<KD_GLOBAL kd_d2*>(lrow + vb));
-                        __builtin_nontemporal_store(kd_d2{Lq[2], Lq[3]}, reinterpret_cast<KD_GLOBAL kd_d2*>(lrow + vb + 2));
-                    }
                     *reinterpret_cast<uint2*>(parv + vb) = make_uint2(pw[0], pw[1]);
                     *reinterpret_cast<uint32_t*>(rixl + vb) = rw;
                 } else {
                     for (int h = 0; h < n - vb; h++) {
-                        if (with_lat && KD_OUT) __builtin_nontemporal_store(Lq[h], lrow + vb + h);
                         parv[vb + h] = (uint16_t)((pw[h >> 1] >> (16 * (h & 1))) & 0xFFFFu);
                         rixl[vb + h] = (uint8_t)((rw >> (8 * h)) & 0xFFu);
                     }
@@ -758,25 +601,11 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
             for (int q = 0; q < 4; q++)
                 pr[q] = *reinterpret_cast<const KD_GLOBAL kd_u4*>(wpr + min(v0 + q * 4 * B, (n - 1) & ~3));
         };
-        if (fuse_lat || walk_lat) {
-            // software-pipelined: trip k + 1's record loads go out before trip k's lat stores
-            kd_u4 pa[4], pb[4];
-            load_trip(4 * tid, pa);
-            for (int v0 = 4 * tid; v0 < n; v0 += 32 * B) {
-                load_trip(v0 + 16 * B, pb);
-                copy_trip(v0, pa, fuse_lat);
-                if (v0 + 16 * B >= n) break;
-                load_trip(v0 + 32 * B, pa);
-                copy_trip(v0 + 16 * B, pb, fuse_lat);
-            }
-        } else {
-            for (int v0 = 4 * tid; v0 < n; v0 += 16 * B) {
-                kd_u4 pr[4];
-                load_trip(v0, pr);
-                copy_trip(v0, pr, false);
-            }
+        for (int v0 = 4 * tid; v0 < n; v0 += 16 * B) {
+            kd_u4 pr[4];
+            load_trip(v0, pr);
+            copy_trip(v0, pr);
         }
-        if (walk_lat) wait_stores();  // the parked distances, visible to every wave's walks
         __syncthreads();
         // Lossless arcs (slot KD_ONE: exactly 1.0) multiply as exact no-ops, so a chain only
         // needs the lossy ones (20% of the arcs on the BASELINE topologies): parv[v] becomes the
@@ -835,17 +664,12 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
         // global load behind the previous group's stores); else over the target list
         const int lim = tsorted ? n : nt;
         const int rpar = (int)(((uintptr_t)rrow >> 3) & 1);
-        // with a seeded next job, the last KD_PREW waves pre-init it (below) and BW threads walk
-        const bool pre = KD_PREW > 0 && B >= 1024 && njb >= 0 && __builtin_amdgcn_readfirstlane(sm->njob.nseed) > 0;
-        const int BW = pre ? B - 64 * KD_PREW : B;
-        if (tid < BW) {
         // one set of KD_WQ chains per thread: walk <= NB blocks of 4 arcs, fold source-first,
         // store.  In a capped first pass (ovl != nullptr) a chain still short of the source
         // after NB blocks is listed in ovl (v | j << 16) instead of stored, and the second pass
         // walks the listed chains again in dense waves: a wave then runs for its deepest
         // ordinary chain, not for the deepest chain of any 128 targets (KD_WCAP)
-        auto walk_set = [&](auto NBC, int (&t2)[KD_WQ], int (&jq)[KD_WQ], KD_GLOBAL uint32_t* ovl, const bool wlat,
-                            const uint32_t dpair) __attribute__((always_inline)) {
+        auto walk_set = [&](auto NBC, int (&t2)[KD_WQ], int (&jq)[KD_WQ], KD_GLOBAL uint32_t* ovl) __attribute__((always_inline)) {
             constexpr int NB = decltype(NBC)::value;
             int cur[KD_WQ];
             uint32_t pk[KD_WQ][NB];
@@ -951,74 +775,27 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                     }
                 }
             }
-            if (wlat) {
-                // lat of this thread's two adjacent targets (identity list: positions = vertices)
-                // from the parked distances, as lat_of computes it
-                double Lq[2];
-#pragma unroll
-                for (int q = 0; q < 2; q++) {
-                    const int t = t2[q];
-                    const unsigned d = (dpair >> (16 * q)) & 0xFFFFu;
-                    double Lv = 0.0;
-                    if (t >= 0) {
-                        if (t == s) {
-                            if (isnan(sw_s)) { raise_err(err, SHD_ROUTE_ENOEDGE); Lv = NAN; }
-                            else { Lv = 0.0 + sw_s; lmin = fmin(lmin, Lv); }
-                        } else if (d == 0xFFFFu) { raise_err(err, SHD_ROUTE_EUNREACH); Lv = NAN; }
-                        else { Lv = (double)d; lmin = fmin(lmin, Lv); }
-                    }
-                    Lq[q] = Lv;
-                }
-                // (positions from t2: a chain listed for the second pass has jq = -1 by now, but
-                // its lat is due here)
-                if (KD_OUT) {
-                    if (t2[0] >= 0 && t2[1] == t2[0] + 1)
-                        __builtin_nontemporal_store(kd_d2{Lq[0], Lq[1]}, reinterpret_cast<KD_GLOBAL kd_d2*>(lrow + t2[0]));
-                    else if (t2[0] >= 0) __builtin_nontemporal_store(Lq[0], lrow + t2[0]);
-                }
-            }
         };
         // blocks of KD_WQ x WB targets: the whole workgroup's threads share a block in turn
         // (static), or each wave takes the next block of KD_WQ x 64 from a counter (wdyn: a
         // wave of shallow chains takes more blocks, no wave waits at the barrier for another)
         constexpr bool wdyn = KD_WDYN != 0;
-        const int WB = wdyn ? 64 : BW;
+        const int WB = wdyn ? 64 : B;
         const int li = wdyn ? lane : tid;  // this thread's place in its block
         // (capped first pass: its list over relv's HBM slice, unused by the walks; the slice
         // holds 2n entries, and a list gets at most one per target position, so a caller's
         // unsorted list longer than 2n (duplicates) walks uncapped in one pass instead)
         KD_GLOBAL uint32_t* const ovl =
             KD_WCAP > 0 && (tsorted || nt <= 2 * n) ? reinterpret_cast<KD_GLOBAL uint32_t*>(relv) : nullptr;
-        // (walk_lat: a wave takes its next block before this one's walks, and loads the next
-        // block's parked distances then, so their wait never includes this block's stores)
         auto grab = [&]() __attribute__((always_inline)) {
             int c = 0;
             if (lane == 0) c = atomicAdd(&sm->wnext, 1);
             return __builtin_amdgcn_readfirstlane(c) * (KD_WQ * 64);
         };
-        auto dload = [&](int jb) __attribute__((always_inline)) {
-            const int v = jb + 2 * lane;
-            return jb < lim && v < n ? *reinterpret_cast<const KD_GLOBAL uint32_t*>(dpark + v) : 0xFFFFFFFFu;
-        };
-        int jnext = 0;
-        uint32_t dnext = 0xFFFFFFFFu;
-        if constexpr (KD_LATWALK != 0) {
-            if (walk_lat) { jnext = grab(); dnext = dload(jnext); }
-        }
         for (int blk = 0;; blk++) {
             int jbase;
-            uint32_t dpair = 0xFFFFFFFFu;
-            if constexpr (wdyn) {
-                if (KD_LATWALK != 0 && walk_lat) {
-                    jbase = jnext;
-                    dpair = dnext;
-                    if (jbase < lim) { jnext = grab(); dnext = dload(jnext); }
-                } else {
-                    jbase = grab();
-                }
-            } else {
-                jbase = blk * (KD_WQ * BW);
-            }
+            if constexpr (wdyn) jbase = grab();
+            else jbase = blk * (KD_WQ * B);
             if (jbase >= lim) break;
             const int j0 = jbase + li;
             // KD_WQ targets per thread: independent parent chains in flight.  A chain that
@@ -1038,8 +815,8 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                     t2[q] = j < nt ? tgt[j] : -1;
                 }
             }
-            if (KD_WCAP > 0 && ovl) walk_set(std::integral_constant<int, (KD_WCAP > 0 ? KD_WCAP : 1)>{}, t2, jq, ovl, walk_lat, dpair);
-            else walk_set(std::integral_constant<int, KD_MAXD / 4>{}, t2, jq, nullptr, walk_lat, dpair);
+            if (KD_WCAP > 0 && ovl) walk_set(std::integral_constant<int, (KD_WCAP > 0 ? KD_WCAP : 1)>{}, t2, jq, ovl);
+            else walk_set(std::integral_constant<int, KD_MAXD / 4>{}, t2, jq, nullptr);
         }
         if (KD_WCAP > 0 && ovl) {
             // second pass: the listed chains, 128 per wave-block, walked in full
@@ -1064,26 +841,16 @@ __device__ __attribute__((noinline)) void kd_output(const int n, const int nw, c
                         t2[q] = e < novf ? tgt[x] : -1;
                     }
                 }
-                walk_set(std::integral_constant<int, KD_MAXD / 4>{}, t2, jq, nullptr, false, 0u);
+                walk_set(std::integral_constant<int, KD_MAXD / 4>{}, t2, jq, nullptr);
             }
         }
 #ifdef SHD_STAMPS
         if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[32] += t_ - kd_t; kd_t = t_; }
 #endif
-        } else if (pre) {
-#ifdef SHD_STAMPS
-            const unsigned long long p0 = __builtin_amdgcn_s_memtime();
-#endif
-            kd_preinit<B>(n, tid - BW, 64 * KD_PREW, err);
-#ifdef SHD_STAMPS
-            if (tid == BW) sm->acc[34] += __builtin_amdgcn_s_memtime() - p0;
-#endif
-        }
         __syncthreads();
 #ifdef SHD_STAMPS
         if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); sm->acc[33] += t_ - kd_t; kd_t = t_; }
 #endif
-        if (tid == 0 && pre) { sm->npre = sm->npre_ok == KD_PREW; sm->npre_ok = 0; }
         KD_ACC(13);
         KD_STAMP(3);
     }
@@ -1308,12 +1075,11 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
     // (a static stride ended with the workgroups holding ceil(ns / grid) sources)
     const bool queued = g.jobs != nullptr;
     if (tid == 0) {
-        sm->njb = -1; sm->npre = 0; sm->npre_ok = 0; sm->wpar = 0;
+        sm->njb = -1; sm->wpar = 0;
         sm->jobs = g.jobs; sm->qnext = g.next; sm->drow = g.drow; sm->prow = g.prow; sm->rstride = g.rstride;
         sm->done = g.done; sm->ns = ns;
         sm->wsl[0] = wslice;
         sm->wsl[1] = reinterpret_cast<uint32_t*>(ws + (size_t)blockIdx.x * ws_stride + kd_ws_wpr1(n));
-        sm->dstage = reinterpret_cast<uint16_t*>(ws + (size_t)blockIdx.x * ws_stride + kd_ws_dstage(n));
     }
     // (the barriers of kd_next_source publish these)
     // the next job: taken in the previous row's output phases (planned launches), else here
@@ -1335,7 +1101,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
             for (int q = 0; q < KD_SEEDS; q++)
                 if (q < sm->job.nseed) bad = bad || sm->job.u[q] < 0 || sm->job.u[q] >= n || sm->job.seed[q] < 0;
             if (bad) {  // (uniform: every thread read the same job)
-                if (tid == 0) { raise_err(err, SHD_ROUTE_EINVAL); sm->npre = 0; }
+                if (tid == 0) raise_err(err, SHD_ROUTE_EINVAL);
                 // njb = -1 (thread 0, above) visible to every thread before the loop
                 // increment reads it: all take the next job from kd_next_source together
                 __syncthreads();
@@ -1361,16 +1127,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
         KD_ACC(9);
 #endif
         const bool seeded = __builtin_amdgcn_readfirstlane(sm->job.nseed) > 0;
-        if (seeded && __builtin_amdgcn_readfirstlane(sm->npre)) {
-#ifdef SHD_STAMPS
-            if (tid == 0) sm->acc[35] += 1;
-#endif
-            // pre-initialised during the previous row (kd_preinit): the parent records are in
-            // place, D0 comes from the staged array
-            const uint16_t* const dstg = sm->dstage;
-            for (int v0 = 8 * tid; v0 <= n; v0 += 8 * B)
-                *reinterpret_cast<uint4*>(dist + v0) = *reinterpret_cast<const uint4*>(dstg + v0);
-        } else if (seeded) {
+        if (seeded) {
             uint32_t* const wpr = wpr_of();
             // the seeds' rows are ready: one relaxed poll of each flag, one agent-scope
             // acquire (this CU's L1 invalidated), then every wave reads them with plain loads.
@@ -1382,20 +1139,10 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
                 const unsigned long long w0 = __builtin_amdgcn_s_memtime();
 #endif
                 const int ns0 = sm->job.nseed;
-                if (KD_SEEDANY && KD_SEEDSPIN > 0) {  // (first any ready seed, then the bounded polls)
-                    for (int spin = 0;; spin++) {
-                        bool any = false;
-                        for (int q = 0; q < ns0; q++)
-                            any = any || __hip_atomic_load(&g.done[sm->job.seed[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-                        if (any) break;
-                        if (spin >= (1 << 22)) { raise_err(err, SHD_ROUTE_EDEVICE); break; }
-                        __builtin_amdgcn_s_sleep(8);
-                    }
-                }
                 int kept = 0;
                 for (int q = 0; q < ns0; q++) {
                     const int* const flag = &g.done[sm->job.seed[q]];
-                    const int cap = ((q == 0 && !KD_SEEDANY) || KD_SEEDSPIN == 0) ? (1 << 22) : KD_SEEDSPIN;
+                    const int cap = (q == 0 || KD_SEEDSPIN == 0) ? (1 << 22) : KD_SEEDSPIN;
                     int spin = 0;
                     while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && spin < cap) {
                         __builtin_amdgcn_s_sleep(8);
@@ -1404,6 +1151,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
                     if (spin >= (1 << 22)) raise_err(err, SHD_ROUTE_EDEVICE);
                     if (spin >= cap && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
                         continue;  // (KD_SEEDSPIN: dropped)
+                    if (q > 0 && ((g.seed_drop >> q) & 1)) continue;  // (tests: a chosen subset)
                     if (kept != q) {
                         sm->job.seed[kept] = sm->job.seed[q];
                         sm->job.u[kept] = sm->job.u[q];
@@ -1429,66 +1177,20 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
             // parents of the seeds attaining D0(v), u_j's own vertex having parent s.  Phase
             // A's records overwrite the vertices that do improve.
             // 4 vertices per lane: 8-B distance and 16-B parent-record loads of every seed
-            constexpr bool icond = KD_ICOND != 0;
-            // (KD_ICOND 2: the next trip's distances are loaded before this trip's records, so
-            // the records' extra dependent step does not add a round trip per trip)
-            constexpr bool ipipe = KD_ICOND == 2;
-            uint2 dqn[KD_SEEDS];
-            if constexpr (ipipe) {
-#pragma unroll
-                for (int q = 0; q < KD_SEEDS; q++)
-                    dqn[q] = q < nseed ? *reinterpret_cast<const uint2*>(sdrow[q] + min(4 * tid, n & ~3))
-                                       : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-            }
+            // (loading a seed's records only where it attains D0 measured slower: round 4,
+            // DESIGN.md 4.3)
             for (int v0 = 4 * tid; v0 <= n; v0 += 4 * B) {
                 const int vl = min(v0, n & ~3);
                 uint2 dq[KD_SEEDS];
                 uint4 pq[KD_SEEDS];
-                if constexpr (ipipe) {
-#pragma unroll
-                    for (int q = 0; q < KD_SEEDS; q++) {
-                        dq[q] = dqn[q];
-                        pq[q] = make_uint4(KD_NONE, KD_NONE, KD_NONE, KD_NONE);
-                        const int vn = min(v0 + 4 * B, n & ~3);
-                        if (q < nseed) dqn[q] = *reinterpret_cast<const uint2*>(sdrow[q] + vn);
-                    }
-                } else {
 #pragma unroll
                 for (int q = 0; q < KD_SEEDS; q++) {
                     if (q < nseed) {
                         dq[q] = *reinterpret_cast<const uint2*>(sdrow[q] + vl);
-                        if (!icond) pq[q] = *reinterpret_cast<const uint4*>(sprow[q] + vl);
+                        pq[q] = *reinterpret_cast<const uint4*>(sprow[q] + vl);
                     } else {
                         dq[q] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
                         pq[q] = make_uint4(KD_NONE, KD_NONE, KD_NONE, KD_NONE);
-                    }
-                }
-                }
-                if constexpr (icond) {
-                    // records only of the seeds that attain D0 at one of the 4 vertices (a seed
-                    // that attains nowhere cannot win; the seed vertex's own record is rsu)
-                    unsigned dmin[4];
-#pragma unroll
-                    for (int h = 0; h < 4; h++) {
-                        dmin[h] = 0xFFFFu;
-#pragma unroll
-                        for (int q = 0; q < KD_SEEDS; q++) {
-                            const uint32_t d2 = (h < 2) ? dq[q].x : dq[q].y;
-                            const unsigned d = (h & 1) ? (d2 >> 16) : (d2 & 0xFFFFu);
-                            if (q < nseed) dmin[h] = min(dmin[h], min(0xFFFFu, wsu[q] + d));
-                        }
-                    }
-#pragma unroll
-                    for (int q = 0; q < KD_SEEDS; q++) {
-                        bool need = false;
-#pragma unroll
-                        for (int h = 0; h < 4; h++) {
-                            const uint32_t d2 = (h < 2) ? dq[q].x : dq[q].y;
-                            const unsigned d = (h & 1) ? (d2 >> 16) : (d2 & 0xFFFFu);
-                            need = need || (q < nseed && min(0xFFFFu, wsu[q] + d) == dmin[h] && v0 + h != su[q]);
-                        }
-                        if (need) pq[q] = *reinterpret_cast<const uint4*>(sprow[q] + vl);
-                        else pq[q] = make_uint4(KD_NONE, KD_NONE, KD_NONE, KD_NONE);
                     }
                 }
                 uint32_t dw[2], rw[4];
@@ -1536,7 +1238,6 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
             dist[s] = 0;
             pend[s >> 6] = 1ull << (s & 63);
             wmin[s >> 6] = 0;
-            sm->npre = 0;  // (consumed: every thread read it before the barrier above)
         }
         lds_barrier();
 

@@ -25,7 +25,7 @@ def route():
 KERNEL_ID = {"f64": 0, "k32": 1, "kb": 2, "k16": 3, "kd": 4, "kf": 5}
 
 
-@pytest.fixture(params=["auto", "kd", "k32", "f64", "kf"])  # K16: diagnostic build only
+@pytest.fixture(params=["auto", "kd", "k32", "f64", "kf"])
 def kernel(request, monkeypatch):
     """Run a test on the auto-selected kernel and on each forced kernel."""
     if request.param == "auto":

@@ -229,6 +229,36 @@ def test_full_table_every_row(monkeypatch, cfg):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("cfg,mask", [("c3", 2), ("c3", 4), ("c3", 6), ("c4", 2), ("c4", 4)])
+def test_seed_subsets_every_row(monkeypatch, cfg, mask):
+    """Seed dropping (KD_SEEDSPIN: a seed after the first not ready in time leaves the job)
+    claims ANY subset of a row's seeds gives exact rows.  SHD_ROUTE_SEEDDROP forces a chosen
+    subset on every seeded job -- bit 1 drops the second seed, bit 2 the third, 6 both --
+    and every row of the C3 / C4 table must still equal the oracle's digests."""
+    import torch
+    from shadow_amd import route
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    monkeypatch.delenv("SHD_ROUTE_KDGRID", raising=False)
+    monkeypatch.delenv("SHD_ROUTE_SEED", raising=False)
+    monkeypatch.setenv("SHD_ROUTE_SEEDDROP", str(mask))
+    gold = _gold(cfg)
+    g = config(cfg)
+    eng = route.RouteEngine(g)
+    T = g.targets()
+    plan = eng.plan(T)
+    assert plan.info["seeded"] == 1
+    dev = torch.device("cuda", 0)
+    d_tgt = torch.from_numpy(T.astype(np.int32)).to(dev)
+    d_lat = torch.empty((len(T), len(T)), dtype=torch.float64, device=dev)
+    d_rel = torch.empty_like(d_lat)
+    d_min = torch.empty(len(T), dtype=torch.float64, device=dev)
+    plan.rows_async(d_tgt, d_lat, d_rel, d_min, dispatch=False)
+    eng.sync()
+    assert _check_every_row(d_lat, d_rel, d_min, plan.sources, gold) == len(T)
+    del d_lat, d_rel
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("n,landmarks", [(20, None), (40, None), (300, "1"), (300, "64"), (300, "0")])
 def test_landmark_seeded_roots(oracle_mod, monkeypatch, n, landmarks):
     """Full grid (every workgroup slot starts with a landmark-seeded row): graphs smaller

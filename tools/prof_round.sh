@@ -37,4 +37,8 @@ pmc c3 FETCH_SIZE --config c3 --steps 2 --warmup 1
 pmc c3 WRITE_SIZE --config c3 --steps 2 --warmup 1
 pmc c5 FETCH_SIZE --config c5 --steps 3 --warmup 1
 pmc c5 WRITE_SIZE --config c5 --steps 3 --warmup 1
+pmc c3f FETCH_SIZE --config c3f --steps 2 --warmup 1
+pmc c3f WRITE_SIZE --config c3f --steps 2 --warmup 1
+pmc c4f FETCH_SIZE --config c4f --steps 1 --warmup 1
+pmc c4f WRITE_SIZE --config c4f --steps 1 --warmup 1
 echo prof done

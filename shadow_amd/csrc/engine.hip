@@ -1473,11 +1473,14 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, D
         std::memset(&jobs[q], 0, sizeof(KDJob));
         jobs[q].row = -1; jobs[q].s = verts[q]; jobs[q].store = q; jobs[q].nseed = 0;
     }
-    // the launch's own per-workgroup scratch (at most 256 workgroups, one per CU: each row is
-    // unseeded, so k rows on fewer workgroups would take k / grid row latencies): the
-    // context's is left to its rows launches, so none of those can share it even if one is
-    // still in flight
-    const int grid = std::min(k, 256);
+    // one round of workgroups for all k rows (each row is unseeded: k rows on fewer
+    // workgroups take k / grid row latencies): up to 256 rows in 1024-thread workgroups, one
+    // per CU, and more in the context's own (256-thread contexts: four per CU, each row only
+    // ~25% slower: C3's 512 hub rows 1.0 ms in two rounds of 1024-thread rows).  The launch
+    // has its own per-workgroup scratch: the context's is left to its rows launches, so none
+    // of those can share it even if one is still in flight.
+    const bool hub1024 = c->kd_hub_block > 0 && k <= 256;
+    const int grid = std::min(k, hub1024 ? 256 : std::max(256, c->kd_slots));
     DevBuf dj, dn, dw;
     if (dj.alloc(sizeof(KDJob) * k) || dd.alloc(sizeof(uint16_t) * (size_t)rs * k) ||
         dp.alloc(sizeof(uint32_t) * (size_t)rs * k) || dn.alloc(sizeof(int) * (1 + (size_t)k)) ||
@@ -1496,7 +1499,7 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, D
     g.drow = (const uint16_t*)dd.p; g.drow_out = (uint16_t*)dd.p; g.prow = (uint32_t*)dp.p; g.rstride = rs;
     g.done = (int*)dn.p + 1;
     if ((rc = kd_launch(c, g, (int*)dn.p, nullptr, k, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, true,
-                        (char*)dw.p, grid, true)))
+                        (char*)dw.p, grid, hub1024)))
         return rc;
     if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
     if ((rc = take_err(c))) return rc;
@@ -1788,6 +1791,12 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             for (int q = 0; q < nj; q++) jr[q] = job_row[jpos_of[order[q]]];
             job_pos.swap(order);
             job_row.swap(jr);
+            // (landmark-only plans have no seed order to keep: SHD_ROUTE_LMALL_REV=1 queues the
+            // peripheral rows, the costliest to bound from landmarks, first)
+            if (lm_all && getenv("SHD_ROUTE_LMALL_REV") && atoi(getenv("SHD_ROUTE_LMALL_REV"))) {
+                std::reverse(job_pos.begin(), job_pos.end());
+                std::reverse(job_row.begin(), job_row.end());
+            }
         }
         std::vector<int> first(n, -1);  // first job of each source vertex
         for (int j = 0; j < nj; j++) if (first[src[job_pos[j]]] < 0) first[src[job_pos[j]]] = j;
@@ -2128,8 +2137,10 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // thread while this one builds the schedule (C4: ~0.5 ms of hipMalloc and copies)
         bool store_ok = false;
         std::thread store_th;
-        if (ntot > 0)
-            store_th = std::thread([&]() {
+        // (SHD_ROUTE_STORE_SYNC=1: the allocation after the schedule, on this thread -- an A/B
+        // of the schedule's time with and without the allocating thread beside it)
+        const bool store_sync = getenv("SHD_ROUTE_STORE_SYNC") && atoi(getenv("SHD_ROUTE_STORE_SYNC"));
+        auto store_fn = [&]() {
                 bool r = hipSetDevice(c->device) == hipSuccess &&
                          hipMalloc((void**)&P->d_drow, sizeof(uint16_t) * (size_t)rs * ntot) == hipSuccess &&
                          hipMalloc((void**)&P->d_prow, sizeof(uint32_t) * (size_t)rs * ntot) == hipSuccess;
@@ -2144,7 +2155,8 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
                 r = r && hipMalloc((void**)&P->d_jobs, sizeof(KDJob) * (size_t)nj) == hipSuccess &&
                     hipMalloc((void**)&P->d_next, sizeof(int) * (1 + (size_t)ntot)) == hipSuccess;
                 store_ok = r;
-            });
+            };
+        if (ntot > 0 && !store_sync) store_th = std::thread(store_fn);
         struct JoinOne { std::thread& t; ~JoinOne() { if (t.joinable()) t.join(); } } join_store{store_th};
         t_alloc = since();
         if (ntot > 0) {
@@ -2268,6 +2280,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             }
         }
         if (store_th.joinable()) store_th.join();
+        if (ntot > 0 && store_sync) store_fn();
         t_store = since();
         if (store_ok) {
             P->seeded = 1;

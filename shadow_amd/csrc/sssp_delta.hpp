@@ -176,6 +176,24 @@ constexpr int KD_NACC = 40;
 #define KD_FLUSH() do { } while (0)
 #endif
 
+// the output phases' launch-invariant arguments, staged in LDS once per launch: kd_output
+// takes only its row's values (its ~26 arguments used to overflow the 32 argument VGPRs of
+// the call ABI, and every row stored the rest to the stack: scratch traffic per row)
+struct KDOut {
+    const KD_GLOBAL int* tgt;
+    KD_GLOBAL double* lat_out;
+    KD_GLOBAL double* rel_out;
+    KD_GLOBAL double* row_min;
+    int* err;
+    KD_GLOBAL double* relv;      // this workgroup's HBM slice
+    const KD_GLOBAL double* rtab;
+    const KD_GLOBAL double* vf;
+    long long ld;
+    int n, nw, nt, tsorted;
+    unsigned rmask;
+    int rc, walk, nrtab, rone, has_vf, dflags;
+};
+
 struct KDSmall {
     unsigned gmin[2];   // min pending distance at the start of a bucket round (by parity)
     int head, tail;     // work queue of this bucket round: grabbed / reserved
@@ -207,6 +225,7 @@ struct KDSmall {
     int* done;
     uint32_t* wsl[2];   // the two record slices of this workgroup
     int ns;
+    KDOut out;          // kd_output's launch-invariant arguments
 #ifdef SHD_STAMPS
     unsigned long long acc[KD_NACC];
 #endif
@@ -464,19 +483,41 @@ __device__ inline int kd_next_source(int* ctr, int* slot, int tid, bool all_queu
 // Phases C/D of one row (lat row, parent copy, reliability by walks or level sweeps, rel
 // row, row min), called once per row.  Not inlined, on purpose: see the call site.
 template <int B>
-__device__ __attribute__((noinline)) void kd_output(const int n, const int nw, const int nt, const long long ld, const int i,
-                                                    const int s, const double cs, const double sw_s, const double sr_s,
-                                                    const int tsorted, const unsigned rmask, const int rc,
-                                                    const KD_GLOBAL int* __restrict__ tgt, KD_GLOBAL double* __restrict__ lat_out,
-                                                    KD_GLOBAL double* __restrict__ rel_out, KD_GLOBAL double* __restrict__ row_min,
-                                                    int* __restrict__ err, const KD_GLOBAL uint32_t* __restrict__ wpr,
-                                                    KD_GLOBAL double* __restrict__ relv, const int walk,
-                                                    const KD_GLOBAL double* __restrict__ rtab, const int nrtab, const int rone,
-                                                    const KD_GLOBAL double* __restrict__ vf, const int has_vf, const int dflags) {
+__device__ __attribute__((noinline)) void kd_output(const int i, const int s, const double cs, const double sw_s,
+                                                    const double sr_s, const KD_GLOBAL uint32_t* __restrict__ wpr) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int RR = kd_rr<B>();
-    const KDLayout<B> L = KDLayout<B>::make(n, rc, RR);
     KDSmall* sm = reinterpret_cast<KDSmall*>(smem);
+    // the launch-invariant arguments out of LDS, as wave-uniform (scalar) values
+    auto uni = [](auto x) __attribute__((always_inline)) {
+        using T = decltype(x);
+        if constexpr (sizeof(T) == 8) {
+            unsigned long long b;
+            __builtin_memcpy(&b, &x, 8);
+            b = (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)b) |
+                ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32)) << 32);
+            T y;
+            __builtin_memcpy(&y, &b, 8);
+            return y;
+        } else {
+            return (T)__builtin_amdgcn_readfirstlane((int)x);
+        }
+    };
+    const KDOut& O = sm->out;
+    const KD_GLOBAL int* __restrict__ const tgt = uni(O.tgt);
+    KD_GLOBAL double* __restrict__ const lat_out = uni(O.lat_out);
+    KD_GLOBAL double* __restrict__ const rel_out = uni(O.rel_out);
+    KD_GLOBAL double* __restrict__ const row_min = uni(O.row_min);
+    int* __restrict__ const err = uni(O.err);
+    KD_GLOBAL double* __restrict__ const relv = uni(O.relv);
+    const KD_GLOBAL double* __restrict__ const rtab = uni(O.rtab);
+    const KD_GLOBAL double* __restrict__ const vf = uni(O.vf);
+    const long long ld = uni(O.ld);
+    const int n = uni(O.n), nw = uni(O.nw), nt = uni(O.nt), tsorted = uni(O.tsorted);
+    const unsigned rmask = uni(O.rmask);
+    const int rc = uni(O.rc), walk = uni(O.walk), nrtab = uni(O.nrtab), rone = uni(O.rone);
+    const int has_vf = uni(O.has_vf), dflags = uni(O.dflags);
+    const KDLayout<B> L = KDLayout<B>::make(n, rc, RR);
     const int tid = threadIdx.x, lane = tid & 63;
     uint16_t* dist = reinterpret_cast<uint16_t*>(smem + L.dist);
     unsigned long long* pend = reinterpret_cast<unsigned long long*>(smem + L.pend);
@@ -1080,6 +1121,12 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
         sm->done = g.done; sm->ns = ns;
         sm->wsl[0] = wslice;
         sm->wsl[1] = reinterpret_cast<uint32_t*>(ws + (size_t)blockIdx.x * ws_stride + kd_ws_wpr1(n));
+        KDOut& o = sm->out;
+        o.tgt = (const KD_GLOBAL int*)tgt; o.lat_out = (KD_GLOBAL double*)lat_out; o.rel_out = (KD_GLOBAL double*)rel_out;
+        o.row_min = (KD_GLOBAL double*)row_min; o.err = err; o.relv = (KD_GLOBAL double*)relv;
+        o.rtab = (const KD_GLOBAL double*)g.rtab; o.vf = (const KD_GLOBAL double*)g.vf; o.ld = ld;
+        o.n = n; o.nw = nw; o.nt = nt; o.tsorted = tsorted ? 1 : 0; o.rmask = rmask; o.rc = g.rc; o.walk = g.walk;
+        o.nrtab = g.nrtab; o.rone = g.rone; o.has_vf = g.has_vf; o.dflags = KD_DFLAGS;
     }
     // (the barriers of kd_next_source publish these)
     // the next job: taken in the previous row's output phases (planned launches), else here
@@ -1855,10 +1902,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
         // output phases in their own function: its registers are allocated for these loops
         // alone (inlined, phase A's pressure spilled the values they use to scratch, and
         // every reload waited behind the row's output stores: one in-order vmcnt)
-        kd_output<B>(n, nw, nt, ld, i, s, cs, sw_s, sr_s, tsorted ? 1 : 0, rmask, g.rc, (const KD_GLOBAL int*)tgt,
-                     (KD_GLOBAL double*)lat_out, (KD_GLOBAL double*)rel_out, (KD_GLOBAL double*)row_min, err,
-                     (const KD_GLOBAL uint32_t*)wpr, (KD_GLOBAL double*)relv, g.walk, (const KD_GLOBAL double*)g.rtab,
-                     g.nrtab, g.rone, (const KD_GLOBAL double*)g.vf, g.has_vf, KD_DFLAGS);
+        kd_output<B>(i, s, cs, sw_s, sr_s, (const KD_GLOBAL uint32_t*)wpr);
         lds_barrier();
         KD_STAMP(4);
         KD_FLUSH();

@@ -423,3 +423,42 @@ def test_c3_eight_rank_plans_every_row(monkeypatch):
         assert _check_every_row(d_lat, d_rel, d_min, plan.sources, gold) == plan.info["rows"]
         seen.extend(plan.positions.tolist())
     assert sorted(seen) == list(range(len(T)))
+
+
+@pytest.mark.parametrize("world,vloss", [(1, False), (1, True), (3, False)])
+def test_landmark_only_plans(oracle_mod, monkeypatch, world, vloss):
+    """Landmark-only plans (round 5: 256-thread contexts with n >= 4 x 512, and ranks with at
+    most 1.5 rows per workgroup slot): every row seeded from its 3 nearest of 512 landmark
+    rows, all at level 0, a rank taking every world-th row.  Bit-exact against the oracle,
+    the ranks covering the source list exactly once; the landmark seeds chosen on the device
+    equal the host's choice (SHD_ROUTE_GPUCHOICE=0)."""
+    from shadow_amd import route
+    from shadow_amd.graph import internet_like
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    monkeypatch.delenv("SHD_ROUTE_KDGRID", raising=False)
+    monkeypatch.delenv("SHD_ROUTE_SEED", raising=False)
+    monkeypatch.delenv("SHD_ROUTE_LANDMARKS", raising=False)
+    g = internet_like(3000, 3, seed=77, vloss=vloss, name="ba3000")
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 4 and eng.info["block"] == 256
+    T = g.targets()
+    og = oracle_mod.OracleGraph(g)
+    seen = []
+    for r in range(world):
+        plan = eng.plan(T, world, r)
+        info = dict(plan.info)
+        assert info["seeded"] == 1 and info["levels"] == 1 and info["helpers"] == 0 and info["stored_rows"] == 0, info
+        lat, rel, mn = _plan_rows(eng, plan, T)
+        pos = plan.positions.copy()
+        olat, orel, _, _ = og.source_rows(T[pos], T, oracle_mod.TIE_MINKEY)
+        assert np.array_equal(lat, olat) and np.array_equal(rel, orel) and np.array_equal(mn, olat.min(axis=1))
+        seen.extend(pos.tolist())
+        plan.close()
+        monkeypatch.setenv("SHD_ROUTE_GPUCHOICE", "0")
+        plan = eng.plan(T, world, r)
+        assert plan.info == info and np.array_equal(plan.positions, pos)
+        lat2, rel2, _ = _plan_rows(eng, plan, T)
+        assert np.array_equal(lat2, lat) and np.array_equal(rel2, rel)
+        plan.close()
+        monkeypatch.delenv("SHD_ROUTE_GPUCHOICE")
+    assert sorted(seen) == list(range(len(T)))

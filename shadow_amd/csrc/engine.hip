@@ -164,6 +164,9 @@ struct shd_route {
     uint32_t* d_fwinl = nullptr;  // K4 parent search: sorted in-arc keys per vertex (np x np)
     uint16_t* d_fwpos = nullptr;  // and the start index per small threshold (n x FW_X)
     uint32_t* d_fwkey = nullptr;
+    uint8_t* d_fwrix = nullptr;  // K4 rows: reliability index of each arc (dense n x n u8)
+    double* d_fwrtab = nullptr;  // and the distinct reliabilities (fw_nrtab <= 255; 0: dense R reads)
+    int fw_nrtab = 0;
     size_t fwkey_cap = 0;
     int fw_np = 0, fw_ready = 0;
     uint64_t device_bytes = 0;
@@ -1439,7 +1442,8 @@ namespace {
 
 // landmark-only plans: at most this many rows per workgroup slot, and their landmark count
 constexpr double PLAN_LMALL_RPS = 1.5;
-constexpr int PLAN_LMALL_COUNT = 512;
+constexpr int PLAN_LMALL_COUNT = 1024;  // (C3 1 GPU: 256 / 512 / 1024 / 2048 landmarks 2.49 / 2.30 / 2.18 / 2.07 ms;
+                                        //  2048 take two rounds of hub rows in the plan)
 
 // host threads of a plan (the box's CPU quota is 16)
 int plan_threads() {
@@ -1614,7 +1618,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     int lmall_small = 1;
     if (const char* e = getenv("SHD_ROUTE_LMALL_SMALL")) lmall_small = atoi(e);
     const bool lm_all = !c->multigraph && c->kd_slots > 0 &&
-                        ((lmall_small && c->kd_block < 1024 && n >= 4 * PLAN_LMALL_COUNT) ||
+                        ((lmall_small && c->kd_block < 1024 && n >= 2048) ||
                          (double)ns / world <= lmall_rps * (double)c->kd_slots);
     if (lm_all) nland = std::min(n, PLAN_LMALL_COUNT);
     else if (world > 1 && !c->multigraph) nland = std::min(n, 256);
@@ -1791,9 +1795,10 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             for (int q = 0; q < nj; q++) jr[q] = job_row[jpos_of[order[q]]];
             job_pos.swap(order);
             job_row.swap(jr);
-            // (landmark-only plans have no seed order to keep: SHD_ROUTE_LMALL_REV=1 queues the
-            // peripheral rows, the costliest to bound from landmarks, first)
-            if (lm_all && getenv("SHD_ROUTE_LMALL_REV") && atoi(getenv("SHD_ROUTE_LMALL_REV"))) {
+            // (landmark-only plans have no seed order to keep: the peripheral rows, the costliest
+            // to bound from landmarks, go first, so the launch ends on cheap central ones: C3
+            // 2.18 -> 2.12 ms, 8-way 0.63 -> 0.61 ms; SHD_ROUTE_LMALL_REV=0 keeps rank order)
+            if (lm_all && !(getenv("SHD_ROUTE_LMALL_REV") && atoi(getenv("SHD_ROUTE_LMALL_REV")) == 0)) {
                 std::reverse(job_pos.begin(), job_pos.end());
                 std::reverse(job_row.begin(), job_row.end());
             }
@@ -2432,6 +2437,41 @@ int fw_prepare(shd_route* c, hipStream_t st) {
     if (hipMalloc((void**)&D, 2 * cells) != hipSuccess || hipMalloc((void**)&inl, 4 * cells) != hipSuccess ||
         hipMalloc((void**)&pos, sizeof(uint16_t) * FW_X * (size_t)c->n) != hipSuccess)
         return undo(SHD_ROUTE_ENOMEM);
+    // reliability indices (round 5): every distinct 1 - loss (exact bits), at most 255 of them
+    // (C5: 101), as a dense u8 matrix: fw_rows reads a parent arc's index and multiplies the
+    // table entry in LDS
+    std::vector<uint64_t> rbits;
+    for (int e = 0; e < c->m; e++) { uint64_t b; std::memcpy(&b, &c->e_rel[e], 8); rbits.push_back(b); }
+    std::sort(rbits.begin(), rbits.end());
+    rbits.erase(std::unique(rbits.begin(), rbits.end()), rbits.end());
+    uint8_t* rixd = nullptr;
+    if (rbits.size() <= 255 && !getenv("SHD_ROUTE_FWDENSER")) {
+        std::vector<double> rt(rbits.size());
+        for (size_t q = 0; q < rbits.size(); q++) std::memcpy(&rt[q], &rbits[q], 8);
+        std::vector<uint8_t> rix((size_t)c->n * c->n, 0xFF);
+        auto idx = [&](double r) {
+            uint64_t b; std::memcpy(&b, &r, 8);
+            return (uint8_t)(std::lower_bound(rbits.begin(), rbits.end(), b) - rbits.begin());
+        };
+        // (the same edge ensure_dense keeps: the lowest edge id of a pair)
+        for (int e = c->m - 1; e >= 0; e--) {
+            const int a = c->e_src[e], b = c->e_dst[e];
+            rix[(size_t)a * c->n + b] = idx(c->e_rel[e]);
+            if (!c->directed) rix[(size_t)b * c->n + a] = idx(c->e_rel[e]);
+        }
+        if (hipMalloc((void**)&rixd, rix.size()) != hipSuccess ||
+            hipMalloc((void**)&c->d_fwrtab, sizeof(double) * 256) != hipSuccess ||
+            hipMemcpy(rixd, rix.data(), rix.size(), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(c->d_fwrtab, rt.data(), sizeof(double) * rt.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            for (void* q : {(void*)rixd, (void*)c->d_fwrtab}) if (q) (void)hipFree(q);
+            c->d_fwrtab = nullptr;
+            return undo(SHD_ROUTE_ENOMEM);
+        }
+        c->d_fwrix = rixd;
+        c->allocs.push_back(c->d_fwrix);
+        c->allocs.push_back(c->d_fwrtab);
+        c->fw_nrtab = (int)rt.size();
+    }
     hipLaunchKernelGGL(fw_inlist_kernel, dim3(c->n), dim3(1024), 4 * sp, st, c->d_W, c->n, np, sp, inl, pos);
     if ((rc = hip_check(hipGetLastError()))) return undo(rc);
     c->d_fwD = D;
@@ -2518,10 +2558,15 @@ int shd_route_fw_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, co
         if (hipMalloc((void**)&c->d_fwkey, need * sizeof(uint32_t)) != hipSuccess) return SHD_ROUTE_ENOMEM;
         c->fwkey_cap = need;
     }
-    hipLaunchKernelGGL(fw_parent_kernel, dim3(std::min(ns, 4096)), dim3(1024), 2 * np, st, c->d_fwD, c->d_fwinl,
+    // (256-thread workgroups: at fw_parent's 70 VGPRs a CU holds seven of them, against one of
+    // 1024 threads: C5 rows 1.02 -> 0.94 ms; SHD_ROUTE_FWPBLK=512 / 1024 for the A/B)
+    int pblk = 256;
+    if (const char* e = getenv("SHD_ROUTE_FWPBLK")) pblk = atoi(e) == 1024 ? 1024 : atoi(e) == 512 ? 512 : 256;
+    hipLaunchKernelGGL(fw_parent_kernel, dim3(std::min(ns, 8192)), dim3(pblk), 2 * np, st, c->d_fwD, c->d_fwinl,
                        c->d_fwpos, c->n, np, d_src, ns, c->d_fwkey);
     FWRowsArgs a;
     a.n = c->n; a.np = np; a.bound = c->k32_bound; a.D = c->d_fwD; a.key = c->d_fwkey; a.R = c->d_R;
+    a.rix = c->d_fwrix; a.rtab = c->d_fwrtab; a.nrtab = c->d_fwrix ? c->fw_nrtab : 0;
     a.vf = c->d_vf; a.self_w = c->d_self_w; a.self_r = c->d_self_r;
     const size_t lds = a16(sizeof(double) * c->n) + a16(sizeof(int) * c->n) + a16(sizeof(int) * (c->k32_bound + 2));
     hipLaunchKernelGGL(fw_rows_kernel, dim3(std::min(ns, 2048)), dim3(1024), lds, st, a, d_src, ns, d_tgt, nt,

@@ -624,15 +624,25 @@ __global__ __launch_bounds__(1024) void fw_inlist_kernel(const double* __restric
 
 // parents: key[s][v] = min over u != v with D[s][u] + w(u,v) == D[s][v] of
 // (0xFFFF - w) << 16 | u (largest w, then smallest u: the engine tie rule), FW_END for the
-// source and unreachable vertices.  One workgroup per source with D[s][.] in LDS; a
-// thread per target scans v's in-arc list in key order from the first arc with
-// w <= D[s][v] (pos table, or a binary search past FW_X) and stops at the first tight
-// arc, which is the minimum key.  A scan visits only the arcs with w in (w*, D[s][v]].
+// source and unreachable vertices.  One workgroup per source with D[s][.] in LDS; a thread
+// scans its targets' in-arc lists in key order from the first arc with w <= D[s][v] (pos
+// table, or a binary search past FW_X) and stops at the first tight arc, which is the
+// minimum key.  A scan visits only the arcs with w in (w*, D[s][v]]: on K4000 with
+// U[1,250] latencies ~20 trips of 8 arcs, each a dependent global load.  Round 5: a thread
+// keeps FW_PQ scans in flight (a slot whose scan ends takes the thread's next target in the
+// same trip), so a trip's loads cover FW_PQ targets (0.90 ms for C5's 16 M pairs with one).
+// The scan starts at the 8-arc boundary below the first candidate: the arcs before it
+// have w > D[s][v], never tight (D[s][u] + w > D[s][v]), so they cost a compare, not a
+// result.  In-arc lists hold np entries padded with FW_END, so a scan always ends.
+#ifndef FW_PQ
+#define FW_PQ 4
+#endif
 __global__ __launch_bounds__(1024) void fw_parent_kernel(const uint16_t* __restrict__ D, const uint32_t* __restrict__ inl,
                                                          const uint16_t* __restrict__ pos, int n, int np,
                                                          const int* __restrict__ src, int ns,
                                                          uint32_t* __restrict__ key) {
     extern __shared__ __attribute__((aligned(16))) uint16_t drow[];
+    static_assert(FW_SCAN == 8, "two 16-byte loads per scan trip");
     for (int i = blockIdx.x; i < ns; i += gridDim.x) {
         const int s = src[i];
         if (s < 0 || s >= n) continue;  // fw_rows raises the error for this row
@@ -641,50 +651,81 @@ __global__ __launch_bounds__(1024) void fw_parent_kernel(const uint16_t* __restr
         for (int q = threadIdx.x; q < np / 8; q += blockDim.x)
             reinterpret_cast<uint4*>(drow)[q] = reinterpret_cast<const uint4*>(Ds)[q];
         __syncthreads();
-        for (int v = threadIdx.x; v < n; v += blockDim.x) {
-            const unsigned d = drow[v];
-            uint32_t best = FW_END;
-            if (v != s && d != 0xFFFFu) {
-                const uint32_t* lv = inl + (long long)v * np;
-                int k;
-                if (d < (unsigned)FW_X) {
-                    k = pos[(long long)v * FW_X + d];
-                } else {
+        uint32_t* const krow = key + (long long)i * np;
+        // slots: target v (-1 idle), its distance, scan position (-1: not yet located)
+        int sv[FW_PQ], sk[FW_PQ];
+        unsigned sd[FW_PQ];
+        int vnext = threadIdx.x;
+        // the next target that needs a scan (the source and unreachable vertices are written
+        // here; a target at distance >= FW_X is located by its binary search at once)
+        auto take = [&](int q) __attribute__((always_inline)) {
+            sv[q] = -1;
+            while (vnext < n) {
+                const int v = vnext;
+                vnext += blockDim.x;
+                const unsigned d = drow[v];
+                if (v == s || d == 0xFFFFu) { krow[v] = FW_END; continue; }
+                sv[q] = v; sd[q] = d; sk[q] = -1;
+                if (d >= (unsigned)FW_X) {
+                    const uint32_t* lv = inl + (long long)v * np;
                     const uint32_t thr = (0xFFFFu - d) << 16;
                     int lo = 0, hi = pos[(long long)v * FW_X + FW_X - 1];
                     while (lo < hi) {
                         const int mid = (lo + hi) >> 1;
                         if (lv[mid] < thr) lo = mid + 1; else hi = mid;
                     }
-                    k = lo;
+                    sk[q] = lo & ~(FW_SCAN - 1);
                 }
-                // to a 4-arc boundary one arc at a time, then 4 arcs per trip (one 16-byte
-                // load, four independent LDS gathers, the first tight one in key order)
-                bool done = false;
-                for (; k < np && (k & (FW_SCAN - 1)); k++) {
-                    const uint32_t e = lv[k];
-                    if (e == FW_END) { done = true; break; }
-                    if (drow[e & 0xFFFFu] + (0xFFFFu - (e >> 16)) == d) { best = e; done = true; break; }
-                }
-                for (; !done && k < np; k += FW_SCAN) {  // (np: a multiple of 64)
-                    uint32_t e[FW_SCAN];
+                return;
+            }
+        };
 #pragma unroll
-                    for (int q4 = 0; q4 < FW_SCAN; q4 += 4) {
-                        const uint4 e4 = *reinterpret_cast<const uint4*>(lv + k + q4);
-                        e[q4] = e4.x; e[q4 + 1] = e4.y; e[q4 + 2] = e4.z; e[q4 + 3] = e4.w;
-                    }
-                    unsigned dd[FW_SCAN];
+        for (int q = 0; q < FW_PQ; q++) take(q);
+        for (;;) {
+            bool any = false;
 #pragma unroll
-                    for (int q = 0; q < FW_SCAN; q++) dd[q] = drow[e[q] == FW_END ? 0u : (e[q] & 0xFFFFu)];
+            for (int q = 0; q < FW_PQ; q++) any = any || sv[q] >= 0;
+            if (!any) break;
+            // one trip: every slot's loads first (a located slot's next 8 arcs, an unlocated
+            // one's pos entry), then the checks
+            uint4 ea[FW_PQ], eb[FW_PQ];
+            unsigned pk[FW_PQ];
 #pragma unroll
-                    for (int q = 0; q < FW_SCAN; q++) {
-                        if (done) continue;
-                        if (e[q] == FW_END) done = true;
-                        else if (dd[q] + (0xFFFFu - (e[q] >> 16)) == d) { best = e[q]; done = true; }
-                    }
+            for (int q = 0; q < FW_PQ; q++) {
+                ea[q] = eb[q] = make_uint4(FW_END, FW_END, FW_END, FW_END);
+                pk[q] = 0u;
+                if (sv[q] < 0) continue;
+                if (sk[q] >= 0) {
+                    const uint32_t* lv = inl + (long long)sv[q] * np + sk[q];
+                    ea[q] = *reinterpret_cast<const uint4*>(lv);
+                    eb[q] = *reinterpret_cast<const uint4*>(lv + 4);
+                } else {
+                    pk[q] = pos[(long long)sv[q] * FW_X + sd[q]];
                 }
             }
-            key[(long long)i * np + v] = best;
+#pragma unroll
+            for (int q = 0; q < FW_PQ; q++) {
+                if (sv[q] < 0) continue;
+                if (sk[q] < 0) { sk[q] = (int)pk[q] & ~(FW_SCAN - 1); continue; }
+                const uint32_t e[FW_SCAN] = {ea[q].x, ea[q].y, ea[q].z, ea[q].w, eb[q].x, eb[q].y, eb[q].z, eb[q].w};
+                unsigned dd[FW_SCAN];
+#pragma unroll
+                for (int h = 0; h < FW_SCAN; h++) dd[h] = drow[e[h] == FW_END ? 0u : (e[h] & 0xFFFFu)];
+                uint32_t best = FW_END;
+                bool done = false;
+#pragma unroll
+                for (int h = 0; h < FW_SCAN; h++) {
+                    if (done) continue;
+                    if (e[h] == FW_END) done = true;
+                    else if (dd[h] + (0xFFFFu - (e[h] >> 16)) == sd[q]) { best = e[h]; done = true; }
+                }
+                sk[q] += FW_SCAN;
+                if (!done && sk[q] >= np) done = true;  // (np: a multiple of 64; lists end in FW_END)
+                if (done) {
+                    krow[sv[q]] = best;
+                    take(q);
+                }
+            }
         }
     }
 }
@@ -697,6 +738,12 @@ struct FWRowsArgs {
     const uint16_t* D;
     const uint32_t* key;     // [ns][np]
     const double* R;         // dense 1 - loss, n x n (NaN = no edge)
+    // (round 5) the same as indices into a table of the distinct reliabilities (<= 255 of
+    // them, nrtab > 0): a random (p, v) read of 1 byte from a 16 MB matrix (C5) instead of 8
+    // from a 128 MB one, the factor from the table in LDS
+    const uint8_t* rix;
+    const double* rtab;
+    int nrtab;
     const double* vf;
     const double* self_w;
     const double* self_r;
@@ -711,6 +758,8 @@ __global__ __launch_bounds__(1024) void fw_rows_kernel(FWRowsArgs a, const int* 
     int* order = reinterpret_cast<int*>(smem + a16(sizeof(double) * a.n));
     int* bstart = reinterpret_cast<int*>(smem + a16(sizeof(double) * a.n) + a16(sizeof(int) * a.n));
     __shared__ unsigned long long rmin;
+    __shared__ double rtl[256];
+    for (int k = threadIdx.x; k < a.nrtab; k += blockDim.x) rtl[k] = a.rtab[k];
     const int nbk = a.bound + 2;
     for (int i = blockIdx.x; i < ns; i += gridDim.x) {
         const int s = src[i];
@@ -747,7 +796,7 @@ __global__ __launch_bounds__(1024) void fw_rows_kernel(FWRowsArgs a, const int* 
                 const uint32_t k = Ks[v];
                 if (k == 0xFFFFFFFFu) { raise_err(err, SHD_ROUTE_EUNREACH); rel[v] = NAN; continue; }
                 const int p = (int)(k & 0xFFFFu);
-                rel[v] = rel[p] * a.R[(long long)p * a.n + v];
+                rel[v] = rel[p] * (a.nrtab > 0 ? rtl[a.rix[(long long)p * a.n + v]] : a.R[(long long)p * a.n + v]);
             }
             __syncthreads();
         }

@@ -292,7 +292,10 @@ constexpr int KD_MAXD = 32;           // phase C path walk: arcs held in registe
 #ifndef KD_SEEDSPIN
 #define KD_SEEDSPIN 8  // seeded init: polls (s_sleep 8 each) of a second or third seed's flag before it is dropped (0: wait; round 4: C3 2.68 -> 2.53 ms, C4 44.7 -> 44.4)
 #endif
-constexpr int KD_WQ = 2;              // phase C path walk: targets per thread (4 measured 1% slower at C4: its registers put 39 VGPRs of the output function in callee-saved ranges, saved to scratch and restored around every row; 2: 13)
+#ifndef KD_WQ_N
+#define KD_WQ_N 2
+#endif
+constexpr int KD_WQ = KD_WQ_N;        // phase C path walk: targets per thread (4 measured 1% slower at C4: its registers put 39 VGPRs of the output function in callee-saved ranges, saved to scratch and restored around every row; 2: 13)
 constexpr int KD_ONE = 254;           // phase C: rtab slot holding 1.0 (the source's own step)
 constexpr int KD_NAN = 255;           // phase C: rtab slot holding NaN (unreachable vertices)
 constexpr int KD_RR = 512;  // parent-record ring slots (1024-thread workgroups; smaller ones use 256)
@@ -549,18 +552,51 @@ __device__ __attribute__((noinline)) void kd_output(const int i, const int s, co
         else { Lv = (double)dist[t]; lmin = fmin(lmin, Lv); }
         return Lv;
     };
+    // phase B's parent records (wpr) visible to every wave (loading the parent copy's first
+    // trip here, under the lat row, measured slower: its registers cost callee saves, 41.5 ->
+    // 41.8 ms at C4)
+    const bool walks = g.walk && rrow;
+    wait_stores();
+    __syncthreads();
     if (tsorted) {
-        // two adjacent vertices per lane: consecutive positions go out as one 16-B store
+        // four adjacent vertices per lane (one 64-bit mask word, one prefix entry and one 8-B
+        // distance read for all four; round 5: two per lane took 6 LDS reads per pair),
+        // consecutive positions out as 16-B stores.  (dist holds n + 1 entries padded to 8:
+        // the group at the end reads at most the padding and the next area, and uses neither)
         const int lpar = (int)(((uintptr_t)lrow >> 3) & 1);
-        for (int v = 2 * tid; v < (i >= 0 ? n : 0); v += 2 * B) {
-            const int j0 = tpos(v), j1 = v + 1 < n ? tpos(v + 1) : -1;
-            const double L0 = j0 >= 0 ? lat_of(v) : 0.0, L1 = j1 >= 0 ? lat_of(v + 1) : 0.0;
+        for (int v0 = 4 * tid; v0 < (i >= 0 ? n : 0); v0 += 4 * B) {
+            const unsigned long long wd = tmask[v0 >> 6];
+            const int sh = v0 & 63;
+            int j = (int)tpre[v0 >> 6] + __popcll(wd & ((1ull << sh) - 1ull));
+            const uint2 d4 = *reinterpret_cast<const uint2*>(dist + v0);
+            int jq[4];
+            double Lq[4];
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                const int v = v0 + h;
+                const bool tg = v < n && ((wd >> (sh + h)) & 1ull);
+                jq[h] = tg ? j++ : -1;
+                const unsigned d = ((h < 2 ? d4.x : d4.y) >> (16 * (h & 1))) & 0xFFFFu;
+                double Lv = 0.0;
+                if (tg) {
+                    if (v == s) {
+                        if (isnan(sw_s)) { raise_err(err, SHD_ROUTE_ENOEDGE); Lv = NAN; }
+                        else { Lv = 0.0 + sw_s; lmin = fmin(lmin, Lv); }
+                    } else if (d == 0xFFFFu) { raise_err(err, SHD_ROUTE_EUNREACH); Lv = NAN; }
+                    else { Lv = (double)d; lmin = fmin(lmin, Lv); }
+                }
+                Lq[h] = Lv;
+            }
             if (!lrow || !KD_OUT) continue;
-            if (j0 >= 0 && j1 == j0 + 1 && !((j0 + lpar) & 1))
-                __builtin_nontemporal_store(kd_d2{L0, L1}, reinterpret_cast<KD_GLOBAL kd_d2*>(lrow + j0));
-            else {
-                if (j0 >= 0) __builtin_nontemporal_store(L0, lrow + j0);
-                if (j1 >= 0) __builtin_nontemporal_store(L1, lrow + j1);
+#pragma unroll
+            for (int h = 0; h < 4; h += 2) {
+                const int ja = jq[h], jb = jq[h + 1];
+                if (ja >= 0 && jb == ja + 1 && !((ja + lpar) & 1))
+                    __builtin_nontemporal_store(kd_d2{Lq[h], Lq[h + 1]}, reinterpret_cast<KD_GLOBAL kd_d2*>(lrow + ja));
+                else {
+                    if (ja >= 0) __builtin_nontemporal_store(Lq[h], lrow + ja);
+                    if (jb >= 0) __builtin_nontemporal_store(Lq[h + 1], lrow + jb);
+                }
             }
         }
     } else {
@@ -569,7 +605,6 @@ __device__ __attribute__((noinline)) void kd_output(const int i, const int s, co
             if (lrow && KD_OUT) __builtin_nontemporal_store(Lv, lrow + j);
         }
     }
-    wait_stores();  // wpr of phase B visible to the whole workgroup
     // planned launches: the next job is taken here (queue order is unchanged: a job is still
     // taken after every job it seeds from)
     const bool queued = sm->jobs != nullptr;
@@ -587,7 +622,7 @@ __device__ __attribute__((noinline)) void kd_output(const int i, const int s, co
     KD_ACC(18);
     // dist is dead: its LDS becomes the parent array
     uint16_t* parv = dist;
-    if (g.walk && rrow) {
+    if (walks) {
         // ---- C': reliability by walking each target's tree path in LDS -------------
         // parv u16 + rix u8 (index of the parent arc's reliability) + rtab in LDS; each
         // target walks <= KD_MAXD arcs to the source, then folds the product source-first

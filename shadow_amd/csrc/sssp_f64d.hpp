@@ -223,7 +223,9 @@ __device__ __attribute__((always_inline)) int kfh_levels(int n, int s, int tid, 
 }
 
 template <int B, bool H = false>
-__global__ __launch_bounds__(B) void sssp_f64d_kernel(DevF64D g, const int* __restrict__ src, int ns,
+// (amdgpu_waves_per_eu(4): four 256-thread workgroups per CU need 128 VGPRs or fewer; the
+// 256-thread build came out at 129, three waves per SIMD, so only three workgroups per CU)
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sssp_f64d_kernel(DevF64D g, const int* __restrict__ src, int ns,
                                                       const int* __restrict__ tgt, int nt, long long ld,
                                                       double* __restrict__ lat_out, double* __restrict__ rel_out,
                                                       double* __restrict__ row_min, int* __restrict__ err,

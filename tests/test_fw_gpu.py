@@ -231,3 +231,28 @@ def test_fw_fused_panels_equal_separate_launches(monkeypatch, cfg):
         out.append((lat, rel, mn))
     for o in out[1:]:
         assert torch.equal(out[0][0], o[0]) and torch.equal(out[0][1], o[1]) and torch.equal(out[0][2], o[2])
+
+
+@pytest.mark.parametrize("case", ["k200_dense_r", "manyrel"])
+def test_fw_rows_reliability_paths(oracle_mod, monkeypatch, case):
+    """fw_rows' two ways to a parent arc's reliability (round 5): by its index in a dense u8
+    matrix into a table of the distinct reliabilities (<= 255 of them, the default) or by the
+    dense n x n f64 table -- forced (SHD_ROUTE_FWDENSER=1), or because a graph has more distinct
+    reliabilities than an index holds ("manyrel": a continuous loss per edge)."""
+    import dataclasses
+    from shadow_amd import route
+    if case == "k200_dense_r":
+        monkeypatch.setenv("SHD_ROUTE_FWDENSER", "1")
+        g = complete_graph(200, seed=5)
+    else:
+        monkeypatch.delenv("SHD_ROUTE_FWDENSER", raising=False)
+        g = internet_like(300, 3, seed=19)
+        rng = np.random.default_rng(4)
+        g = dataclasses.replace(g, packetloss=rng.random(g.m) * 0.01)
+    eng = route.RouteEngine(g)
+    T = np.arange(g.n, dtype=np.int32)
+    S = T[::2]
+    lat, rel, mn = _fw_rows(eng, S, T)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(S, T, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(rel, orel)

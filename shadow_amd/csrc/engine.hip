@@ -148,6 +148,8 @@ struct shd_route {
     long long lm_rs = 0;
     uint16_t* d_lm_drow = nullptr;  // the landmark rows in the row-store format (device)
     uint32_t* d_lm_prow = nullptr;
+    char* d_hub_ws = nullptr;       // the planner's hub-row launch scratch (kept: a free costs a sync)
+    size_t hub_ws_bytes = 0;
     int sel = 0;  // selected SSSP kernel: 0 f64, 1 K32, 2 KB+K2, 4 KD, 5 KF (3: the retired K16)
     // KF (fractional latencies, LDS-resident f64 delta-stepping)
     int kf_block = 0, kf_slots = 0;
@@ -951,6 +953,7 @@ void shd_route_destroy(shd_route_t* c) {
     if (c->d_fwkey) (void)hipFree(c->d_fwkey);
     if (c->d_lm_drow) (void)hipFree(c->d_lm_drow);
     if (c->d_lm_prow) (void)hipFree(c->d_lm_prow);
+    if (c->d_hub_ws) (void)hipFree(c->d_hub_ws);
     for (void* p : c->allocs) (void)hipFree(p);
     delete c;
 }
@@ -1139,27 +1142,38 @@ struct LmChoice {
     uint32_t rec[3];
     int pad[2];
 };
-__global__ void plan_landmark_kernel(const uint16_t* __restrict__ drow, const uint32_t* __restrict__ prow, long long rs,
-                                     const int* __restrict__ lmv, int nland, const int* __restrict__ srcq, int nq, int klm,
-                                     int n, LmChoice* __restrict__ out) {
-    const int lane = threadIdx.x & 63;
-    const int q = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (q >= nq) return;  // the whole wave
-    const int s = srcq[q];
+__device__ inline LmChoice lm_pick(const uint16_t* __restrict__ drow, const uint32_t* __restrict__ prow, long long rs,
+                                   const int* __restrict__ lmv, int nland, int s, int klm, int n, int lane) {
     LmChoice o;
     o.m = 0; o.pad[0] = o.pad[1] = 0;
     for (int k = 0; k < 3; k++) { o.l[k] = 0; o.d[k] = 0; o.rec[k] = 0u; }
-    uint32_t prev = 0u;  // picks come in increasing (d, l) order: the next one is past prev
-    for (int k = 0; k < klm && k < 3; k++) {
-        uint32_t best = 0xFFFFFFFFu;
-        for (int l = lane; l < nland; l += 64) {
-            const uint32_t d = drow[(long long)l * rs + s];
-            const uint32_t key = (d << 16) | (uint32_t)l;
-            if (d != 0xFFFFu && (k == 0 || key > prev) && key < best) best = key;
+    // each lane's three smallest keys (d << 16 | l) over its landmarks l = lane + 64 j, read
+    // once; the wave's k-th pick is then the minimum over the lanes' lists past the (k-1)-th
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    uint32_t c0 = NONE, c1 = NONE, c2 = NONE;
+    for (int l0 = 0; l0 < nland; l0 += 64 * 8) {
+        uint32_t d8[8];
+#pragma unroll
+        for (int h = 0; h < 8; h++) {
+            const int l = l0 + 64 * h + lane;
+            d8[h] = l < nland ? drow[(long long)l * rs + s] : 0xFFFFu;
         }
+#pragma unroll
+        for (int h = 0; h < 8; h++) {
+            const uint32_t key = (d8[h] << 16) | (uint32_t)(l0 + 64 * h + lane);
+            if (d8[h] == 0xFFFFu) continue;
+            if (key < c2) {
+                c2 = key;
+                if (c2 < c1) { const uint32_t t = c1; c1 = c2; c2 = t; }
+                if (c1 < c0) { const uint32_t t = c0; c0 = c1; c1 = t; }
+            }
+        }
+    }
+    for (int k = 0; k < klm && k < 3; k++) {
+        uint32_t best = c0;
         for (int off = 32; off > 0; off >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, off));
-        if (best == 0xFFFFFFFFu) break;
-        prev = best;
+        if (best == NONE) break;
+        if (c0 == best) { c0 = c1; c1 = c2; c2 = NONE; }  // (keys are unique: one lane owns it)
         const int l = (int)(best & 0xFFFFu), L = lmv[l];
         uint32_t rec = KD_SRC_MARK;
         if (L != s) {
@@ -1171,7 +1185,84 @@ __global__ void plan_landmark_kernel(const uint16_t* __restrict__ drow, const ui
         o.l[k] = l; o.d[k] = (int)(best >> 16); o.rec[k] = rec;
         o.m = k + 1;
     }
+    return o;
+}
+
+__global__ void plan_landmark_kernel(const uint16_t* __restrict__ drow, const uint32_t* __restrict__ prow, long long rs,
+                                     const int* __restrict__ lmv, int nland, const int* __restrict__ srcq, int nq, int klm,
+                                     int n, LmChoice* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (q >= nq) return;  // the whole wave
+    const LmChoice o = lm_pick(drow, prow, rs, lmv, nland, srcq[q], klm, n, lane);
     if (lane == 0) out[q] = o;
+}
+
+// Landmark-only plans built on the device (round 5): the queue order and the job records
+// without a host round trip.  The order is the host rule's: descending (closeness, vertex,
+// position), closeness = the sum of the first nclose hub rows' distances (unreached: the
+// largest key).  Keys are unique, so a job's queue slot is the number of larger keys (a rank
+// sort: every workgroup holds all keys in LDS, nq <= PLAN_DEV_MAXJ; ~20 us at C3, where a
+// one-workgroup bitonic sort took ~0.3 ms).
+constexpr int PLAN_DEV_MAXJ = 16384;
+__global__ void plan_lmall_keys_kernel(const uint16_t* __restrict__ drow, long long rs, int nclose,
+                                       const int* __restrict__ srcq, int nq, unsigned long long* __restrict__ keys) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const int s = srcq[i];
+    unsigned sum = 0;
+    bool unr = false;
+    for (int q = 0; q < nclose; q++) {
+        const unsigned d = drow[(long long)q * rs + s];
+        unr = unr || d == 0xFFFFu;
+        sum += d;
+    }
+    if (unr) sum = (1u << 20) - 1;  // (16 finite distances sum below it)
+    keys[i] = ((unsigned long long)sum << 40) | ((unsigned long long)s << 24) | (unsigned long long)i;
+}
+__global__ __launch_bounds__(256) void plan_lmall_rank_kernel(const unsigned long long* __restrict__ keys, int nq,
+                                                              int* __restrict__ slot) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long rkeys[];
+    for (int j = threadIdx.x; j < nq; j += blockDim.x) rkeys[j] = keys[j];
+    __syncthreads();
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const unsigned long long k = rkeys[i];
+    int r = 0;
+    for (int j = 0; j < nq; j++) r += rkeys[j] > k;  // (same j across the wave: an LDS broadcast)
+    slot[i] = r;
+}
+
+// one wave per job i (jobs in position order, so that a workgroup's waves read neighbouring
+// columns of the landmark rows, and consecutive workgroups on one XCD: blockIdx.x % 8 picks
+// the XCD, which takes one contiguous eighth of the jobs), the landmark seeds of the row
+// (lm_pick) written as its KDJob at its queue slot.  row = the position's index in this
+// rank's rows, seeds = landmark slots (the borrowed store holds the landmark rows only).
+// nroots counts the jobs left unseeded (no landmark reaches s).
+__global__ void plan_lmall_jobs_kernel(const uint16_t* __restrict__ drow, const uint32_t* __restrict__ prow, long long rs,
+                                       const int* __restrict__ lmv, int nland, const int* __restrict__ srcq,
+                                       const int* __restrict__ slot, int nq, int klm, int n, KDJob* __restrict__ out,
+                                       int* __restrict__ nroots) {
+    const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
+    const int per = gridDim.x / 8;  // (the grid is a multiple of 8 workgroups)
+    const int b = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);  // (XCD-contiguous block order)
+    const int i = b * wpb + (threadIdx.x >> 6);
+    if (i >= nq) return;  // the whole wave
+    const int s = srcq[i];
+    const LmChoice o = lm_pick(drow, prow, rs, lmv, nland, s, klm, n, lane);
+    if (lane == 0) {
+        KDJob J;
+        J.row = i; J.s = s; J.store = -1; J.nseed = o.m;
+        for (int k = 0; k < KD_SEEDS; k++) {
+            const bool on = k < o.m;
+            J.seed[k] = on ? o.l[k] : 0;
+            J.u[k] = on ? lmv[o.l[k]] : 0;
+            J.wr[k] = on ? o.d[k] : 0;
+            J.rec[k] = on ? (int)o.rec[k] : 0;
+        }
+        out[slot[i]] = J;
+        if (o.m == 0) atomicAdd(nroots, 1);
+    }
 }
 
 // lexicographic minimum of (x, u, t) over the wave (t: a tie-breaking key, arc or record)
@@ -1432,9 +1523,13 @@ struct shd_route_plan {
     uint16_t* d_drow = nullptr;    // row store
     uint32_t* d_prow = nullptr;
     uint64_t store_bytes = 0;
+    bool store_borrowed = false;   // d_drow / d_prow are the context's landmark rows (device-built landmark-only plans)
     ~shd_route_plan() {
-        for (void* q : {(void*)d_jobs, (void*)d_next, (void*)d_src, (void*)d_drow, (void*)d_prow})
+        for (void* q : {(void*)d_jobs, (void*)d_next, (void*)d_src})
             if (q) (void)hipFree(q);
+        if (!store_borrowed)
+            for (void* q : {(void*)d_drow, (void*)d_prow})
+                if (q) (void)hipFree(q);
     }
 };
 
@@ -1485,11 +1580,17 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, D
     // of those can share it even if one is still in flight.
     const bool hub1024 = c->kd_hub_block > 0 && k <= 256;
     const int grid = std::min(k, hub1024 ? 256 : std::max(256, c->kd_slots));
-    DevBuf dj, dn, dw;
+    DevBuf dj, dn;
     if (dj.alloc(sizeof(KDJob) * k) || dd.alloc(sizeof(uint16_t) * (size_t)rs * k) ||
-        dp.alloc(sizeof(uint32_t) * (size_t)rs * k) || dn.alloc(sizeof(int) * (1 + (size_t)k)) ||
-        dw.alloc(c->kd_stride * (size_t)grid))
+        dp.alloc(sizeof(uint32_t) * (size_t)rs * k) || dn.alloc(sizeof(int) * (1 + (size_t)k)))
         return SHD_ROUTE_ENOMEM;
+    const size_t wsb = c->kd_stride * (size_t)grid;
+    if (c->hub_ws_bytes < wsb) {
+        if (c->d_hub_ws) (void)hipFree(c->d_hub_ws);
+        c->d_hub_ws = nullptr; c->hub_ws_bytes = 0;
+        if (hipMalloc((void**)&c->d_hub_ws, wsb) != hipSuccess) { c->d_hub_ws = nullptr; return SHD_ROUTE_ENOMEM; }
+        c->hub_ws_bytes = wsb;
+    }
     // (errors of earlier launches are reported by their own sync, not by this plan)
     if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
     int rc = take_err(c);
@@ -1503,7 +1604,7 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, D
     g.drow = (const uint16_t*)dd.p; g.drow_out = (uint16_t*)dd.p; g.prow = (uint32_t*)dp.p; g.rstride = rs;
     g.done = (int*)dn.p + 1;
     if ((rc = kd_launch(c, g, (int*)dn.p, nullptr, k, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, true,
-                        (char*)dw.p, grid, hub1024)))
+                        c->d_hub_ws, grid, hub1024)))
         return rc;
     if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
     if ((rc = take_err(c))) return rc;
@@ -1527,23 +1628,40 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, D
 // plans' roots, kept on the device in the row-store format (a plan copies them device to
 // device).  (Before round 3: 16 pseudo-random closeness rows, then the 16 (64) most central
 // vertices' rows in a second launch.)
-int ensure_hub_rows(shd_route* c, int k) {
+int ensure_hub_rows(shd_route* c, int k, bool host_close = true) {
     const int n = c->n;
     k = std::min(n, std::max(k, 16));
-    if ((int)c->lm_v.size() >= k) return SHD_ROUTE_OK;
-    std::vector<int> ord(n);
-    std::iota(ord.begin(), ord.end(), 0);
-    auto deg = [&](int v) { return c->h_row.empty() ? 0 : c->h_row[v + 1] - c->h_row[v]; };
-    std::partial_sort(ord.begin(), ord.begin() + k, ord.end(), [&](int a, int b) {
-        return deg(a) != deg(b) ? deg(a) > deg(b) : a < b;
-    });
-    std::vector<int> lv(ord.begin(), ord.begin() + k);
-    std::vector<uint16_t> hd;
-    DevBuf dd, dp;
-    const int L = std::min(k, 16);
-    int rc = device_store_rows(c, lv, dd, dp, hd, L);
-    if (rc) return rc;
+    const int L = std::min(n, 16);  // the closeness rows: the first 16 hub rows
     const long long rs = kd_row_stride(n);
+    std::vector<uint16_t> hd;
+    if ((int)c->lm_v.size() < k) {
+        std::vector<int> ord(n);
+        std::iota(ord.begin(), ord.end(), 0);
+        auto deg = [&](int v) { return c->h_row.empty() ? 0 : c->h_row[v + 1] - c->h_row[v]; };
+        std::partial_sort(ord.begin(), ord.begin() + k, ord.end(), [&](int a, int b) {
+            return deg(a) != deg(b) ? deg(a) > deg(b) : a < b;
+        });
+        std::vector<int> lv(ord.begin(), ord.begin() + k);
+        DevBuf dd, dp;
+        int rc = device_store_rows(c, lv, dd, dp, hd, host_close ? L : 0);
+        if (rc) return rc;
+        // (the previous rows are retired, not freed: a device-built plan may still read them)
+        if (c->d_lm_drow) c->allocs.push_back(c->d_lm_drow);
+        if (c->d_lm_prow) c->allocs.push_back(c->d_lm_prow);
+        c->d_lm_drow = (uint16_t*)dd.p; dd.p = nullptr;
+        c->d_lm_prow = (uint32_t*)dp.p; dp.p = nullptr;
+        c->lm_v = lv;
+        c->lm_hd.clear();  // (host copies on demand: ensure_lm_host)
+        c->lm_hp.clear();
+        c->lm_rs = rs;
+        c->close.clear();
+        if (!host_close) return SHD_ROUTE_OK;
+    } else {
+        if (!host_close || (int)c->close.size() == n) return SHD_ROUTE_OK;
+        hd.resize((size_t)rs * L);  // (rows computed by a device-built plan: their closeness now)
+        if (hipMemcpy(hd.data(), c->d_lm_drow, sizeof(uint16_t) * hd.size(), hipMemcpyDeviceToHost) != hipSuccess)
+            return SHD_ROUTE_EDEVICE;
+    }
     c->close.assign(n, 0.0);
     for (int v = 0; v < n; v++) {
         double sum = 0;
@@ -1553,14 +1671,6 @@ int ensure_hub_rows(shd_route* c, int k) {
         }
         c->close[v] = sum / L;
     }
-    if (c->d_lm_drow) (void)hipFree(c->d_lm_drow);
-    if (c->d_lm_prow) (void)hipFree(c->d_lm_prow);
-    c->d_lm_drow = (uint16_t*)dd.p; dd.p = nullptr;
-    c->d_lm_prow = (uint32_t*)dp.p; dp.p = nullptr;
-    c->lm_v = lv;
-    c->lm_hd.clear();  // (host copies on demand: ensure_lm_host)
-    c->lm_hp.clear();
-    c->lm_rs = rs;
     return SHD_ROUTE_OK;
 }
 int ensure_landmarks(shd_route* c, int k) { return ensure_hub_rows(c, k); }
@@ -1623,6 +1733,60 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     if (lm_all) nland = std::min(n, PLAN_LMALL_COUNT);
     else if (world > 1 && !c->multigraph) nland = std::min(n, 256);
     if (const char* e = getenv("SHD_ROUTE_LANDMARKS")) nland = c->multigraph ? 0 : std::max(0, std::min(atoi(e), n));
+    // A landmark-only plan is built on the device (round 5): the hub rows without their host
+    // closeness, then one kernel for the queue order and one for the job records, and one
+    // sync at the end; the plan borrows the context's landmark rows as its row store (no
+    // kept rows, no copies).  C3: plan 2.6 -> ~1.3 ms.  The host build below stays for
+    // SHD_ROUTE_GPUCHOICE=0 / SHD_ROUTE_LMALL_REV=0 / SHD_ROUTE_PLANDEV=0 and larger ranks.
+    auto env_off = [](const char* k) { const char* e = getenv(k); return e && atoi(e) == 0; };
+    const int nmine = ns > rank ? (ns - rank + world - 1) / world : 0;
+    if (want && lm_all && nland > 0 && nmine >= 2 && nmine <= PLAN_DEV_MAXJ && !env_off("SHD_ROUTE_GPUCHOICE") &&
+        !env_off("SHD_ROUTE_LMALL_REV") && !env_off("SHD_ROUTE_PLANDEV")) {
+        int rc = ensure_hub_rows(c, nland, false);
+        if (rc) return rc;
+        t_close = since();
+        std::vector<int> sq;
+        sq.reserve(nmine);
+        for (int p = rank; p < ns; p += world) { P->row_pos.push_back(p); sq.push_back(src[p]); }
+        const int nj = (int)sq.size();
+        int klm = KD_SEEDS;
+        if (const char* e = getenv("SHD_ROUTE_LMSEEDS")) klm = std::max(1, std::min(KD_SEEDS, atoi(e)));
+        DevBuf dsq, dlv, dslot, dkey;
+        if (dsq.alloc(sizeof(int) * nj) || dlv.alloc(sizeof(int) * nland) || dslot.alloc(sizeof(int) * nj) ||
+            dkey.alloc(sizeof(unsigned long long) * nj) ||
+            hipMalloc((void**)&P->d_jobs, sizeof(KDJob) * (size_t)nj) != hipSuccess ||
+            hipMalloc((void**)&P->d_next, sizeof(int) * (1 + (size_t)nland)) != hipSuccess)
+            return SHD_ROUTE_ENOMEM;
+        if (hipMemcpy(dsq.p, sq.data(), sizeof(int) * nj, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(dlv.p, c->lm_v.data(), sizeof(int) * nland, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemset(P->d_next, 0, sizeof(int)) != hipSuccess)
+            return SHD_ROUTE_EDEVICE;
+        const long long rs = kd_row_stride(n);
+        if ((rc = hip_check(hipFuncSetAttribute((const void*)plan_lmall_rank_kernel,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 8 * nj))))
+            return rc;
+        const int nb = (nj + 255) / 256;
+        hipLaunchKernelGGL(plan_lmall_keys_kernel, dim3(nb), dim3(256), 0, 0, c->d_lm_drow, rs, std::min(n, 16),
+                           (const int*)dsq.p, nj, (unsigned long long*)dkey.p);
+        hipLaunchKernelGGL(plan_lmall_rank_kernel, dim3(nb), dim3(256), 8 * nj, 0, (const unsigned long long*)dkey.p, nj,
+                           (int*)dslot.p);
+        hipLaunchKernelGGL(plan_lmall_jobs_kernel, dim3(8 * (((nj + 15) / 16 + 7) / 8)), dim3(1024), 0, 0, c->d_lm_drow, c->d_lm_prow, rs,
+                           (const int*)dlv.p, nland, (const int*)dsq.p, (const int*)dslot.p, nj, klm, n, P->d_jobs,
+                           P->d_next);
+        int nroots = 0;
+        if ((rc = hip_check(hipGetLastError()))) return rc;
+        if (hipMemcpy(&nroots, P->d_next, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return SHD_ROUTE_EDEVICE;
+        if ((rc = take_err(c))) return rc;
+        P->d_drow = c->d_lm_drow; P->d_prow = c->d_lm_prow; P->store_borrowed = true;
+        P->nslots = 0; P->nland = nland; P->store_bytes = 0; P->nroots = nroots; P->seeded = 1;
+        P->lvl_off = {0, nj};
+        if (getenv("SHD_ROUTE_PLAN_DEBUG"))
+            fprintf(stderr, "plan world %d rank %d: jobs %d levels 1, device-built landmark-only plan (%d landmarks, "
+                    "%d unseeded): hub rows done %.2f ms, plan total %.2f ms\n", world, rank, nj, nland, nroots,
+                    1e3 * t_close, 1e3 * since());
+        *out = P.release();
+        return SHD_ROUTE_OK;
+    }
     if (want) {
         const int rc = ensure_hub_rows(c, nland);
         if (rc) return rc;

@@ -87,6 +87,9 @@ constexpr uint32_t KD_SRC_MARK = 0xFFFFFFFEu;  // parent record of the source it
 #define KD_NSEEDS 3  // seeds per row at most (KDJob holds up to 3; the planner's default: engine.hip)
 #endif
 constexpr int KD_SEEDS = KD_NSEEDS;
+#ifndef KD_PCOPY_PIPE
+#define KD_PCOPY_PIPE 0  // phase C parent copy: > 0: that many 16-B records per lane per half-trip, the next half-trip's loads issued before this one's copy
+#endif
 #ifndef KD_JUMPS
 #define KD_JUMPS 1  // phase C pointer-jumping rounds before the walks (C4: 0: 50.5 ms, 1: 48.6, 2: 49.3, 3: 51.5, to convergence: 54.2)
 #endif
@@ -637,13 +640,14 @@ __device__ __attribute__((noinline)) void kd_output(const int i, const int s, co
         // vertices per trip: C4 takes 4 trips instead of the 7 of one 4-B load per vertex)
         // (wpr rows hold n + 8 records, dist n + 1 entries padded to 16 B: the last group's
         // reads stay inside; its writes past n are dropped)
-        auto copy_trip = [&](const int v0, const kd_u4 (&pr)[4]) __attribute__((always_inline)) {
-            uint2 dv[4];
+        auto copy_trip = [&](const int v0, const auto& pr) __attribute__((always_inline)) {
+            constexpr int NQ = sizeof(pr) / sizeof(pr[0]);
+            uint2 dv[NQ];
 #pragma unroll
-            for (int q = 0; q < 4; q++) dv[q] = *reinterpret_cast<const uint2*>(dist + min(v0 + q * 4 * B, (n - 1) & ~3));
+            for (int q = 0; q < NQ; q++) dv[q] = *reinterpret_cast<const uint2*>(dist + min(v0 + q * 4 * B, (n - 1) & ~3));
             // (each thread overwrites only the dist entries it read itself)
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
+            for (int q = 0; q < NQ; q++) {
                 const int vb = v0 + q * 4 * B;
                 if (vb >= n) continue;
                 uint32_t pw[2] = {0u, 0u}, rw = 0u;
@@ -672,16 +676,35 @@ __device__ __attribute__((noinline)) void kd_output(const int i, const int s, co
                 }
             }
         };
-        auto load_trip = [&](const int v0, kd_u4 (&pr)[4]) __attribute__((always_inline)) {
+        auto load_trip = [&](const int v0, auto& pr) __attribute__((always_inline)) {
+            constexpr int NQ = sizeof(pr) / sizeof(pr[0]);
 #pragma unroll
-            for (int q = 0; q < 4; q++)
+            for (int q = 0; q < NQ; q++)
                 pr[q] = *reinterpret_cast<const KD_GLOBAL kd_u4*>(wpr + min(v0 + q * 4 * B, (n - 1) & ~3));
         };
+#if KD_PCOPY_PIPE
+        {
+            // the next trip's records in flight while this one is copied
+            constexpr int PQ = KD_PCOPY_PIPE;  // (records per lane and half-trip)
+            kd_u4 pa[PQ], pb[PQ];
+            int v0 = 4 * tid;
+            if (v0 < n) load_trip(v0, pa);
+            for (; v0 < n; v0 += 8 * PQ * B) {
+                const int v1 = v0 + 4 * PQ * B;
+                if (v1 < n) load_trip(v1, pb);
+                copy_trip(v0, pa);
+                if (v1 >= n) break;
+                if (v1 + 4 * PQ * B < n) load_trip(v1 + 4 * PQ * B, pa);
+                copy_trip(v1, pb);
+            }
+        }
+#else
         for (int v0 = 4 * tid; v0 < n; v0 += 16 * B) {
             kd_u4 pr[4];
             load_trip(v0, pr);
             copy_trip(v0, pr);
         }
+#endif
         __syncthreads();
         // Lossless arcs (slot KD_ONE: exactly 1.0) multiply as exact no-ops, so a chain only
         // needs the lossy ones (20% of the arcs on the BASELINE topologies): parv[v] becomes the

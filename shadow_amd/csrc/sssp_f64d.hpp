@@ -395,10 +395,12 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                 // the slice's non-empty entries are lanes 0 .. R-1)
                 const bool valid = q < qn;
                 unsigned long long* wm4 = sm->wmark[tid >> 6];
-                for (int p0 = 0; p0 < total; p0 += 4 * 64) {
-                    // owners: each entry marks its start in the window (of 64 positions) that
-                    // holds it; the owner of position p is the entries starting before the
-                    // window plus the marks at or below p, minus one
+                // one trip: owners, then the trip's arc loads issued (not waited on).  owners:
+                // each entry marks its start in the window (of 64 positions) that holds it; the
+                // owner of position p is the entries starting before the window plus the marks at
+                // or below p, minus one
+                auto stage = [&](int p0, int (&aq)[4], int (&uq)[4], int (&vq)[4], double (&wq)[4],
+                                 double (&duq)[4]) __attribute__((always_inline)) {
                     if (lane < 4) wm4[lane] = 0ull;
                     __builtin_amdgcn_wave_barrier();
                     const int rel = excl - p0;
@@ -413,8 +415,6 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         lo[r] = max(0, __popcll(before) + __popcll(mk & upto) - 1);
                     }
                     __builtin_amdgcn_wave_barrier();  // (the marks are read before the next trip clears them)
-                    int aq[4], uq[4], vq[4];
-                    double wq[4], duq[4];
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         const int p = p0 + r * 64 + lane;
@@ -430,18 +430,10 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         vq[r] = g.col[a];
                         wq[r] = g.w[a];
                     }
-                    if (tid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    KF_ACC(14);
-                    // (KFH: the key filter, then the candidates' HBM atomics issued together)
-                    unsigned long long hold[4];
-                    if constexpr (H) {
-#pragma unroll
-                        for (int r = 0; r < 4; r++) {
-                            const unsigned long long nb = as_u(duq[r] + wq[r]);
-                            const bool cand = aq[r] >= 0 && kf_key(nb) <= keyl[vq[r]];
-                            hold[r] = cand ? atomicMin(&dist[vq[r]], nb) : 0ull;
-                        }
-                    }
+                };
+                // a trip's relaxations (KFH: hold = the candidates' HBM atomicMin results)
+                auto relax = [&](const int (&aq)[4], const int (&uq)[4], const int (&vq)[4], const double (&wq)[4],
+                                 const double (&duq)[4], const unsigned long long (&hold)[4]) __attribute__((always_inline)) {
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         if (aq[r] < 0) continue;
@@ -470,6 +462,64 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                                 }
                             }
                         }
+                    }
+                };
+                if constexpr (H) {
+                    // KFH, software-pipelined: a trip's HBM atomics are in flight while the next
+                    // trip's owners are found and its arc loads issued; its relaxations (which
+                    // wait for the atomics' results) come after.  Past the filter a trip keeps
+                    // only v, its candidate distance nb and the atomic's result.
+                    int aq[4], uq[4], vq[4];
+                    double wq[4], duq[4];
+                    stage(0, aq, uq, vq, wq, duq);
+                    for (int p0 = 0;; p0 += 4 * 64) {
+#ifdef SHD_STAMPS
+                        if (tid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        KF_ACC(14);
+#endif
+                        // the key filter, then the candidates' HBM atomics issued together
+                        unsigned long long hold[4], nbq[4];
+                        int vc[4];
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            nbq[r] = as_u(duq[r] + wq[r]);
+                            const bool cand = aq[r] >= 0 && kf_key(nbq[r]) <= keyl[vq[r]];
+                            vc[r] = cand ? vq[r] : -1;
+                            hold[r] = cand ? atomicMin(&dist[vq[r]], nbq[r]) : 0ull;
+                        }
+                        const bool more = p0 + 4 * 64 < total;  // (wave-uniform)
+                        if (more) stage(p0 + 4 * 64, aq, uq, vq, wq, duq);
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const int v = vc[r];
+                            const unsigned long long nb = nbq[r];
+                            if (v >= 0 && nb < hold[r]) {
+                                kf_key_min(keyl, v, kf_key(nb));
+                                const unsigned long long bit = 1ull << (v & 63);
+                                if (as_d(nb) < T) {  // this bucket: straight back into the ring
+                                    if (!(atomicOr(&inq[v >> 6], bit) & bit)) {
+                                        const unsigned at = (unsigned)atomicAdd(&sm->qtail, 1);
+                                        if (at - qhead < R) ring[at % R] = (uint16_t)v;
+                                        else if (B < 1024) atomicOr(&sm->ovf, 1 << rpar);
+                                        else sm->ovf = 1;  // (a dropped push: see the relax above)
+                                    }
+                                } else {
+                                    atomicOr(&pend[v >> 6], bit);
+                                    atomicMin(&wmin[v >> 6], nb);
+                                }
+                            }
+                        }
+                        if (!more) break;
+                    }
+                } else {
+                    for (int p0 = 0; p0 < total; p0 += 4 * 64) {
+                        int aq[4], uq[4], vq[4];
+                        double wq[4], duq[4];
+                        stage(p0, aq, uq, vq, wq, duq);
+                        if (tid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        KF_ACC(14);
+                        const unsigned long long hold[4] = {0ull, 0ull, 0ull, 0ull};
+                        relax(aq, uq, vq, wq, duq, hold);
                     }
                 }
             }

@@ -123,9 +123,12 @@ def test_partition_forest_device_equals_host(kd, cfg, world):
         dev.append((p.info, p.positions.copy()))
         p.close()
     kd.setenv("SHD_ROUTE_GPUCHOICE", "0")
+
+    def shape(info):  # (a device-built landmark-only plan borrows its store: store_bytes 0)
+        return {k: v for k, v in info.items() if k != "store_bytes"}
     for r in range(world):
         p = eng.plan(T, world, r)
-        assert p.info == dev[r][0]
+        assert shape(p.info) == shape(dev[r][0])
         assert np.array_equal(p.positions, dev[r][1])
         p.close()
 
@@ -431,8 +434,9 @@ def test_landmark_only_plans(oracle_mod, monkeypatch, world, vloss):
     most 1.5 rows per workgroup slot): every row seeded from its 3 nearest of the landmark
     rows (1024 of the 3000 vertices), all at level 0, a rank taking every
     world-th row.  Bit-exact against the oracle,
-    the ranks covering the source list exactly once; the landmark seeds chosen on the device
-    equal the host's choice (SHD_ROUTE_GPUCHOICE=0)."""
+    the ranks covering the source list exactly once; the device-built plan (order and jobs
+    on the device, the landmark rows borrowed as the store) gives the rows of the host builds
+    (SHD_ROUTE_GPUCHOICE=0: host seeds; SHD_ROUTE_PLANDEV=0: device seeds, host jobs)."""
     from shadow_amd import route
     from shadow_amd.graph import internet_like
     monkeypatch.setenv("SHD_ROUTE_KERNEL", "kd")  # (a 3000-vertex graph would take KBF)
@@ -465,11 +469,17 @@ def test_landmark_only_plans(oracle_mod, monkeypatch, world, vloss):
             assert np.array_equal(rel, orel)
         seen.extend(pos.tolist())
         plan.close()
-        monkeypatch.setenv("SHD_ROUTE_GPUCHOICE", "0")
-        plan = eng.plan(T, world, r)
-        assert plan.info == info and np.array_equal(plan.positions, pos)
-        lat2, rel2, _ = _plan_rows(eng, plan, T)
-        assert np.array_equal(lat2, lat) and np.array_equal(rel2, rel)
-        plan.close()
-        monkeypatch.delenv("SHD_ROUTE_GPUCHOICE")
+        # the device-built plan (default) borrows the landmark rows as its store; the host
+        # builds (host seeds, or device seeds with host jobs) copy them into their own
+        assert info["store_bytes"] == 0, info
+        for knob in ("SHD_ROUTE_GPUCHOICE", "SHD_ROUTE_PLANDEV"):
+            monkeypatch.setenv(knob, "0")
+            plan = eng.plan(T, world, r)
+            i2 = dict(plan.info)
+            assert i2.pop("store_bytes") > 0 and i2 == {k: v for k, v in info.items() if k != "store_bytes"}, (knob, i2)
+            assert np.array_equal(plan.positions, pos)
+            lat2, rel2, _ = _plan_rows(eng, plan, T)
+            assert np.array_equal(lat2, lat) and np.array_equal(rel2, rel)
+            plan.close()
+            monkeypatch.delenv(knob)
     assert sorted(seen) == list(range(len(T)))

@@ -87,9 +87,6 @@ constexpr uint32_t KD_SRC_MARK = 0xFFFFFFFEu;  // parent record of the source it
 #define KD_NSEEDS 3  // seeds per row at most (KDJob holds up to 3; the planner's default: engine.hip)
 #endif
 constexpr int KD_SEEDS = KD_NSEEDS;
-#ifndef KD_PCOPY_PIPE
-#define KD_PCOPY_PIPE 0  // phase C parent copy: > 0: that many 16-B records per lane per half-trip, the next half-trip's loads issued before this one's copy
-#endif
 #ifndef KD_JUMPS
 #define KD_JUMPS 1  // phase C pointer-jumping rounds before the walks (C4: 0: 50.5 ms, 1: 48.6, 2: 49.3, 3: 51.5, to convergence: 54.2)
 #endif
@@ -636,8 +633,8 @@ __device__ __attribute__((noinline)) void kd_output(const int i, const int s, co
         double* rtl = reinterpret_cast<double*>(smem + L.rtabl);
         for (int k = tid; k < 256; k += B)
             rtl[k] = k < g.nrtab ? g.rtab[k] : k == KD_ONE ? 1.0 : NAN;
-        // 4 consecutive vertices per 16-B record load, 4 loads in flight per thread (16 K
-        // vertices per trip: C4 takes 4 trips instead of the 7 of one 4-B load per vertex)
+        // 4 consecutive vertices per 16-B record load, 2 loads per half-trip and thread (8 K
+        // vertices), the next half-trip's loads issued before this one's copy
         // (wpr rows hold n + 8 records, dist n + 1 entries padded to 16 B: the last group's
         // reads stay inside; its writes past n are dropped)
         auto copy_trip = [&](const int v0, const auto& pr) __attribute__((always_inline)) {
@@ -682,10 +679,11 @@ __device__ __attribute__((noinline)) void kd_output(const int i, const int s, co
             for (int q = 0; q < NQ; q++)
                 pr[q] = *reinterpret_cast<const KD_GLOBAL kd_u4*>(wpr + min(v0 + q * 4 * B, (n - 1) & ~3));
         };
-#if KD_PCOPY_PIPE
         {
-            // the next trip's records in flight while this one is copied
-            constexpr int PQ = KD_PCOPY_PIPE;  // (records per lane and half-trip)
+            // the next half-trip's records in flight while this one is copied (two 16-B
+            // records per lane and half-trip: four, or one-trip lookahead at four, raised the
+            // callee saves, kernel scratch 152 -> 260 B/lane; C3 2.09 -> 2.02 ms, C4 the same)
+            constexpr int PQ = 2;
             kd_u4 pa[PQ], pb[PQ];
             int v0 = 4 * tid;
             if (v0 < n) load_trip(v0, pa);
@@ -698,13 +696,6 @@ __device__ __attribute__((noinline)) void kd_output(const int i, const int s, co
                 copy_trip(v1, pb);
             }
         }
-#else
-        for (int v0 = 4 * tid; v0 < n; v0 += 16 * B) {
-            kd_u4 pr[4];
-            load_trip(v0, pr);
-            copy_trip(v0, pr);
-        }
-#endif
         __syncthreads();
         // Lossless arcs (slot KD_ONE: exactly 1.0) multiply as exact no-ops, so a chain only
         // needs the lossy ones (20% of the arcs on the BASELINE topologies): parv[v] becomes the

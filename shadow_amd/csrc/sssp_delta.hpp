@@ -677,7 +677,10 @@ __device__ __attribute__((noinline)) void kd_output(const int i, const int s, co
             constexpr int NQ = sizeof(pr) / sizeof(pr[0]);
 #pragma unroll
             for (int q = 0; q < NQ; q++)
-                pr[q] = *reinterpret_cast<const KD_GLOBAL kd_u4*>(wpr + min(v0 + q * 4 * B, (n - 1) & ~3));
+                if constexpr (B >= 1024)  // (streamed, as the seeded init's loads: C4 41.23 -> 41.13 ms)
+                    pr[q] = __builtin_nontemporal_load(reinterpret_cast<const KD_GLOBAL kd_u4*>(wpr + min(v0 + q * 4 * B, (n - 1) & ~3)));
+                else
+                    pr[q] = *reinterpret_cast<const KD_GLOBAL kd_u4*>(wpr + min(v0 + q * 4 * B, (n - 1) & ~3));
         };
         {
             // the next half-trip's records in flight while this one is copied (two 16-B
@@ -1282,8 +1285,20 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
 #pragma unroll
                 for (int q = 0; q < KD_SEEDS; q++) {
                     if (q < nseed) {
-                        dq[q] = *reinterpret_cast<const uint2*>(sdrow[q] + vl);
-                        pq[q] = *reinterpret_cast<const uint4*>(sprow[q] + vl);
+                        if constexpr (B >= 1024) {
+                            // streaming loads: a neighbour seed's row is read by few rows, and
+                            // passes through L2 without pushing out the CSR (C4 41.50 -> 41.23
+                            // ms); 256-thread rows keep them cached (C3's landmark rows seed
+                            // ~27 rows each: 2.03 -> 2.17 ms streamed)
+                            typedef unsigned u2v __attribute__((ext_vector_type(2)));
+                            const u2v d2 = __builtin_nontemporal_load(reinterpret_cast<const u2v*>(sdrow[q] + vl));
+                            const kd_u4 p4 = __builtin_nontemporal_load(reinterpret_cast<const kd_u4*>(sprow[q] + vl));
+                            dq[q] = make_uint2(d2.x, d2.y);
+                            pq[q] = make_uint4(p4.x, p4.y, p4.z, p4.w);
+                        } else {
+                            dq[q] = *reinterpret_cast<const uint2*>(sdrow[q] + vl);
+                            pq[q] = *reinterpret_cast<const uint4*>(sprow[q] + vl);
+                        }
                     } else {
                         dq[q] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
                         pq[q] = make_uint4(KD_NONE, KD_NONE, KD_NONE, KD_NONE);
@@ -1937,6 +1952,8 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
             // flag (agent-scope release first) lets the rows it seeds start, before this
             // row's own output
             uint16_t* dr = g.drow_out + (size_t)store * g.rstride;
+            // (streaming stores here and for the init's records measured the same: C4 41.87 / 41.91
+            // against 41.93 / 41.89 ms)
             for (int v0 = 8 * tid; v0 <= n; v0 += 8 * B)
                 *reinterpret_cast<uint4*>(dr + v0) = *reinterpret_cast<const uint4*>(dist + v0);
             wait_stores();

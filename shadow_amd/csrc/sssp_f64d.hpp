@@ -561,6 +561,91 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             }
             return as_d(dist[u]);
         };
+        if constexpr (H) {
+        // KFH, coalesced: a wave takes 64 consecutive vertices at a time (a counter), walks their
+        // contiguous in-arc range 256 arcs per trip (lane = arc, four positions per lane: the
+        // heads and weights are coalesced loads), finds each arc's vertex by a binary search
+        // over the lanes' row starts (row_in is ascending over the lanes), and hands the
+        // trip's tight arcs (few) to their vertices' lanes one by one, in arc order, so a
+        // full (d[u], u) tie keeps the first arc.  (The per-vertex scan below reads each
+        // vertex's arcs in its own lane, 64 lines per load instruction: KFH C4f 799 -> 779 ms
+        // with this walk, and its register peak went, 68 B/lane of scratch -> none; the LDS
+        // kernels keep the scan: C3f 10.4 against 13.5 ms, C2f 0.45 against 0.62 ms.)
+        (void)dnb;
+        if (tid == 0) sm->rhead = 0;
+        __syncthreads();
+        for (;;) {
+            int c0 = 0;
+            if (lane == 0) c0 = atomicAdd(&sm->rhead, 64);
+            c0 = __builtin_amdgcn_readfirstlane(c0);
+            if (c0 >= n) break;
+            const int v = c0 + lane;
+            const bool vok = v < n;
+            const int a0 = vok ? g.row_in[v] : 0x7fffffff;
+            const int aend = g.row_in[min(c0 + 64, n)];
+            const double dvr = vok ? as_d(dist[v]) : (double)INFINITY;
+            const bool scan = vok && v != s && dvr < INFINITY;
+            const double dvt = scan ? dvr : -1.0;  // (-1: never tight -- the source, unreachable)
+            double bd = INFINITY;
+            int bu = 0x7fffffff, ba = -1;
+            const int A0 = __builtin_amdgcn_readfirstlane(a0);
+            for (int base = A0; base < aend; base += 4 * 64) {
+                int uq[4];
+                double wq[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int a = min(base + r * 64 + lane, aend - 1);
+                    uq[r] = g.col_in[a];
+                    wq[r] = g.w_in[a];
+                }
+                int jq[4];
+                double dq[4];
+                bool tq[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int a = base + r * 64 + lane;
+                    int j = 0;
+#pragma unroll
+                    for (int st = 32; st >= 1; st >>= 1)
+                        if (__shfl(a0, j + st, 64) <= a) j += st;
+                    jq[r] = j;
+                    const double dvo = __shfl(dvt, j, 64);
+                    dq[r] = INFINITY;
+                    tq[r] = false;
+                    if (a < aend && dvo >= 0.0) {
+                        if constexpr (H) {
+                            const unsigned ku = keyl[uq[r]];
+                            if (kf_key_lo(ku) + wq[r] <= dvo && dvo <= kf_key_hi(ku) + wq[r]) dq[r] = as_d(dist[uq[r]]);
+                        } else {
+                            dq[r] = as_d(dist[uq[r]]);
+                        }
+                        tq[r] = dq[r] + wq[r] == dvo;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    for (unsigned long long tb = __ballot(tq[r]); tb;) {
+                        const int l = __ffsll((long long)tb) - 1;
+                        tb &= tb - 1;
+                        const int jl = __builtin_amdgcn_readlane(jq[r], l);
+                        const int ul = __builtin_amdgcn_readlane(uq[r], l);
+                        const unsigned long long db = as_u(dq[r]);
+                        const double dl = as_d((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)db, l) |
+                                               ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(db >> 32), l) << 32));
+                        if (lane == jl && (dl < bd || (dl == bd && ul < bu))) { bd = dl; bu = ul; ba = base + r * 64 + l; }
+                    }
+                }
+            }
+            if (vok) {
+                int pu = v, pr = 255;
+                if (ba >= 0) { pu = bu; pr = g.rix_in[ba]; }
+                else if (scan) raise_err(err, SHD_ROUTE_EUNREACH);  // (cannot happen)
+                par[v] = (uint16_t)pu;
+                rix[v] = (uint8_t)pr;
+            }
+        }
+        __syncthreads();
+        } else {
         for (int v0 = tid; v0 < n; v0 += 2 * B) {
             int vv[2], a0[2], a1[2], bu[2], ba[2];
             double dv[2], bd[2];
@@ -664,6 +749,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         }
         __syncthreads();
 
+        }
         KF_STAMP(2);
         // ---- C: lat row, then reliability down the tree ------------------------------
         const double fs = g.vf[s];

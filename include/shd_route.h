@@ -97,7 +97,9 @@ typedef struct shd_route_info {
                               * state in HBM, up to 65535 vertices); 3 = K16 in diagnostic builds only */
     int32_t dist_bound;      /* K32: proven bound on every shortest-path latency (ms) */
     int32_t block;           /* threads per workgroup of the SSSP kernel */
-    int32_t reserved;        /* KD: bucket width delta; KB: 1 when path attributes are fused */
+    int32_t reserved;        /* KD: bucket width delta; KB: 1 when path attributes are fused; KF:
+                              * the packed arcs' decimal scale (latency = k / scale, 4 bytes per
+                              * arc; 0 = f64 arcs) */
     int32_t lat16;           /* 1 when every table latency, the self-loop diagonal included, is an
                               * integer below 0xFFFF: the SHD_ROUTE_PAYLOAD_LAT16 eligibility */
 } shd_route_info_t;

@@ -160,6 +160,9 @@ struct shd_route {
     char* d_kf_ws = nullptr;
     size_t kf_ws_stride = 0;
     uint8_t* d_kf_rix = nullptr;
+    uint32_t* d_kf_opk = nullptr;  // KF packed arcs (head | k << 16, weight k / kf_wscale), or null
+    uint32_t* d_kf_ipk = nullptr;
+    double kf_wscale = 0.0;
     double* d_kf_rtab = nullptr;
     // K4 (fw.hpp): u16 all-pairs table + dense u16 weights, Np x Np (Np = n rounded to 64)
     uint16_t* d_fwD = nullptr;
@@ -745,8 +748,8 @@ const char* shd_route_strerror(int code) {
 // the per-source LDS state does and every thread holds at most 16 vertices in the level
 // passes (n <= 16 B); above that KFH (n <= 65535: the ring is u16), one 1024-thread
 // workgroup per CU with its vertex state in an HBM slice (C4f: 550 KB per slice).
-int prepare_kf(shd_route* c, const std::vector<int>& row_in, const std::vector<int>& col_in,
-               const std::vector<double>& w_in, const std::vector<double>& r_in) {
+int prepare_kf(shd_route* c, const std::vector<int>& col, const std::vector<double>& w, const std::vector<int>& row_in,
+               const std::vector<int>& col_in, const std::vector<double>& w_in, const std::vector<double>& r_in) {
     const int n = c->n;
     const char* force = getenv("SHD_ROUTE_KERNEL");
     if (force && *force && strcmp(force, "kf") && strcmp(force, "auto")) return SHD_ROUTE_OK;
@@ -793,8 +796,43 @@ int prepare_kf(shd_route* c, const std::vector<int>& row_in, const std::vector<i
     if (!(delta > 0.0) || std::isinf(delta)) delta = c->min_w > 0 ? c->min_w : 1.0;
     int rc = upload(c, &c->d_kf_rix, rix);
     if (!rc) rc = upload(c, &c->d_kf_rtab, rtab);
-    const void* kfn = hbm ? (const void*)sssp_f64d_kernel<1024, true>
-                          : blk == 256 ? (const void*)sssp_f64d_kernel<256> : (const void*)sssp_f64d_kernel<1024>;
+    // Packed arcs (KFH): when every latency is a decimal k / scale (scale 1, 10, 100 or 1000)
+    // with k < 65536, an arc is one u32, head | k << 16, and the kernel divides k by the scale
+    // -- IEEE division of two exact integers is the correctly rounded k / scale, the double the
+    // decimal parses to, and each arc is checked here (C4f's latencies have two decimals: 4
+    // bytes per arc read instead of 12; C4f 780 -> 764 ms).  The LDS kernels keep f64 arcs:
+    // there the division costs more than the bytes (C3f 10.39 -> 10.59, C2f 0.45 -> 0.49 ms)
+    double wscale = 0.0;
+    if (hbm && !(getenv("SHD_ROUTE_KFPK") && atoi(getenv("SHD_ROUTE_KFPK")) == 0)) {
+        for (const double sc : {1.0, 10.0, 100.0, 1000.0}) {
+            auto fits = [&](const std::vector<double>& ws) {
+                for (const double x : ws) {
+                    const double k = std::nearbyint(x * sc);
+                    if (!(k >= 1.0 && k <= 65535.0) || k / sc != x) return false;
+                }
+                return true;
+            };
+            if (fits(w) && (c->directed ? fits(w_in) : true)) { wscale = sc; break; }
+        }
+    }
+    if (!rc && wscale > 0.0) {
+        auto pack = [&](const std::vector<int>& cc, const std::vector<double>& ws) {
+            std::vector<uint32_t> pk(cc.size());
+            for (size_t a = 0; a < cc.size(); a++)
+                pk[a] = (uint32_t)cc[a] | ((uint32_t)std::nearbyint(ws[a] * wscale) << 16);
+            return pk;
+        };
+        rc = upload(c, &c->d_kf_opk, pack(col, w));
+        if (!rc) {
+            if (c->directed) rc = upload(c, &c->d_kf_ipk, pack(col_in, w_in));
+            else c->d_kf_ipk = c->d_kf_opk;
+        }
+        c->kf_wscale = wscale;
+    }
+    const bool pk = wscale > 0.0;
+    const void* kfn = hbm ? (pk ? (const void*)sssp_f64d_kernel<1024, true, true> : (const void*)sssp_f64d_kernel<1024, true>)
+                    : blk == 256 ? (pk ? (const void*)sssp_f64d_kernel<256, false, true> : (const void*)sssp_f64d_kernel<256>)
+                                 : (pk ? (const void*)sssp_f64d_kernel<1024, false, true> : (const void*)sssp_f64d_kernel<1024>);
     if (!rc) rc = hip_check(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (rc) return rc;
     c->kf_block = blk; c->kf_lds = lds; c->kf_delta = delta; c->kf_nrtab = (int)rtab.size();
@@ -935,7 +973,7 @@ int shd_route_create(shd_route_t** out, const shd_graph_t* g, int device) {
     if (!rc) rc = prepare_k32(c, row, col, w, eid, c->directed ? row_in : row, c->directed ? col_in : col,
                               c->directed ? w_in : w);
     if (!rc && c->sel == 0)
-        rc = prepare_kf(c, c->directed ? row_in : row, c->directed ? col_in : col, c->directed ? w_in : w,
+        rc = prepare_kf(c, col, w, c->directed ? row_in : row, c->directed ? col_in : col, c->directed ? w_in : w,
                         c->directed ? r_in : r);
     if (rc) {
         shd_route_destroy(c);
@@ -980,7 +1018,7 @@ int shd_route_get_info(const shd_route_t* c, shd_route_info_t* info) {
     info->dist_bound = c->k32_bound;
     info->block = c->sel == 2 ? KB_BLOCK : c->sel == 3 ? 1024 : c->sel == 4 ? c->kd_block
                 : c->sel == 1 ? c->k32_block : c->sel == 5 ? c->kf_block : kBlock;
-    info->reserved = c->sel == 4 ? c->kd_delta : c->sel == 2 ? c->kb_fused : 0;
+    info->reserved = c->sel == 4 ? c->kd_delta : c->sel == 2 ? c->kb_fused : c->sel == 5 ? (int)c->kf_wscale : 0;
     info->lat16 = lat16_ok(c) ? 1 : 0;
     info->device_bytes = c->device_bytes;
     info->min_edge_latency = c->min_w;
@@ -1076,16 +1114,23 @@ int shd_route_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, const
         k.hring = 0;
         if (const char* e = getenv("SHD_ROUTE_KFH_RING")) k.hring = std::max(0, atoi(e));  // (tests: a small ring)
         k.vf = c->d_vf; k.self_w = c->d_self_w; k.self_r = c->d_self_r; k.dbg = c->d_dbg;
+        k.opk = c->d_kf_opk; k.ipk = c->d_kf_ipk; k.wscale = c->kf_wscale;
         const int grid = std::min(ns, c->kf_slots);
-        if (c->kf_h)  // (the slices: one per workgroup slot, grid <= kf_slots)
-            hipLaunchKernelGGL((sssp_f64d_kernel<1024, true>), dim3(grid), dim3(1024), c->kf_lds, st, k, d_src, ns, d_tgt,
-                               nt, (long long)ld, d_lat, d_rel, d_row_min, c->d_err, c->d_kf_ws, c->kf_ws_stride);
-        else if (c->kf_block == 256)
-            hipLaunchKernelGGL(sssp_f64d_kernel<256>, dim3(grid), dim3(256), c->kf_lds, st, k, d_src, ns, d_tgt, nt,
-                               (long long)ld, d_lat, d_rel, d_row_min, c->d_err, (char*)nullptr, (size_t)0);
-        else
-            hipLaunchKernelGGL(sssp_f64d_kernel<1024>, dim3(grid), dim3(1024), c->kf_lds, st, k, d_src, ns, d_tgt, nt,
-                               (long long)ld, d_lat, d_rel, d_row_min, c->d_err, (char*)nullptr, (size_t)0);
+        auto go = [&](auto kern, int blk, char* ws, size_t wst) {
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(blk), c->kf_lds, st, k, d_src, ns, d_tgt, nt, (long long)ld, d_lat,
+                               d_rel, d_row_min, c->d_err, ws, wst);
+        };
+        const bool pk = c->d_kf_opk != nullptr;
+        if (c->kf_h) {  // (the slices: one per workgroup slot, grid <= kf_slots)
+            if (pk) go(sssp_f64d_kernel<1024, true, true>, 1024, c->d_kf_ws, c->kf_ws_stride);
+            else go(sssp_f64d_kernel<1024, true>, 1024, c->d_kf_ws, c->kf_ws_stride);
+        } else if (c->kf_block == 256) {
+            if (pk) go(sssp_f64d_kernel<256, false, true>, 256, (char*)nullptr, (size_t)0);
+            else go(sssp_f64d_kernel<256>, 256, (char*)nullptr, (size_t)0);
+        } else {
+            if (pk) go(sssp_f64d_kernel<1024, false, true>, 1024, (char*)nullptr, (size_t)0);
+            else go(sssp_f64d_kernel<1024>, 1024, (char*)nullptr, (size_t)0);
+        }
         return hip_check(hipGetLastError());
     }
     DevGraph g = dev_graph(c);

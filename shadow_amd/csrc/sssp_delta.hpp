@@ -87,6 +87,9 @@ constexpr uint32_t KD_SRC_MARK = 0xFFFFFFFEu;  // parent record of the source it
 #define KD_NSEEDS 3  // seeds per row at most (KDJob holds up to 3; the planner's default: engine.hip)
 #endif
 constexpr int KD_SEEDS = KD_NSEEDS;
+#ifndef KD_NTLOAD
+#define KD_NTLOAD 1  // 1024-thread rows: streaming loads of the seed rows and phase C's parent records
+#endif
 #ifndef KD_JUMPS
 #define KD_JUMPS 1  // phase C pointer-jumping rounds before the walks (C4: 0: 50.5 ms, 1: 48.6, 2: 49.3, 3: 51.5, to convergence: 54.2)
 #endif
@@ -677,7 +680,7 @@ __device__ __attribute__((noinline)) void kd_output(const int i, const int s, co
             constexpr int NQ = sizeof(pr) / sizeof(pr[0]);
 #pragma unroll
             for (int q = 0; q < NQ; q++)
-                if constexpr (B >= 1024)  // (streamed, as the seeded init's loads: C4 41.23 -> 41.13 ms)
+                if constexpr (B >= 1024 && KD_NTLOAD)  // (streamed, as the seeded init's loads: C4 41.23 -> 41.13 ms)
                     pr[q] = __builtin_nontemporal_load(reinterpret_cast<const KD_GLOBAL kd_u4*>(wpr + min(v0 + q * 4 * B, (n - 1) & ~3)));
                 else
                     pr[q] = *reinterpret_cast<const KD_GLOBAL kd_u4*>(wpr + min(v0 + q * 4 * B, (n - 1) & ~3));
@@ -1285,7 +1288,7 @@ __device__ __attribute__((always_inline)) inline void kd_rows_body(KD_KERNEL_PAR
 #pragma unroll
                 for (int q = 0; q < KD_SEEDS; q++) {
                     if (q < nseed) {
-                        if constexpr (B >= 1024) {
+                        if constexpr (B >= 1024 && KD_NTLOAD) {
                             // streaming loads: a neighbour seed's row is read by few rows, and
                             // passes through L2 without pushing out the CSR (C4 41.50 -> 41.23
                             // ms); 256-thread rows keep them cached (C3's landmark rows seed

@@ -42,6 +42,11 @@ struct DevF64D {
     const double* __restrict__ rtab;     // distinct 1 - loss values (<= 254)
     int nrtab;
     int hring;                           // KFH: ring entries cap (0: what LDS holds; tests)
+    // packed arcs (kernels with PK): head | k << 16 per out- / in-arc, weight = k / wscale,
+    // exact (every arc checked when the context is made: decimal latencies, k < 65536)
+    const uint32_t* __restrict__ opk;
+    const uint32_t* __restrict__ ipk;
+    double wscale;
     const double* __restrict__ vf;
     const double* __restrict__ self_w;
     const double* __restrict__ self_r;
@@ -222,7 +227,7 @@ __device__ __attribute__((always_inline)) int kfh_levels(int n, int s, int tid, 
     }
 }
 
-template <int B, bool H = false>
+template <int B, bool H = false, bool PK = false>
 // (amdgpu_waves_per_eu(4): four 256-thread workgroups per CU need 128 VGPRs or fewer; the
 // 256-thread build came out at 129, three waves per SIMD, so only three workgroups per CU)
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sssp_f64d_kernel(DevF64D g, const int* __restrict__ src, int ns,
@@ -427,8 +432,19 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         const int a = aq[r] >= 0 ? aq[r] : 0;
-                        vq[r] = g.col[a];
-                        wq[r] = g.w[a];
+                        if constexpr (PK) vq[r] = (int)g.opk[a];  // (decoded when used: the load stays in flight)
+                        else { vq[r] = g.col[a]; wq[r] = g.w[a]; }
+                    }
+                };
+                // packed arcs: head and weight out of the loaded word
+                auto decode = [&](int (&vq)[4], double (&wq)[4]) __attribute__((always_inline)) {
+                    if constexpr (PK) {
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const uint32_t x = (uint32_t)vq[r];
+                            vq[r] = (int)(x & 0xFFFFu);
+                            wq[r] = (double)(x >> 16) / g.wscale;
+                        }
                     }
                 };
                 // a trip's relaxations (KFH: hold = the candidates' HBM atomicMin results)
@@ -477,6 +493,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         if (tid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         KF_ACC(14);
 #endif
+                        decode(vq, wq);
                         // the key filter, then the candidates' HBM atomics issued together
                         unsigned long long hold[4], nbq[4];
                         int vc[4];
@@ -516,6 +533,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         int aq[4], uq[4], vq[4];
                         double wq[4], duq[4];
                         stage(p0, aq, uq, vq, wq, duq);
+                        decode(vq, wq);
                         if (tid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         KF_ACC(14);
                         const unsigned long long hold[4] = {0ull, 0ull, 0ull, 0ull};
@@ -595,8 +613,8 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const int a = min(base + r * 64 + lane, aend - 1);
-                    uq[r] = g.col_in[a];
-                    wq[r] = g.w_in[a];
+                    if constexpr (PK) uq[r] = (int)g.ipk[a];
+                    else { uq[r] = g.col_in[a]; wq[r] = g.w_in[a]; }
                 }
                 int jq[4];
                 double dq[4];
@@ -609,6 +627,11 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     for (int st = 32; st >= 1; st >>= 1)
                         if (__shfl(a0, j + st, 64) <= a) j += st;
                     jq[r] = j;
+                    if constexpr (PK) {
+                        const uint32_t x = (uint32_t)uq[r];
+                        uq[r] = (int)(x & 0xFFFFu);
+                        wq[r] = (double)(x >> 16) / g.wscale;
+                    }
                     const double dvo = __shfl(dvt, j, 64);
                     dq[r] = INFINITY;
                     tq[r] = false;
@@ -676,9 +699,19 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
 #pragma unroll
                     for (int q = 0; q < KBW; q++) {
                         const int a = min(a0[h] + t0 + q, max(a1[h] - 1, 0));
-                        uq[h][q] = g.col_in[a];
-                        wq[h][q] = g.w_in[a];
+                        if constexpr (PK) uq[h][q] = (int)g.ipk[a];
+                        else { uq[h][q] = g.col_in[a]; wq[h][q] = g.w_in[a]; }
                     }
+                if constexpr (PK) {
+#pragma unroll
+                    for (int h = 0; h < 2; h++)
+#pragma unroll
+                        for (int q = 0; q < KBW; q++) {
+                            const uint32_t x = (uint32_t)uq[h][q];
+                            uq[h][q] = (int)(x & 0xFFFFu);
+                            wq[h][q] = (double)(x >> 16) / g.wscale;
+                        }
+                }
 #pragma unroll
                 for (int h = 0; h < 2; h++)
 #pragma unroll
@@ -722,8 +755,11 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
                         const int a = min(t + 16 * q, max(a1 - 1, 0));
-                        uq[q] = g.col_in[a];
-                        wq[q] = g.w_in[a];
+                        if constexpr (PK) {
+                            const uint32_t x = g.ipk[a];
+                            uq[q] = (int)(x & 0xFFFFu);
+                            wq[q] = (double)(x >> 16) / g.wscale;
+                        } else { uq[q] = g.col_in[a]; wq[q] = g.w_in[a]; }
                     }
 #pragma unroll
                     for (int q = 0; q < 4; q++) {

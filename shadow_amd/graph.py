@@ -143,10 +143,13 @@ def complete_graph(n: int, seed: int, name: str = "complete") -> Graph:
 
 def fractional(g: Graph, seed: int = 0, name: Optional[str] = None) -> Graph:
     """The same topology with two-decimal latencies (the format of the reference's own
-    resource/topology.graphml.xml.xz, e.g. 2293.85 ms): latency + U{0..99} / 100.  No
-    integer kernel applies; the fractional path (KF, or the generic f64 kernel) does."""
+    resource/topology.graphml.xml.xz, e.g. 2293.85 ms): latency + U{0..99} / 100, each the
+    double its decimal text parses to (strtod: the nearest double, here (100 latency + k) /
+    100.0, one correctly rounded division; until round 5 the sum latency + k / 100.0, one ulp
+    off that for ~0.2% of the arcs).  No integer kernel applies; the fractional path (KF, or
+    the generic f64 kernel) does."""
     rng = np.random.default_rng(10_000 + seed)
-    lat = g.latency + rng.integers(0, 100, size=g.m) / 100.0
+    lat = (np.rint(g.latency * 100.0) + rng.integers(0, 100, size=g.m)) / 100.0
     return dataclasses.replace(g, latency=lat, name=name or (g.name + "_frac"))
 
 

@@ -41,6 +41,29 @@ def test_kf_fractional_bitexact(route, oracle_mod, monkeypatch, cfg, step):
     assert np.array_equal(mn, olat.min(axis=1))
 
 
+@pytest.mark.parametrize("kfh", [0, 1])
+def test_kf_packed_arcs(route, oracle_mod, monkeypatch, kfh):
+    """C2f's latencies have two decimals: KFH reads each arc as one u32 (head | k << 16,
+    latency k / 100.0, the double the decimal parses to); the LDS kernel keeps f64 arcs.  The
+    same rows as the f64 arcs (SHD_ROUTE_KFPK=0) and the oracle."""
+    g = config("c2f")
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    if kfh:
+        monkeypatch.setenv("SHD_ROUTE_KFH", "1")
+    src = np.arange(0, g.n, 3, dtype=np.int32)
+    tgt = g.targets()
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 5 and eng.info["reserved"] == (100 if kfh else 0) and eng.info["lds_resident"] == 1 - kfh
+    lat, rel, mn = eng.rows(src, tgt, dispatch=False)
+    monkeypatch.setenv("SHD_ROUTE_KFPK", "0")
+    e0 = route.RouteEngine(g)
+    assert e0.info["reserved"] == 0
+    l0, r0, m0 = e0.rows(src, tgt, dispatch=False)
+    assert np.array_equal(lat, l0) and np.array_equal(rel, r0) and np.array_equal(mn, m0)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(src, tgt, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat) and np.array_equal(rel, orel)
+
+
 def test_kf_many_sources_per_workgroup(route, monkeypatch):
     # every source of C2f in one launch (about two per workgroup) against KF one source per
     # workgroup: per-source state is reset between sources

@@ -480,7 +480,97 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         }
                     }
                 };
-                if constexpr (H) {
+                if constexpr (H && PK) {
+                    // KFH with packed arcs, two trips of atomics in flight (C4f 765 -> 733 ms
+                    // against the one-trip pipeline below): iteration t issues
+                    // trip t + 1's arc loads, then trip t's filter and atomics, then trip t - 1's
+                    // relaxations -- the loads return in issue order, so trip t's filter waits
+                    // for its own loads only, and trip t - 1's results are waited for with trip
+                    // t's atomics still out.  A trip between stage and filter is its loaded arc
+                    // words and its owner lanes (8 bits each, 0xFF: no arc); past the filter its
+                    // candidate heads, distances and atomic results.
+                    auto stage2 = [&](int p0, int (&xq)[4], unsigned& lop) __attribute__((always_inline)) {
+                        if (lane < 4) wm4[lane] = 0ull;
+                        __builtin_amdgcn_wave_barrier();
+                        const int rel = excl - p0;
+                        if (valid && rel >= 0 && rel < 4 * 64) atomicOr(&wm4[rel >> 6], 1ull << (rel & 63));
+                        __builtin_amdgcn_wave_barrier();
+                        lop = 0u;
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const unsigned long long before = __ballot(valid && excl < p0 + r * 64);
+                            const unsigned long long mk = wm4[r];
+                            const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+                            const int lo = max(0, __popcll(before) + __popcll(mk & upto) - 1);
+                            const int p = p0 + r * 64 + lane;
+                            const int ob = __shfl(beg, lo, 64), oe = __shfl(excl, lo, 64);
+                            const bool ok = p < total;
+                            xq[r] = (int)g.opk[ok ? ob + (p - oe) : 0];
+                            lop |= (unsigned)(ok ? lo : 0xFF) << (8 * r);
+                        }
+                        __builtin_amdgcn_wave_barrier();  // (the marks are read before the next trip clears them)
+                    };
+                    auto filter2 = [&](const int (&xq)[4], const unsigned lop, int (&vc)[4], unsigned long long (&nbq)[4],
+                                       unsigned long long (&hold)[4]) __attribute__((always_inline)) {
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const unsigned lo = (lop >> (8 * r)) & 0xFFu;
+                            const double du = __shfl(dun, (int)(lo & 63u), 64);
+                            const uint32_t x = (uint32_t)xq[r];
+                            const int v = (int)(x & 0xFFFFu);
+                            nbq[r] = as_u(du + (double)(x >> 16) / g.wscale);
+                            const bool cand = lo != 0xFFu && kf_key(nbq[r]) <= keyl[v];
+                            vc[r] = cand ? v : -1;
+                            hold[r] = cand ? atomicMin(&dist[v], nbq[r]) : 0ull;
+                        }
+                    };
+                    auto relax2 = [&](const int (&vc)[4], const unsigned long long (&nbq)[4],
+                                      const unsigned long long (&hold)[4]) __attribute__((always_inline)) {
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const int v = vc[r];
+                            const unsigned long long nb = nbq[r];
+                            if (v >= 0 && nb < hold[r]) {
+                                kf_key_min(keyl, v, kf_key(nb));
+                                const unsigned long long bit = 1ull << (v & 63);
+                                if (as_d(nb) < T) {
+                                    if (!(atomicOr(&inq[v >> 6], bit) & bit)) {
+                                        const unsigned at = (unsigned)atomicAdd(&sm->qtail, 1);
+                                        if (at - qhead < R) ring[at % R] = (uint16_t)v;
+                                        else if (B < 1024) atomicOr(&sm->ovf, 1 << rpar);
+                                        else sm->ovf = 1;
+                                    }
+                                } else {
+                                    atomicOr(&pend[v >> 6], bit);
+                                    atomicMin(&wmin[v >> 6], nb);
+                                }
+                            }
+                        }
+                    };
+                    int xa[4], vp[4];
+                    unsigned la;
+                    unsigned long long np_[4], hp[4];
+                    stage2(0, xa, la);
+                    bool prev = false;
+                    for (int p0 = 0;; p0 += 4 * 64) {
+                        const bool more = p0 + 4 * 64 < total;  // (wave-uniform)
+                        int xb[4];
+                        unsigned lb = 0u;
+                        if (more) stage2(p0 + 4 * 64, xb, lb);
+                        int vc[4];
+                        unsigned long long nbq[4], hold[4];
+                        filter2(xa, la, vc, nbq, hold);
+                        if (prev) relax2(vp, np_, hp);
+#pragma unroll
+                        for (int r = 0; r < 4; r++) { vp[r] = vc[r]; np_[r] = nbq[r]; hp[r] = hold[r]; }
+                        prev = true;
+                        if (!more) break;
+#pragma unroll
+                        for (int r = 0; r < 4; r++) xa[r] = xb[r];
+                        la = lb;
+                    }
+                    relax2(vp, np_, hp);
+                } else if constexpr (H) {
                     // KFH, software-pipelined: a trip's HBM atomics are in flight while the next
                     // trip's owners are found and its arc loads issued; its relaxations (which
                     // wait for the atomics' results) come after.  Past the filter a trip keeps

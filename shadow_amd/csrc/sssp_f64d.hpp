@@ -674,8 +674,8 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         // contiguous in-arc range 256 arcs per trip (lane = arc, four positions per lane: the
         // heads and weights are coalesced loads), finds each arc's vertex by a binary search
         // over the lanes' row starts (row_in is ascending over the lanes), and hands the
-        // trip's tight arcs (few) to their vertices' lanes one by one, in arc order, so a
-        // full (d[u], u) tie keeps the first arc.  (The per-vertex scan below reads each
+        // trip's candidate arcs (few) to their vertices' lanes one by one, in arc order (see
+        // the candidates below).  (The per-vertex scan below reads each
         // vertex's arcs in its own lane, 64 lines per load instruction: KFH C4f 799 -> 779 ms
         // with this walk, and its register peak went, 68 B/lane of scratch -> none; the LDS
         // kernels keep the scan: C3f 10.4 against 13.5 ms, C2f 0.45 against 0.62 ms.)
@@ -694,9 +694,16 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             const double dvr = vok ? as_d(dist[v]) : (double)INFINITY;
             const bool scan = vok && v != s && dvr < INFINITY;
             const double dvt = scan ? dvr : -1.0;  // (-1: never tight -- the source, unreachable)
-            double bd = INFINITY;
-            int bu = 0x7fffffff, ba = -1;
+            // Candidates: the in-arcs whose key interval admits fl(d[u] + w) == d[v] -- every
+            // tight arc among them (keys are conservative), and v has at least one tight arc.
+            // A vertex with exactly one candidate takes it without loading d[u]; only vertices
+            // with two or more (ties, or a near miss inside the key interval) load their
+            // candidates' distances and apply the tie rule in a second scan of their arcs
+            // (each candidate's d[u] was an HBM load per trip: C4f phase B ~3.1 M cycles/row).
+            int cnt = 0, bu = 0x7fffffff, ba = -1;
             const int A0 = __builtin_amdgcn_readfirstlane(a0);
+            // (loading the next trip's packed words at the top of each trip, under this trip's
+            // candidate distance loads, measured slower: C4f 731.7 -> 736.3 ms)
             for (int base = A0; base < aend; base += 4 * 64) {
                 int uq[4];
                 double wq[4];
@@ -707,8 +714,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     else { uq[r] = g.col_in[a]; wq[r] = g.w_in[a]; }
                 }
                 int jq[4];
-                double dq[4];
-                bool tq[4];
+                bool cq[4];
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const int a = base + r * 64 + lane;
@@ -723,30 +729,44 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         wq[r] = (double)(x >> 16) / g.wscale;
                     }
                     const double dvo = __shfl(dvt, j, 64);
-                    dq[r] = INFINITY;
-                    tq[r] = false;
+                    cq[r] = false;
                     if (a < aend && dvo >= 0.0) {
-                        if constexpr (H) {
-                            const unsigned ku = keyl[uq[r]];
-                            if (kf_key_lo(ku) + wq[r] <= dvo && dvo <= kf_key_hi(ku) + wq[r]) dq[r] = as_d(dist[uq[r]]);
-                        } else {
-                            dq[r] = as_d(dist[uq[r]]);
-                        }
-                        tq[r] = dq[r] + wq[r] == dvo;
+                        const unsigned ku = keyl[uq[r]];
+                        cq[r] = kf_key_lo(ku) + wq[r] <= dvo && dvo <= kf_key_hi(ku) + wq[r];
                     }
                 }
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
-                    for (unsigned long long tb = __ballot(tq[r]); tb;) {
+                    for (unsigned long long tb = __ballot(cq[r]); tb;) {
                         const int l = __ffsll((long long)tb) - 1;
                         tb &= tb - 1;
                         const int jl = __builtin_amdgcn_readlane(jq[r], l);
                         const int ul = __builtin_amdgcn_readlane(uq[r], l);
-                        const unsigned long long db = as_u(dq[r]);
-                        const double dl = as_d((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)db, l) |
-                                               ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(db >> 32), l) << 32));
-                        if (lane == jl && (dl < bd || (dl == bd && ul < bu))) { bd = dl; bu = ul; ba = base + r * 64 + l; }
+                        if (lane == jl) {
+                            if (cnt == 0) { bu = ul; ba = base + r * 64 + l; }
+                            cnt++;
+                        }
                     }
+                }
+            }
+            if (scan && cnt >= 2) {
+                // the exact rule over this vertex's arcs: tight (fl(d[u] + w) == d[v], d[u]
+                // loaded for candidates only), minimum (d[u], u), the first arc on a full tie
+                double bd = INFINITY;
+                bu = 0x7fffffff; ba = -1;
+                const int a1v = g.row_in[v + 1];
+                for (int a = a0; a < a1v; a++) {
+                    int u;
+                    double w;
+                    if constexpr (PK) {
+                        const uint32_t x = g.ipk[a];
+                        u = (int)(x & 0xFFFFu);
+                        w = (double)(x >> 16) / g.wscale;
+                    } else { u = g.col_in[a]; w = g.w_in[a]; }
+                    const unsigned ku = keyl[u];
+                    if (!(kf_key_lo(ku) + w <= dvr && dvr <= kf_key_hi(ku) + w)) continue;
+                    const double du = as_d(dist[u]);
+                    if (du + w == dvr && (du < bd || (du == bd && u < bu))) { bd = du; bu = u; ba = a; }
                 }
             }
             if (vok) {
@@ -901,6 +921,80 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         }
         __syncthreads();
         KF_STAMP(3);
+        // KFH (round 5): reliability by walks in LDS.  Phase A/B's LDS is dead now; the
+        // parents (u16) and factor indices (u8) come in from the slice (150 KB at C4f), and
+        // each target walks its tree path to the source, keeping the indices of the lossy arcs
+        // (a lossless arc's exact 1.0 leaves every product unchanged) and folds them
+        // source-first: the products of the level passes below, bit for bit.  Two targets per
+        // lane in turn.  A path with more than 16 lossy arcs sends the whole row to the level
+        // passes (rare: ~2 lossy arcs per C4f path).
+        bool walked = false;
+        if constexpr (H) {
+            const size_t po = LH.pend, ro = LH.pend + a16(2 * (size_t)n);
+            if (rrow && ro + a16((size_t)n) <= LH.rtab) {
+                uint16_t* parl = reinterpret_cast<uint16_t*>(smem + po);
+                uint8_t* rixl = reinterpret_cast<uint8_t*>(smem + ro);
+                for (int v = tid; v < n; v += B) { parl[v] = par[v]; rixl[v] = rix[v]; }
+                if (tid == 0) sm->flag = 0;
+                __syncthreads();
+                int deep = 0;
+                for (int j0 = tid; j0 < nt; j0 += 2 * B) {
+                    int t2[2], v2[2], ns2[2];
+                    unsigned long long lo2[2], hi2[2];
+                    bool go2[2];
+                    double R2[2];
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const int j = j0 + h * B;
+                        const int t = j < nt ? tgt[j] : -1;
+                        t2[h] = t; v2[h] = t; ns2[h] = 0; lo2[h] = hi2[h] = 0ull; go2[h] = false; R2[h] = NAN;
+                        if (j >= nt) continue;
+                        if (t < 0 || t >= n) continue;  // (the lat row raised EINVAL)
+                        if (t == s) R2[h] = isnan(sw_s) ? (double)NAN : cs * sr_s;
+                        else if (rixl[t] != 255) go2[h] = true;  // (255: unreachable, NaN)
+                    }
+                    for (int step = 0; (go2[0] || go2[1]) && step < n; step++) {
+#pragma unroll
+                        for (int h = 0; h < 2; h++) {
+                            if (!go2[h]) continue;
+                            const int v = v2[h];
+                            const unsigned r = rixl[v];
+                            const int pv = parl[v];
+                            if (rtl[r] != 1.0) {
+                                const int k = ns2[h]++;
+                                if (k < 8) lo2[h] |= (unsigned long long)r << (8 * k);
+                                else if (k < 16) hi2[h] |= (unsigned long long)r << (8 * (k - 8));
+                                else deep = 1;
+                            }
+                            v2[h] = pv;
+                            if (pv == s) go2[h] = false;
+                        }
+                    }
+                    if (go2[0] || go2[1]) deep = 1;  // (a parent cycle: cannot happen)
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const int j = j0 + h * B;
+                        if (j >= nt) continue;
+                        const int t = t2[h];
+                        if (t >= 0 && t < n && t != s && rixl[t] != 255) {
+                            double x = cs;
+                            for (int k = min(ns2[h], 16) - 1; k >= 0; k--) {
+                                const unsigned r = (unsigned)((k < 8 ? lo2[h] >> (8 * k) : hi2[h] >> (8 * (k - 8))) & 0xFFull);
+                                x *= rtl[r];
+                            }
+                            const double ft = g.vf[t];
+                            R2[h] = isnan(ft) ? x : x * ft;
+                        }
+                        rrow[j] = R2[h];
+                    }
+                }
+                if (deep) sm->flag = 1;
+                __syncthreads();
+                walked = sm->flag == 0;
+                __syncthreads();  // (every thread has read the flag)
+            }
+        }
+        if (!walked) {
         // relv over dist's LDS: the source cs, unreachable NaN, the rest pending (-1)
         for (int v = tid; v < n; v += B) {
             const bool unr = v != s && !(as_d(dist[v]) < INFINITY);
@@ -963,8 +1057,9 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             if (!again) break;
         }
         }
+        }  // (!walked)
         KF_STAMP(4);
-        for (int j = tid; j < nt; j += B) {
+        for (int j = tid; j < (walked ? 0 : nt); j += B) {
             const int t = tgt[j];
             double Rv = NAN;
             if (t >= 0 && t < n) {

@@ -233,6 +233,51 @@ def test_kfh_vertex_loss_directed(route, oracle_mod, monkeypatch):
     np.testing.assert_allclose(rel, orel, rtol=REL_TOL, atol=0)
 
 
+@pytest.mark.parametrize("lossy", [0.05, 1.0])
+def test_kfh_walks_and_deep_paths(route, oracle_mod, monkeypatch, lossy):
+    """KFH's reliability rows by LDS walks (round 5), and the level passes a row falls back
+    to when a path has more than 16 lossy arcs: an undirected chain of 600 vertices with
+    sparse chords (paths of hundreds of hops), every arc lossy (1.0: every row falls back)
+    or 5% of them (0.05: most rows walk), with vertex loss."""
+    rng = np.random.default_rng(21)
+    n = 600
+    a = np.arange(n - 1)
+    ch = rng.integers(0, n, (40, 2))
+    ch = ch[ch[:, 0] != ch[:, 1]]
+    src = np.concatenate([a, ch[:, 0]]).astype(np.int32)
+    dst = np.concatenate([a + 1, ch[:, 1]]).astype(np.int32)
+    key = np.minimum(src, dst).astype(np.int64) * n + np.maximum(src, dst)
+    _, first = np.unique(key, return_index=True)
+    first = np.sort(first)
+    src, dst = src[first], dst[first]
+    lat = np.round(rng.uniform(0.5, 20.0, len(src)), 2)
+    loss = np.where(rng.random(len(src)) < lossy, rng.integers(1, 40, len(src)) * 1e-3, 0.0)
+    # self-loops: a row's own target takes one (topology.c:1471-1499)
+    src = np.concatenate([src, np.arange(n, dtype=np.int32)])
+    dst = np.concatenate([dst, np.arange(n, dtype=np.int32)])
+    lat = np.concatenate([lat, np.full(n, 0.25)])
+    loss = np.concatenate([loss, np.zeros(n)])
+    vl = np.where(rng.random(n) < 0.2, rng.integers(1, 30, n) * 1e-3, np.nan)
+    g = Graph(n=n, src=src, dst=dst, latency=lat, packetloss=loss, vertex_packetloss=vl, name="kfh_chain")
+    monkeypatch.delenv("SHD_ROUTE_KERNEL", raising=False)
+    monkeypatch.setenv("SHD_ROUTE_KFH", "1")
+    eng = route.RouteEngine(g)
+    assert eng.info["kernel"] == 5 and eng.info["lds_resident"] == 0
+    tgt = np.arange(n, dtype=np.int32)
+    s_ = np.arange(0, n, 7, dtype=np.int32)
+    lat_, rel_, mn_ = eng.rows(s_, tgt, dispatch=False)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(s_, tgt, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat_, olat)
+    np.testing.assert_allclose(rel_, orel, rtol=REL_TOL, atol=0)
+    # the walks and the level passes agree bit for bit (vertex factors included): the same
+    # rows from the LDS kernel, which has only level passes
+    monkeypatch.delenv("SHD_ROUTE_KFH")
+    e2 = route.RouteEngine(g)
+    assert e2.info["lds_resident"] == 1
+    l2, r2, _ = e2.rows(s_, tgt, dispatch=False)
+    assert np.array_equal(l2, lat_) and np.array_equal(r2, rel_)
+
+
 def test_kfh_20k_vertices(route, oracle_mod, monkeypatch):
     # above KF's LDS limit: KFH by default, sampled rows bit-exact against the oracle
     g = fractional(internet_like(20000, 4, 6, name="kfh_20k"), 5)

@@ -480,6 +480,8 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         }
                     }
                 };
+                // (eight arc positions per lane and trip with one trip of atomics in flight
+                // measured slower than this: C4f 620.9 against 572.1 ms)
                 if constexpr (H && PK) {
                     // KFH with packed arcs, two trips of atomics in flight (C4f 765 -> 733 ms
                     // against the one-trip pipeline below): iteration t issues
@@ -702,21 +704,22 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             // (each candidate's d[u] was an HBM load per trip: C4f phase B ~3.1 M cycles/row).
             int cnt = 0, bu = 0x7fffffff, ba = -1;
             const int A0 = __builtin_amdgcn_readfirstlane(a0);
-            // (loading the next trip's packed words at the top of each trip, under this trip's
-            // candidate distance loads, measured slower: C4f 731.7 -> 736.3 ms)
-            for (int base = A0; base < aend; base += 4 * 64) {
-                int uq[4];
-                double wq[4];
+            // (the next trip's words loaded under this one, or eight positions per lane: C4f
+            // 570.8 / 577.3 ms against 570.9)
+            constexpr int BW = 4;  // arc positions per lane and trip
+            for (int base = A0; base < aend; base += BW * 64) {
+                int uq[BW];
+                double wq[BW];
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
+                for (int r = 0; r < BW; r++) {
                     const int a = min(base + r * 64 + lane, aend - 1);
                     if constexpr (PK) uq[r] = (int)g.ipk[a];
                     else { uq[r] = g.col_in[a]; wq[r] = g.w_in[a]; }
                 }
-                int jq[4];
-                bool cq[4];
+                int jq[BW];
+                bool cq[BW];
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
+                for (int r = 0; r < BW; r++) {
                     const int a = base + r * 64 + lane;
                     int j = 0;
 #pragma unroll
@@ -736,7 +739,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     }
                 }
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
+                for (int r = 0; r < BW; r++) {
                     for (unsigned long long tb = __ballot(cq[r]); tb;) {
                         const int l = __ffsll((long long)tb) - 1;
                         tb &= tb - 1;

@@ -13,6 +13,7 @@ ks() {  # name bench-args...
     -- python3 bench.py --no-cpu-baseline --verify 0 "$@" > gpurun_out/prof_$tag/$name.json 2> gpurun_out/prof_$tag/$name.err \
     || { echo "kernel trace $name failed"; tail -5 gpurun_out/prof_$tag/$name.err; exit 1; }
 }
+if [ "${PROF_STATS:-1}" != 0 ]; then  # (PROF_STATS=0: the PMC passes only)
 ks c2 --config c2 --steps 20 --warmup 5
 ks c3 --config c3 --steps 10 --warmup 2
 ks c4 --config c4 --steps 5 --warmup 1
@@ -20,6 +21,7 @@ ks c5 --config c5 --steps 5 --warmup 1
 ks c3f --config c3f --steps 3 --warmup 1
 ks c2f --config c2f --steps 10 --warmup 2
 ks c4f --config c4f --steps 2 --warmup 1
+fi
 pmc() {  # cfg counter bench-args...
   local cfg=$1 ctr=$2; shift 2
   timeout -s KILL 120 rocprofv3 --pmc $ctr -d gpurun_out/prof_$tag/pmc_$cfg/$ctr -o run --output-format csv \

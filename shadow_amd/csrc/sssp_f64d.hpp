@@ -67,6 +67,18 @@ struct DevF64D {
 #endif
 
 constexpr int KF_HUB = 24;  // phase B: vertices of more in-arcs are done by a whole wave
+#ifndef KFH_SDIV
+#define KFH_SDIV 32  // KFH phase A: slice = max(KFH_SMIN, min(64, entries left / KFH_SDIV)) (0: 64)
+#endif
+#ifndef KFH_SMIN
+#define KFH_SMIN 8
+#endif
+#ifndef KF_SDIV
+#define KF_SDIV 0  // the same for the LDS kernels (0: 64-entry slices)
+#endif
+#ifndef KF_SMIN
+#define KF_SMIN 8
+#endif
 #ifndef KFH_HUB
 #define KFH_HUB KF_HUB  // (KFH's threshold; C4f 12 / 24 / 48 / 96: 830 / 814 / 860 / 905 ms)
 #endif
@@ -376,16 +388,28 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             // owners by a binary search over the slice's lane offsets (ds_bpermute), the 8
             // arc loads of a trip issued together
             for (;;) {
-                int c = 0;
-                if (lane == 0) c = atomicAdd(&sm->rhead, 64);
+                int c = 0, nn = 64;
+                if (lane == 0) {
+                    constexpr int sdiv = H ? KFH_SDIV : KF_SDIV, smin = H ? KFH_SMIN : KF_SMIN;
+                    if constexpr (sdiv > 0) {
+                        // a round's entries in smaller slices as they run out, so the waves
+                        // finish the round together (it ends at a barrier): KFH C4f 570.8 ->
+                        // 534.5 ms at 32 / 8 (16 / 16: 542.9, 8 / 32: 556.3, 64 / 8: 540.2,
+                        // 32 / 4: 536.5, 128 / 4: 569.1)
+                        const int left = qn - __hip_atomic_load(&sm->rhead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        nn = max(smin, min(64, (left + sdiv - 1) / sdiv));
+                    }
+                    c = atomicAdd(&sm->rhead, nn);
+                }
                 c = __builtin_amdgcn_readfirstlane(c);
+                nn = __builtin_amdgcn_readfirstlane(nn);
                 if (c >= qn) break;
                 KF_COUNT(11);
                 KF_ACC(9);
                 const int q = c + lane;
                 int u = 0, beg = 0, deg = 0;
                 double dun = 0.0;  // (KFH: the entry's distance, one HBM load per entry)
-                if (q < qn) {
+                if (lane < nn && q < qn) {
                     u = ring[(qhead + (unsigned)q) % R];
                     atomicAnd(&inq[u >> 6], ~(1ull << (u & 63)));  // (may be queued again below)
                     beg = rowl[u];
@@ -398,7 +422,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                 KF_ACC(12);
                 // (every queued vertex has an out-arc -- the graph is strongly connected -- so
                 // the slice's non-empty entries are lanes 0 .. R-1)
-                const bool valid = q < qn;
+                const bool valid = lane < nn && q < qn;
                 unsigned long long* wm4 = sm->wmark[tid >> 6];
                 // one trip: owners, then the trip's arc loads issued (not waited on).  owners:
                 // each entry marks its start in the window (of 64 positions) that holds it; the

@@ -74,10 +74,16 @@ constexpr int KF_HUB = 24;  // phase B: vertices of more in-arcs are done by a w
 #define KFH_SMIN 8
 #endif
 #ifndef KF_SDIV
-#define KF_SDIV 0  // the same for the LDS kernels (0: 64-entry slices)
+#define KF_SDIV 16  // the same for the 1024-thread LDS kernel (0: 64-entry slices)
 #endif
 #ifndef KF_SMIN
 #define KF_SMIN 8
+#endif
+#ifndef KF_SDIV4
+#define KF_SDIV4 4  // ... and for 256-thread workgroups
+#endif
+#ifndef KF_SMIN4
+#define KF_SMIN4 16
 #endif
 #ifndef KFH_HUB
 #define KFH_HUB KF_HUB  // (KFH's threshold; C4f 12 / 24 / 48 / 96: 830 / 814 / 860 / 905 ms)
@@ -269,6 +275,9 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
     uint16_t* keyl = reinterpret_cast<uint16_t*>(smem + LH.key);  // (KFH only)
     const unsigned R = H ? (g.hring > 0 ? min(LH.ring, (unsigned)g.hring) : LH.ring) : (unsigned)n;  // ring entries
     const int tid = threadIdx.x, lane = tid & 63;
+    // ring-overflow flag by round parity (no barrier to reset it): 256-thread rows (KFH
+    // with it measured slower: C4f 541.4 against 534.2 ms)
+    constexpr bool kPar = B < 1024;
     for (int k = tid; k < 256; k += B) rtl[k] = k < g.nrtab ? g.rtab[k] : NAN;
 
     for (int i = blockIdx.x; i < ns; i += gridDim.x) {
@@ -382,7 +391,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             __syncthreads();  // every wave has read the round's end before any wave queues more
             // (the other parity's flag was read by every thread before this barrier)
             // (an atomic and: waves already in this round may be setting this parity's bit)
-            if (B < 1024 && tid == 0) atomicAnd(&sm->ovf, ~(1 << (rpar ^ 1)));
+            if (kPar && tid == 0) atomicAnd(&sm->ovf, ~(1 << (rpar ^ 1)));
             // waves pull 64-entry slices of the round's entries (no block barrier inside a
             // round); a slice's arcs are spread over its lanes, 4 positions per lane and trip,
             // owners by a binary search over the slice's lane offsets (ds_bpermute), the 8
@@ -390,12 +399,16 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             for (;;) {
                 int c = 0, nn = 64;
                 if (lane == 0) {
-                    constexpr int sdiv = H ? KFH_SDIV : KF_SDIV, smin = H ? KFH_SMIN : KF_SMIN;
+                    constexpr int sdiv = H ? KFH_SDIV : B >= 1024 ? KF_SDIV : KF_SDIV4,
+                                  smin = H ? KFH_SMIN : B >= 1024 ? KF_SMIN : KF_SMIN4;
                     if constexpr (sdiv > 0) {
                         // a round's entries in smaller slices as they run out, so the waves
                         // finish the round together (it ends at a barrier): KFH C4f 570.8 ->
                         // 534.5 ms at 32 / 8 (16 / 16: 542.9, 8 / 32: 556.3, 64 / 8: 540.2,
-                        // 32 / 4: 536.5, 128 / 4: 569.1)
+                        // 32 / 4: 536.5, 128 / 4: 569.1); LDS kernels, 1024 threads: C3f 10.42 ->
+                        // 9.47 ms at 16 / 8 (32 / 8: 9.80, 8 / 16: 9.75, 16 / 4: 9.51, 24 / 8: 9.69);
+                        // 256 threads: C2f 0.449 -> 0.436 ms at 4 / 16 (8 / 16: 0.444, 16 / 8:
+                        // 0.488, 32 / 8: 0.522)
                         const int left = qn - __hip_atomic_load(&sm->rhead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         nn = max(smin, min(64, (left + sdiv - 1) / sdiv));
                     }
@@ -493,7 +506,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                                         // round's end moves the whole ring to the pending bitmask
                                         const unsigned at = (unsigned)atomicAdd(&sm->qtail, 1);
                                         if (at - qhead < R) ring[at % R] = (uint16_t)v;
-                                        else if (B < 1024) atomicOr(&sm->ovf, 1 << rpar);
+                                        else if (kPar) atomicOr(&sm->ovf, 1 << rpar);
                                         else sm->ovf = 1;
                                     }
                                 } else {
@@ -563,7 +576,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                                     if (!(atomicOr(&inq[v >> 6], bit) & bit)) {
                                         const unsigned at = (unsigned)atomicAdd(&sm->qtail, 1);
                                         if (at - qhead < R) ring[at % R] = (uint16_t)v;
-                                        else if (B < 1024) atomicOr(&sm->ovf, 1 << rpar);
+                                        else if (kPar) atomicOr(&sm->ovf, 1 << rpar);
                                         else sm->ovf = 1;
                                     }
                                 } else {
@@ -633,7 +646,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                                     if (!(atomicOr(&inq[v >> 6], bit) & bit)) {
                                         const unsigned at = (unsigned)atomicAdd(&sm->qtail, 1);
                                         if (at - qhead < R) ring[at % R] = (uint16_t)v;
-                                        else if (B < 1024) atomicOr(&sm->ovf, 1 << rpar);
+                                        else if (kPar) atomicOr(&sm->ovf, 1 << rpar);
                                         else sm->ovf = 1;  // (a dropped push: see the relax above)
                                     }
                                 } else {
@@ -660,7 +673,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             __syncthreads();
             if (tid == 0) sm->rhead = 0;  // (every wave has left the loop above)
             qhead = qend;
-            if (B < 1024 ? (sm->ovf >> rpar) & 1 : sm->ovf) {  // (uniform) ring overflow: its vertices (inq) become pending, the ring empty
+            if (kPar ? (sm->ovf >> rpar) & 1 : sm->ovf) {  // (uniform) ring overflow: its vertices (inq) become pending, the ring empty
                 for (int k = tid; k < nw; k += B) {
                     const unsigned long long b = inq[k];
                     if (b) { pend[k] |= b; wmin[k] = 0ull; inq[k] = 0ull; }  // (0: a valid lower bound)
@@ -672,7 +685,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             // round's start, which spares a barrier per round: C2f 0.72 -> 0.45 ms; 1024-thread
             // rows keep the barrier, measured faster there: C3f 10.4 against 10.6-10.7 ms)
             rpar ^= 1;
-            if (B >= 1024) {
+            if (!kPar) {
                 __syncthreads();
                 if (tid == 0) sm->ovf = 0;  // (every thread has read it)
             }

@@ -168,6 +168,15 @@ def eval_rank(A, n, hubs, close, rk, owner, topset, label, samples):
                 if u not in seen:
                     seen.add(u); sd.append((u, off))
         plans[s] = sd
+    nl = getattr(eval_rank, "landmarks", 0)
+    if nl:  # rows with at most one direct gateway also take their nearest landmark as a seed
+        from scipy.sparse.csgraph import dijkstra as _dj
+        DL = _dj(A, indices=hubs[:nl])
+        direct = {s: sum(1 for u, _ in (plans[s] or []) if A[s, u] != 0) for s in samp}
+        for s in samp:
+            if plans[s] is not None and direct[s] <= 1:
+                q = int(np.argmin(DL[:, s]))
+                plans[s] = plans[s] + [(int(hubs[q]), float(DL[q, s]))]
     need = sorted(set(samp.tolist()) | set(hubs[:16].tolist()) | {u for v in plans.values() if v for u, _ in v})
     D = dijkstra(A, indices=need)
     idx = {v: i for i, v in enumerate(need)}
@@ -229,5 +238,7 @@ if __name__ == "__main__":
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--samples", type=int, default=150)
     ap.add_argument("--louvain", action="store_true")
+    ap.add_argument("--landmarks", type=int, default=0, help="partition: rows with <= 1 direct gateway add their nearest of L hub rows")
     a = ap.parse_args()
+    eval_rank.landmarks = a.landmarks
     gateways(a) if a.mode == "gateways" else partition(a)

@@ -151,7 +151,9 @@ struct KFHLayout {
         L.queue = o;
         const size_t room = o + 8 * 256 + 64 * 2 <= kLdsBudget ? (kLdsBudget - o - 8 * 256) / 2 : 64;
         L.ring = (unsigned)(room < (size_t)n ? room & ~(size_t)63 : (size_t)n);
-        o += a16(2 * (size_t)L.ring);
+        // (at least the 512 B per wave phase B's candidate slots take: small graphs' rings
+        // are shorter)
+        o += a16(std::max(2 * (size_t)L.ring, (size_t)(B / 64) * 512));
         L.rtab = o;  o += 8 * 256;
         L.total = o;
         L.ws_dist = 0;
@@ -741,6 +743,13 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
             // (each candidate's d[u] was an HBM load per trip: C4f phase B ~3.1 M cycles/row).
             int cnt = 0, bu = 0x7fffffff, ba = -1;
             const int A0 = __builtin_amdgcn_readfirstlane(a0);
+            // candidates counted per vertex by LDS atomics in the wave's 64-vertex slot array
+            // (count, first arc); a serial hand-off of each trip's candidates over the ballot
+            // (readlanes to the vertex's lane) took longer: C4f 535.2 -> 506.6 ms
+            uint32_t* pbs = reinterpret_cast<uint32_t*>(smem + LH.queue) + (tid >> 6) * 128;
+            pbs[lane] = 0u;
+            pbs[64 + lane] = 0xFFFFFFFFu;
+            __builtin_amdgcn_wave_barrier();
             // (the next trip's words loaded under this one, or eight positions per lane: C4f
             // 570.8 / 577.3 ms against 570.9)
             constexpr int BW = 4;  // arc positions per lane and trip
@@ -776,19 +785,20 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                     }
                 }
 #pragma unroll
-                for (int r = 0; r < BW; r++) {
-                    for (unsigned long long tb = __ballot(cq[r]); tb;) {
-                        const int l = __ffsll((long long)tb) - 1;
-                        tb &= tb - 1;
-                        const int jl = __builtin_amdgcn_readlane(jq[r], l);
-                        const int ul = __builtin_amdgcn_readlane(uq[r], l);
-                        if (lane == jl) {
-                            if (cnt == 0) { bu = ul; ba = base + r * 64 + l; }
-                            cnt++;
-                        }
+                for (int r = 0; r < BW; r++)
+                    if (cq[r]) {
+                        atomicAdd(&pbs[jq[r]], 1u);
+                        atomicMin(&pbs[64 + jq[r]], (uint32_t)(base + r * 64 + lane));
                     }
-                }
             }
+            __builtin_amdgcn_wave_barrier();
+            cnt = (int)pbs[lane];
+            if (cnt == 1) {
+                ba = (int)pbs[64 + lane];
+                if constexpr (PK) bu = (int)(g.ipk[ba] & 0xFFFFu);
+                else bu = g.col_in[ba];
+            }
+            __builtin_amdgcn_wave_barrier();  // (the slots are read before the next chunk clears them)
             if (scan && cnt >= 2) {
                 // the exact rule over this vertex's arcs: tight (fl(d[u] + w) == d[v], d[u]
                 // loaded for candidates only), minimum (d[u], u), the first arc on a full tie

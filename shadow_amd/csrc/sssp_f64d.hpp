@@ -85,6 +85,9 @@ constexpr int KF_HUB = 24;  // phase B: vertices of more in-arcs are done by a w
 #ifndef KF_SMIN4
 #define KF_SMIN4 16
 #endif
+#ifndef KFH_WQ
+#define KFH_WQ 4  // KFH reliability walks: targets per lane in flight (C4f 506.9 / 505.4 / 506.5 ms at 2 / 4 / 8)
+#endif
 #ifndef KFH_HUB
 #define KFH_HUB KF_HUB  // (KFH's threshold; C4f 12 / 24 / 48 / 96: 830 / 814 / 860 / 905 ms)
 #endif
@@ -725,16 +728,33 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
         (void)dnb;
         if (tid == 0) sm->rhead = 0;
         __syncthreads();
+        // the next chunk is taken, and its row starts and distances loaded, before this one's
+        // arcs are walked (its setup round trip under this chunk's: C4f 506.2 -> 504.6 ms)
+        auto grab = [&]() __attribute__((always_inline)) {
+            int c = 0;
+            if (lane == 0) c = atomicAdd(&sm->rhead, 64);
+            return __builtin_amdgcn_readfirstlane(c);
+        };
+        int cn = grab(), a0n = 0x7fffffff, aendn = 0;
+        unsigned long long dvn = kInfBits;
+        auto setup = [&](int c) __attribute__((always_inline)) {
+            if (c < n) {
+                const int vv = c + lane;
+                a0n = vv < n ? g.row_in[vv] : 0x7fffffff;
+                aendn = g.row_in[min(c + 64, n)];
+                dvn = vv < n ? dist[vv] : kInfBits;
+            }
+        };
+        setup(cn);
         for (;;) {
-            int c0 = 0;
-            if (lane == 0) c0 = atomicAdd(&sm->rhead, 64);
-            c0 = __builtin_amdgcn_readfirstlane(c0);
+            const int c0 = cn;
             if (c0 >= n) break;
             const int v = c0 + lane;
             const bool vok = v < n;
-            const int a0 = vok ? g.row_in[v] : 0x7fffffff;
-            const int aend = g.row_in[min(c0 + 64, n)];
-            const double dvr = vok ? as_d(dist[v]) : (double)INFINITY;
+            const int a0 = a0n, aend = aendn;
+            const double dvr = as_d(dvn);
+            cn = grab();
+            setup(cn);
             const bool scan = vok && v != s && dvr < INFINITY;
             const double dvt = scan ? dvr : -1.0;  // (-1: never tight -- the source, unreachable)
             // Candidates: the in-arcs whose key interval admits fl(d[u] + w) == d[v] -- every
@@ -990,13 +1010,13 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                 if (tid == 0) sm->flag = 0;
                 __syncthreads();
                 int deep = 0;
-                for (int j0 = tid; j0 < nt; j0 += 2 * B) {
-                    int t2[2], v2[2], ns2[2];
-                    unsigned long long lo2[2], hi2[2];
-                    bool go2[2];
-                    double R2[2];
+                for (int j0 = tid; j0 < nt; j0 += KFH_WQ * B) {
+                    int t2[KFH_WQ], v2[KFH_WQ], ns2[KFH_WQ];
+                    unsigned long long lo2[KFH_WQ], hi2[KFH_WQ];
+                    bool go2[KFH_WQ];
+                    double R2[KFH_WQ];
 #pragma unroll
-                    for (int h = 0; h < 2; h++) {
+                    for (int h = 0; h < KFH_WQ; h++) {
                         const int j = j0 + h * B;
                         const int t = j < nt ? tgt[j] : -1;
                         t2[h] = t; v2[h] = t; ns2[h] = 0; lo2[h] = hi2[h] = 0ull; go2[h] = false; R2[h] = NAN;
@@ -1005,9 +1025,15 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         if (t == s) R2[h] = isnan(sw_s) ? (double)NAN : cs * sr_s;
                         else if (rixl[t] != 255) go2[h] = true;  // (255: unreachable, NaN)
                     }
-                    for (int step = 0; (go2[0] || go2[1]) && step < n; step++) {
+                    auto anygo = [&]() __attribute__((always_inline)) {
+                        bool a = false;
 #pragma unroll
-                        for (int h = 0; h < 2; h++) {
+                        for (int h = 0; h < KFH_WQ; h++) a = a || go2[h];
+                        return a;
+                    };
+                    for (int step = 0; anygo() && step < n; step++) {
+#pragma unroll
+                        for (int h = 0; h < KFH_WQ; h++) {
                             if (!go2[h]) continue;
                             const int v = v2[h];
                             const unsigned r = rixl[v];
@@ -1022,9 +1048,9 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                             if (pv == s) go2[h] = false;
                         }
                     }
-                    if (go2[0] || go2[1]) deep = 1;  // (a parent cycle: cannot happen)
+                    if (anygo()) deep = 1;  // (a parent cycle: cannot happen)
 #pragma unroll
-                    for (int h = 0; h < 2; h++) {
+                    for (int h = 0; h < KFH_WQ; h++) {
                         const int j = j0 + h * B;
                         if (j >= nt) continue;
                         const int t = t2[h];

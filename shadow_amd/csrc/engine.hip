@@ -406,8 +406,8 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
         rc = upload(c, &c->d_kb_arc, packed);
         if (rc) return rc;
     }
-    // KD delta-stepping: bucket width ~ the 12th percentile of arc latencies (>= 1), so
-    // ~12% of arcs are light; light in-arcs are the tail of each (-w)-sorted in-row
+    // KD delta-stepping: bucket width ~ the 15th (22nd) percentile of arc latencies (>= 1),
+    // so ~15% (22%) of arcs are light; light in-arcs are the tail of each (-w)-sorted in-row
     const bool want_kd = !force || !strcmp(force, "kd") || !strcmp(force, "auto");
     if (want_kd && c->nnz > 0) {
         // one 1024-thread workgroup per CU when dist fills the LDS; smaller graphs run several
@@ -420,13 +420,14 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
         int delta = 1;
         if (const char* e = getenv("SHD_ROUTE_DELTA")) delta = std::max(1, atoi(e));
         else {
-            // 1024-thread rows: the 12th percentile (30 on C4; seeded rows expand few vertices
+            // 1024-thread rows: the 15th percentile (38 on C4; seeded rows expand few vertices
             // per bucket, so fewer, wider buckets pay: C4 57 -> 53 ms from the 6th percentile's
-            // 15; 20/45/60/90: 52.2/51.3/53.4/59.7 ms against 50.7).  256-thread rows (three
-            // compute waves) take the 18th (45 on C3: 3.00-3.03 ms against 3.06-3.12 at 30)
+            // 15.  Round-5 sweep, two reps each: 30/35/38-40/50/60 = 41.23-41.55/41.05/
+            // 41.04-41.40/41.90/42.92 ms).  256-thread rows (three compute waves) take the
+            // 22nd (55 on C3: 1.986 ms; 45/65/80 = 2.004-2.017/1.991/2.012-2.017 ms)
             std::vector<int> ws(c->nnz);
             for (int a = 0; a < c->nnz; a++) ws[a] = (int)w[a];
-            const size_t k = (size_t)c->nnz * (blk >= 1024 ? 12 : 18) / 100;
+            const size_t k = (size_t)c->nnz * (blk >= 1024 ? 15 : 22) / 100;
             std::nth_element(ws.begin(), ws.begin() + k, ws.end());
             delta = std::max(1, ws[k]);
         }

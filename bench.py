@@ -156,41 +156,61 @@ def cpu_baseline(g, sources, targets, budget_s: float):
     return par, faithful
 
 
-def load_pmc(cfg: str, n_src: int):
-    """The newest committed PMC summary for this config and launch size
-    (profiles/<round>_pmc_<cfg>.json written by tools/pmc_traffic.py), or None."""
+def build_id():
+    """This engine build's identity (shadow_amd/build.py source_id: flags + sources)."""
+    from shadow_amd import build
+    return build.source_id()
+
+
+def load_pmc(cfg: str, n_src: int, kernel: str):
+    """The newest committed PMC summary (profiles/<round>_pmc_<cfg>.json, tools/pmc_traffic.py)
+    for this config and launch size that was profiled on THIS build and holds `kernel`: its
+    per-launch bytes (fetch + write) of that kernel only.  None when there is none; the reason
+    is in the returned note."""
     # (exactly <round>_pmc_<cfg>.json: "c3" must not pick up a c3f summary)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{cfg}.json")))
+    bid = build_id()
+    note = f"no PMC summary for {cfg} at {n_src} sources per launch"
     for f in reversed(files):
         try:
             d = json.load(open(f))
-            if int(d.get("sources_per_launch", -1)) == n_src:
-                d["file"] = os.path.relpath(f, ROOT)
-                return d
         except Exception:
             continue
-    return None
+        if int(d.get("sources_per_launch", -1)) != n_src:
+            continue
+        if d.get("build_id") != bid:
+            note = (f"newest PMC summary {os.path.relpath(f, ROOT)} was profiled on build "
+                    f"{d.get('build_id')}, not this build {bid}: traffic not reported")
+            break  # (an older file is older still)
+        ks = {k: v for k, v in d.get("kernels", {}).items() if kernel in k}
+        if not ks:
+            note = f"{os.path.relpath(f, ROOT)} holds no {kernel} entry"
+            break
+        fetch = sum(float(v["fetch_bytes"]) for v in ks.values())
+        fetch_lo = sum(float(v.get("fetch_bytes_uncorrected", v["fetch_bytes"])) for v in ks.values())
+        write = sum(float(v.get("write_bytes", 0.0)) for v in ks.values())
+        return {"file": os.path.relpath(f, ROOT), "build_id": bid, "kernels": sorted(ks),
+                "bytes": fetch + write, "bytes_range": [fetch_lo + write, fetch + write],
+                "read_bytes": fetch, "write_bytes": write}, None
+    return None, note
 
 
-def load_traffic(cfg: str, n_src: int):
-    """HBM bytes per launch of the dominant kernel (PMC), or None."""
-    d = load_pmc(cfg, n_src)
-    return float(d["hbm_bytes_per_launch"]) if d else None
-
-
-def physical(cfg: str, n_src: int, n_tgt: int, kernel_s: float, peak_gbps: float):
-    """What the counters say beside the algorithmic model: HBM bytes actually moved per
-    launch and their rate, the writes against the compulsory output (16 B per pair),
-    and the time the output write alone needs at peak."""
+def physical(cfg: str, n_src: int, n_tgt: int, kernel_s: float, peak_gbps: float, kernel: str):
+    """What the counters say beside the algorithmic model: HBM bytes the line's kernel
+    actually moved per launch and their rate, the writes against the compulsory output (16 B
+    per pair), and the time the output write alone needs at peak."""
     out = 16.0 * n_src * n_tgt
     res = {"output_bytes": out, "output_floor_ms": out / (peak_gbps * 1e9) * 1e3}
-    d = load_pmc(cfg, n_src)
+    d, note = load_pmc(cfg, n_src, kernel)
     if d:
-        tot = float(d["hbm_bytes_per_launch"])
-        wr = sum(float(k.get("write_bytes", 0.0)) for k in d.get("kernels", {}).values())
-        res.update({"pmc_file": d["file"], "traffic_bytes": tot, "traffic_GBps": tot / kernel_s / 1e9,
-                    "traffic_frac": tot / kernel_s / 1e9 / peak_gbps, "write_bytes": wr,
-                    "write_amplification": wr / out if out else None})
+        tot = d["bytes"]
+        res.update({"pmc_file": d["file"], "pmc_kernels": d["kernels"], "pmc_build_id": d["build_id"],
+                    "traffic_bytes": tot, "traffic_bytes_range": d["bytes_range"],
+                    "traffic_GBps": tot / kernel_s / 1e9, "traffic_frac": tot / kernel_s / 1e9 / peak_gbps,
+                    "read_bytes": d["read_bytes"], "write_bytes": d["write_bytes"],
+                    "write_amplification": d["write_bytes"] / out if out else None})
+    else:
+        res["pmc_note"] = note
     return res
 
 
@@ -306,6 +326,7 @@ def main():
     d_min = torch.full((1,), float("inf"), dtype=torch.float64, device=dev)
     torch.cuda.synchronize()
 
+    l_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     k_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
 
@@ -315,10 +336,17 @@ def main():
         gathered["lat"], gathered["rel"] = allgather_payload(p_lat[:seg], p_rel[:seg], seg, dist)
 
     def step(t=None):
+        # a step is every SSSP of the table: a landmark-only plan (C3) recomputes its landmark
+        # rows, queue order and jobs first, inside rows_async.  The kernel-timing pass (t set)
+        # runs that part ahead of the events and the rows launch alone inside them, so that
+        # kernel_ms / roofline.achieved describe the rows kernel (landmark_ms beside it).
         if t is not None:
+            l_start[t].record(stream)
+            if ns:
+                plan.refresh_async(stream=sh)
             k_start[t].record(stream)
         if ns:
-            plan.rows_async(d_tgt, d_lat, d_rel, d_rmin, stream=sh)
+            plan.rows_async(d_tgt, d_lat, d_rel, d_rmin, stream=sh, reuse=t is not None)
         if t is not None:
             k_end[t].record(stream)
         eng.min_reduce_async(d_rmin, d_min, stream=sh)
@@ -339,6 +367,7 @@ def main():
     torch.cuda.synchronize()
     eng.sync(sh)
     kms = [k_start[t].elapsed_time(k_end[t]) for t in range(args.steps)]
+    lms = [l_start[t].elapsed_time(k_start[t]) for t in range(args.steps)]  # (0 unless landmark-only)
     split = None
     if gather:
         # compute / collective split: the runahead all-reduce and the table
@@ -396,10 +425,14 @@ def main():
     # kernel's HIP-event time; the counters' bytes beside it (traffic, traffic_frac)
     out_bytes = 16.0 * ns * nt
     achieved = out_bytes / kavg_s / 1e9
-    phys = physical(args.config, ns, nt, kavg_s, peak)
+    kname = {0: "sssp_rows_kernel", 1: "sssp_k32_kernel",
+             2: ("sssp_batch_rows_kernel" if eng.info["reserved"] == 1 else "sssp_batch_kernel"),
+             4: "sssp_delta_kernel", 5: "sssp_f64d_kernel"}.get(eng.info["kernel"], str(eng.info["kernel"]))
+    phys = physical(args.config, ns, nt, kavg_s, peak, kname)
     model_bytes = ns * b_src(n, nnz, nt)
     res = {
         "metric": "source-paths/sec",
+        "build_id": build_id(),
         "value": total_src * args.steps / dt,
         "unit": "source-paths/s",
         "n_gpus": world,
@@ -425,15 +458,16 @@ def main():
         "gteps": total_src * g.m_nonloop * args.steps / dt / 1e9,
         "pairs_per_s": total_src * nt * args.steps / dt,
         "kernel_ms": float(np.mean(kms)),
+        "landmark_ms": float(np.mean(lms)),
+        "step_contents": ("landmark rows (hub-row launch) + queue order and job records (3 kernels) + the rows "
+                          "launch + runahead min: every SSSP of the table" if plan.info["launches"] > 1 else
+                          "the rows launch (every row of the table) + runahead min"),
         "time_to_table_ms": t_plan * 1e3 + dt / args.steps * 1e3,
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
-            "traffic": load_traffic(args.config, ns),
+            "traffic": phys.get("traffic_bytes"),
             "traffic_frac": phys.get("traffic_frac"),
-            "kernel": {0: "sssp_rows_kernel", 1: "sssp_k32_kernel",
-                       2: ("sssp_batch_rows_kernel" if eng.info["reserved"] == 1
-                           else "sssp_batch_kernel+path_attr_kernel"),
-                       4: "sssp_delta_kernel", 5: "sssp_f64d_kernel"}.get(eng.info["kernel"], str(eng.info["kernel"])),
+            "kernel": kname,
             "model": "compulsory bytes per launch = the lat + rel output rows (16 B per source-target pair); "
                      "achieved = those bytes / the rows kernel's HIP-event time; traffic = PMC HBM bytes per "
                      "launch (profiles/), traffic_frac = traffic / kernel time / peak",
@@ -590,6 +624,7 @@ def bench_c5(args, torch, dist, world, rank, dev, barrier):
     if rank != 0:
         return
     relax = float(n) ** 3
+    k3_phys = physical("c5", n, n, k3_s, 8000.0, "direct_rows_kernel")
     # packed u16 min-plus: one v_pk_add_u16 + one v_pk_min_u16 per 2 relaxations, i.e. one packed
     # instruction per relaxation.  Nominal: 32 lanes/cycle/SIMD at 2.4 GHz; measured on MI355X
     # (tools/micro/pk_rate.hip, 8 waves/SIMD, independent chains: profiles/r03_pk_rate.txt):
@@ -597,7 +632,7 @@ def bench_c5(args, torch, dist, world, rank, dev, barrier):
     peak_nominal = 256 * 4 * 32 * 2.4e9
     peak_relax = 35.8e12
     res = {
-        "metric": "source-paths/sec", "value": n * args.steps / dt, "unit": "source-paths/s",
+        "metric": "source-paths/sec", "build_id": build_id(), "value": n * args.steps / dt, "unit": "source-paths/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": f"{g.name}: complete K{n} + self-loops, reference semantics = every pair DIRECT "
@@ -606,7 +641,8 @@ def bench_c5(args, torch, dist, world, rank, dev, barrier):
         "pairs_per_s": n * n * args.steps / dt,
         "kernel_ms": k3_s * 1e3,
         "roofline": {"bound": "hbm", "achieved": 32.0 * n * n / k3_s / 1e9, "peak": 8000.0, "unit": "GB/s",
-                     "frac": 32.0 * n * n / k3_s / 1e9 / 8000.0, "traffic": load_traffic("c5", n),
+                     "frac": 32.0 * n * n / k3_s / 1e9 / 8000.0, "traffic": k3_phys.get("traffic_bytes"),
+                     "traffic_frac": k3_phys.get("traffic_frac"), "physical": k3_phys,
                      "kernel": "direct_rows_kernel", "bytes_per_pair": 32,
                      "model": "SURVEY 8(d) K3: read lat + r (16 B) and write lat + rel (16 B) per pair"},
         "k4": {"fw_table_ms": fw_s * 1e3, "grelax_per_s": relax / fw_s / 1e9,

@@ -181,10 +181,22 @@ int shd_route_plan_get_info(const shd_route_plan_t* plan, shd_route_plan_info_t*
 /* positions (in the caller's source list) of this rank's output rows, in row order */
 int shd_route_plan_rows(const shd_route_plan_t* plan, int32_t* pos_out);
 /* this rank's rows of the plan: row r of d_lat / d_rel / d_row_min = source
- * src[pos[r]]; device pointers as shd_route_rows_async */
+ * src[pos[r]]; device pointers as shd_route_rows_async.  A landmark-only plan built on the
+ * device (256-thread contexts, and ranks with few rows per workgroup slot; info.launches 5)
+ * seeds every row from its nearest landmark rows (the highest-degree vertices' exact rows),
+ * and this call computes those landmark rows too, on the stream, before the rows: the
+ * landmark rows, the queue order and the job records are recomputed in every call, so every
+ * SSSP behind the table runs inside it.  SHD_ROUTE_PLAN_REUSE skips that and reuses the
+ * last computation (the plan's creation, or shd_route_plan_refresh_async), which a caller
+ * may run separately to time the rows launch alone; other plans ignore the flag. */
+#define SHD_ROUTE_PLAN_REUSE 0x200u
 int shd_route_rows_planned_async(shd_route_t* ctx, const shd_route_plan_t* plan, const int32_t* d_tgt,
                                  int32_t nt, int64_t ld, uint32_t flags, double* d_lat, double* d_rel,
                                  double* d_row_min, void* stream);
+/* the landmark rows, queue order and job records of a device-built landmark-only plan,
+ * enqueued on the stream (what shd_route_rows_planned_async runs first without
+ * SHD_ROUTE_PLAN_REUSE); SHD_ROUTE_OK and nothing enqueued for other plans */
+int shd_route_plan_refresh_async(shd_route_t* ctx, const shd_route_plan_t* plan, void* stream);
 
 /* ---- the eager fill of a dense Path cache ------------------------------------------
  * The front end's cache (shd_topology.h) replaces topology.c's hash of Paths
@@ -249,12 +261,15 @@ int shd_route_tri_payload_async(shd_route_t* ctx, const double* d_lat, const dou
  * chunk), whose copies wait for each chunk they land in -- so the fill's D2H overlaps the
  * pinning of the rest (C4's 13.3 GB triangle) instead of following it.  A caller's own
  * hipMemcpy into lazy memory must not span a 256 MiB chunk boundary (the runtime fails a
- * copy across two registrations).  shd_route_host_wait returns SHD_ROUTE_EDEVICE when a
- * chunk could not be registered (it stays pageable: usable, slower).  shd_route_host_free
- * takes either. */
+ * copy across two registrations).  shd_route_host_wait returns SHD_ROUTE_OK once every
+ * chunk is settled, including a chunk the runtime refused to register (it stays pageable:
+ * the fill's copies into it still complete, slower); shd_route_host_unpinned(p) waits the
+ * same way and returns how many bytes of p stayed pageable (0 = all pinned; for memory not
+ * from these allocators, 0).  shd_route_host_free takes either. */
 void* shd_route_host_alloc(size_t bytes);
 void* shd_route_host_alloc_lazy(size_t bytes);
 int shd_route_host_wait(void* p);
+int64_t shd_route_host_unpinned(void* p);
 void shd_route_host_free(void* p);
 
 /* KD liveness counters since the last reset (no reference equivalent): the longest single

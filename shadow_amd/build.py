@@ -37,6 +37,18 @@ def build_front(verbose: bool = False) -> str:
     return FRONT_OUT
 
 
+def source_id() -> str:
+    """Identity of the engine build: a hash of its compile flags and every source it is built
+    from.  bench.py writes it into its line and the PMC summaries carry the one they were
+    profiled under, so a line's counter bytes are only ever taken from the same build."""
+    import hashlib
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for p in SOURCES + HEADERS + [os.path.join(ROOT, "include", "shd_route.h")]:
+        h.update(os.path.basename(p).encode())
+        h.update(open(p, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True

@@ -546,7 +546,10 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                             hipFuncSetAttribute((const void*)kd_plan_rows_kernel<1024>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)hl) == hipSuccess) {
                             c->kd_hub_block = 1024; c->kd_hub_qcap = hq; c->kd_hub_lds = hl;
-                            c->kd_hub_delta = std::max(1, ws2[k12]);
+                            // (the light in-CSR above holds the in-arcs with w < delta, and a
+                            // row's fused parents are exact only if its bucket width is at most
+                            // that: the hub rows' 12th percentile never exceeds the context's)
+                            c->kd_hub_delta = std::min(delta, std::max(1, ws2[k12]));
                         }
                     }
                     if (const char* e = getenv("SHD_ROUTE_HUB1024")) if (atoi(e) == 0) c->kd_hub_block = 0;
@@ -1569,13 +1572,24 @@ struct shd_route_plan {
     uint16_t* d_drow = nullptr;    // row store
     uint32_t* d_prow = nullptr;
     uint64_t store_bytes = 0;
-    bool store_borrowed = false;   // d_drow / d_prow are the context's landmark rows (device-built landmark-only plans)
+    // Landmark-only plans built on the device (round 6: their landmark rows are part of every
+    // launch): shd_route_rows_planned_async first recomputes the nhub landmark rows into the
+    // plan's own store (one hub-row launch, jobs d_hjobs, ready flags d_hdone), then the queue
+    // order and the job records from them (plan_lmall_* kernels over d_sq / d_lv / d_key /
+    // d_slot), then the rows: every SSSP the table needs runs inside the launch sequence.
+    bool lm_step = false;
+    int nhub = 0, hub_grid = 0, klm = 0;
+    bool hub1024 = false;
+    KDJob* d_hjobs = nullptr;
+    int* d_hdone = nullptr;
+    int* d_sq = nullptr;
+    int* d_lv = nullptr;
+    int* d_slot = nullptr;
+    unsigned long long* d_key = nullptr;
     ~shd_route_plan() {
-        for (void* q : {(void*)d_jobs, (void*)d_next, (void*)d_src})
+        for (void* q : {(void*)d_jobs, (void*)d_next, (void*)d_src, (void*)d_drow, (void*)d_prow, (void*)d_hjobs,
+                        (void*)d_hdone, (void*)d_sq, (void*)d_lv, (void*)d_slot, (void*)d_key})
             if (q) (void)hipFree(q);
-        if (!store_borrowed)
-            for (void* q : {(void*)d_drow, (void*)d_prow})
-                if (q) (void)hipFree(q);
     }
 };
 
@@ -1674,6 +1688,18 @@ int device_store_rows(shd_route* c, const std::vector<int>& verts, DevBuf& dd, D
 // plans' roots, kept on the device in the row-store format (a plan copies them device to
 // device).  (Before round 3: 16 pseudo-random closeness rows, then the 16 (64) most central
 // vertices' rows in a second launch.)
+// the k highest-degree vertices (ties by id): the hub / landmark rows
+std::vector<int> hub_vertices(const shd_route* c, int k) {
+    const int n = c->n;
+    std::vector<int> ord(n);
+    std::iota(ord.begin(), ord.end(), 0);
+    auto deg = [&](int v) { return c->h_row.empty() ? 0 : c->h_row[v + 1] - c->h_row[v]; };
+    std::partial_sort(ord.begin(), ord.begin() + k, ord.end(), [&](int a, int b) {
+        return deg(a) != deg(b) ? deg(a) > deg(b) : a < b;
+    });
+    return std::vector<int>(ord.begin(), ord.begin() + k);
+}
+
 int ensure_hub_rows(shd_route* c, int k, bool host_close = true) {
     const int n = c->n;
     k = std::min(n, std::max(k, 16));
@@ -1681,19 +1707,14 @@ int ensure_hub_rows(shd_route* c, int k, bool host_close = true) {
     const long long rs = kd_row_stride(n);
     std::vector<uint16_t> hd;
     if ((int)c->lm_v.size() < k) {
-        std::vector<int> ord(n);
-        std::iota(ord.begin(), ord.end(), 0);
-        auto deg = [&](int v) { return c->h_row.empty() ? 0 : c->h_row[v + 1] - c->h_row[v]; };
-        std::partial_sort(ord.begin(), ord.begin() + k, ord.end(), [&](int a, int b) {
-            return deg(a) != deg(b) ? deg(a) > deg(b) : a < b;
-        });
-        std::vector<int> lv(ord.begin(), ord.begin() + k);
+        std::vector<int> lv = hub_vertices(c, k);
         DevBuf dd, dp;
         int rc = device_store_rows(c, lv, dd, dp, hd, host_close ? L : 0);
         if (rc) return rc;
-        // (the previous rows are retired, not freed: a device-built plan may still read them)
-        if (c->d_lm_drow) c->allocs.push_back(c->d_lm_drow);
-        if (c->d_lm_prow) c->allocs.push_back(c->d_lm_prow);
+        // (no plan keeps a pointer to these rows -- a plan copies them into its own store --
+        // so the previous ones are freed; hipFree waits for work still reading them)
+        if (c->d_lm_drow) (void)hipFree(c->d_lm_drow);
+        if (c->d_lm_prow) (void)hipFree(c->d_lm_prow);
         c->d_lm_drow = (uint16_t*)dd.p; dd.p = nullptr;
         c->d_lm_prow = (uint32_t*)dp.p; dp.p = nullptr;
         c->lm_v = lv;
@@ -1733,6 +1754,32 @@ int ensure_lm_host(shd_route* c) {
         return SHD_ROUTE_EDEVICE;
     }
     return SHD_ROUTE_OK;
+}
+
+// A device-built landmark-only plan's in-launch work (shd_route_plan::lm_step), enqueued on
+// st: the landmark rows into the plan's store, then the queue order and the job records
+// from them.  No host synchronisation: errors surface at the next shd_route_sync.
+int lm_refresh(shd_route* c, const shd_route_plan* P, hipStream_t st) {
+    const int n = c->n, nj = (int)P->row_pos.size();
+    const long long rs = kd_row_stride(n);
+    // (the hub-row launch's scratch: the context's, grown at plan creation to this grid)
+    if (!c->d_hub_ws || c->hub_ws_bytes < c->kd_stride * (size_t)P->hub_grid) return SHD_ROUTE_EINVAL;
+    if (hipMemsetAsync(P->d_hdone, 0, sizeof(int) * (1 + (size_t)P->nhub), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    DevDelta g = kd_args(c);
+    g.jobs = P->d_hjobs;
+    g.drow = P->d_drow; g.drow_out = P->d_drow; g.prow = P->d_prow; g.rstride = rs;
+    g.done = P->d_hdone + 1;
+    int rc = kd_launch(c, g, P->d_hdone, nullptr, P->nhub, nullptr, 0, 0, nullptr, nullptr, nullptr, st, true,
+                       c->d_hub_ws, P->hub_grid, P->hub1024);
+    if (rc) return rc;
+    if (hipMemsetAsync(P->d_next, 0, sizeof(int), st) != hipSuccess) return SHD_ROUTE_EDEVICE;  // (root count)
+    const int nb = (nj + 255) / 256;
+    hipLaunchKernelGGL(plan_lmall_keys_kernel, dim3(nb), dim3(256), 0, st, P->d_drow, rs, std::min(n, 16), P->d_sq, nj,
+                       P->d_key);
+    hipLaunchKernelGGL(plan_lmall_rank_kernel, dim3(nb), dim3(256), 8 * nj, st, P->d_key, nj, P->d_slot);
+    hipLaunchKernelGGL(plan_lmall_jobs_kernel, dim3(8 * (((nj + 15) / 16 + 7) / 8)), dim3(1024), 0, st, P->d_drow,
+                       P->d_prow, rs, P->d_lv, P->nhub, P->d_sq, P->d_slot, nj, P->klm, n, P->d_jobs, P->d_next);
+    return hip_check(hipGetLastError());
 }
 
 }  // namespace
@@ -1788,47 +1835,68 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     const int nmine = ns > rank ? (ns - rank + world - 1) / world : 0;
     if (want && lm_all && nland > 0 && nmine >= 2 && nmine <= PLAN_DEV_MAXJ && !env_off("SHD_ROUTE_GPUCHOICE") &&
         !env_off("SHD_ROUTE_LMALL_REV") && !env_off("SHD_ROUTE_PLANDEV")) {
-        int rc = ensure_hub_rows(c, nland, false);
-        if (rc) return rc;
+        // Round 6: the landmark rows are computed inside every launch sequence of the plan
+        // (lm_refresh), into the plan's own store; creating the plan runs that sequence once
+        // (for the root count and to surface errors now), the rows launch reads its results.
+        const int nh = std::min(n, std::max(nland, 16));
+        const std::vector<int> lv = hub_vertices(c, nh);
         t_close = since();
         std::vector<int> sq;
         sq.reserve(nmine);
         for (int p = rank; p < ns; p += world) { P->row_pos.push_back(p); sq.push_back(src[p]); }
         const int nj = (int)sq.size();
-        int klm = KD_SEEDS;
-        if (const char* e = getenv("SHD_ROUTE_LMSEEDS")) klm = std::max(1, std::min(KD_SEEDS, atoi(e)));
-        DevBuf dsq, dlv, dslot, dkey;
-        if (dsq.alloc(sizeof(int) * nj) || dlv.alloc(sizeof(int) * nland) || dslot.alloc(sizeof(int) * nj) ||
-            dkey.alloc(sizeof(unsigned long long) * nj) ||
-            hipMalloc((void**)&P->d_jobs, sizeof(KDJob) * (size_t)nj) != hipSuccess ||
-            hipMalloc((void**)&P->d_next, sizeof(int) * (1 + (size_t)nland)) != hipSuccess)
-            return SHD_ROUTE_ENOMEM;
-        if (hipMemcpy(dsq.p, sq.data(), sizeof(int) * nj, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(dlv.p, c->lm_v.data(), sizeof(int) * nland, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemset(P->d_next, 0, sizeof(int)) != hipSuccess)
-            return SHD_ROUTE_EDEVICE;
+        P->klm = KD_SEEDS;
+        if (const char* e = getenv("SHD_ROUTE_LMSEEDS")) P->klm = std::max(1, std::min(KD_SEEDS, atoi(e)));
         const long long rs = kd_row_stride(n);
+        P->nhub = nh;
+        P->hub1024 = c->kd_hub_block > 0 && nh <= 256;
+        P->hub_grid = std::min(nh, P->hub1024 ? 256 : std::max(256, c->kd_slots));
+        std::vector<KDJob> hj(nh);
+        for (int q = 0; q < nh; q++) {
+            std::memset(&hj[q], 0, sizeof(KDJob));
+            hj[q].row = -1; hj[q].s = lv[q]; hj[q].store = q; hj[q].nseed = 0;
+        }
+        if (hipMalloc((void**)&P->d_sq, sizeof(int) * nj) != hipSuccess ||
+            hipMalloc((void**)&P->d_lv, sizeof(int) * nh) != hipSuccess ||
+            hipMalloc((void**)&P->d_slot, sizeof(int) * nj) != hipSuccess ||
+            hipMalloc((void**)&P->d_key, sizeof(unsigned long long) * nj) != hipSuccess ||
+            hipMalloc((void**)&P->d_hjobs, sizeof(KDJob) * nh) != hipSuccess ||
+            hipMalloc((void**)&P->d_hdone, sizeof(int) * (1 + (size_t)nh)) != hipSuccess ||
+            hipMalloc((void**)&P->d_drow, sizeof(uint16_t) * (size_t)rs * nh) != hipSuccess ||
+            hipMalloc((void**)&P->d_prow, sizeof(uint32_t) * (size_t)rs * nh) != hipSuccess ||
+            hipMalloc((void**)&P->d_jobs, sizeof(KDJob) * (size_t)nj) != hipSuccess ||
+            hipMalloc((void**)&P->d_next, sizeof(int) * (1 + (size_t)nh)) != hipSuccess)
+            return SHD_ROUTE_ENOMEM;
+        const size_t wsb = c->kd_stride * (size_t)P->hub_grid;
+        if (c->hub_ws_bytes < wsb) {
+            if (c->d_hub_ws) (void)hipFree(c->d_hub_ws);
+            c->d_hub_ws = nullptr; c->hub_ws_bytes = 0;
+            if (hipMalloc((void**)&c->d_hub_ws, wsb) != hipSuccess) { c->d_hub_ws = nullptr; return SHD_ROUTE_ENOMEM; }
+            c->hub_ws_bytes = wsb;
+        }
+        if (hipMemcpy(P->d_sq, sq.data(), sizeof(int) * nj, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(P->d_lv, lv.data(), sizeof(int) * nh, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(P->d_hjobs, hj.data(), sizeof(KDJob) * nh, hipMemcpyHostToDevice) != hipSuccess)
+            return SHD_ROUTE_EDEVICE;
+        int rc;
         if ((rc = hip_check(hipFuncSetAttribute((const void*)plan_lmall_rank_kernel,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 8 * nj))))
             return rc;
-        const int nb = (nj + 255) / 256;
-        hipLaunchKernelGGL(plan_lmall_keys_kernel, dim3(nb), dim3(256), 0, 0, c->d_lm_drow, rs, std::min(n, 16),
-                           (const int*)dsq.p, nj, (unsigned long long*)dkey.p);
-        hipLaunchKernelGGL(plan_lmall_rank_kernel, dim3(nb), dim3(256), 8 * nj, 0, (const unsigned long long*)dkey.p, nj,
-                           (int*)dslot.p);
-        hipLaunchKernelGGL(plan_lmall_jobs_kernel, dim3(8 * (((nj + 15) / 16 + 7) / 8)), dim3(1024), 0, 0, c->d_lm_drow, c->d_lm_prow, rs,
-                           (const int*)dlv.p, nland, (const int*)dsq.p, (const int*)dslot.p, nj, klm, n, P->d_jobs,
-                           P->d_next);
+        P->row_pos.shrink_to_fit();
+        // (errors of earlier launches are reported by their own sync, not by this plan)
+        if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
+        if ((rc = take_err(c))) return rc;
+        if ((rc = lm_refresh(c, P.get(), nullptr))) return rc;
         int nroots = 0;
-        if ((rc = hip_check(hipGetLastError()))) return rc;
         if (hipMemcpy(&nroots, P->d_next, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return SHD_ROUTE_EDEVICE;
         if ((rc = take_err(c))) return rc;
-        P->d_drow = c->d_lm_drow; P->d_prow = c->d_lm_prow; P->store_borrowed = true;
-        P->nslots = 0; P->nland = nland; P->store_bytes = 0; P->nroots = nroots; P->seeded = 1;
+        P->lm_step = true;
+        P->nslots = 0; P->nland = nh; P->store_bytes = (uint64_t)nh * (uint64_t)rs * 6u; P->nroots = nroots;
+        P->seeded = 1;
         P->lvl_off = {0, nj};
         if (getenv("SHD_ROUTE_PLAN_DEBUG"))
             fprintf(stderr, "plan world %d rank %d: jobs %d levels 1, device-built landmark-only plan (%d landmarks, "
-                    "%d unseeded): hub rows done %.2f ms, plan total %.2f ms\n", world, rank, nj, nland, nroots,
+                    "%d unseeded), landmark rows in every launch: setup %.2f ms, plan total %.2f ms\n", world, rank, nj, nh, nroots,
                     1e3 * t_close, 1e3 * since());
         *out = P.release();
         return SHD_ROUTE_OK;
@@ -2533,7 +2601,7 @@ int shd_route_plan_get_info(const shd_route_plan_t* P, shd_route_plan_info_t* in
     if (!P || !info) return SHD_ROUTE_EINVAL;
     info->rows = (int32_t)P->row_pos.size();
     info->seeded = P->seeded;
-    info->launches = 1;
+    info->launches = P->lm_step ? 5 : 1;  // (landmark-only: hub rows, three plan kernels, rows)
     info->levels = P->seeded ? (int32_t)P->lvl_off.size() - 1 : 1;
     info->roots = P->nroots;
     info->helpers = P->nhelpers;
@@ -2550,6 +2618,13 @@ int shd_route_plan_rows(const shd_route_plan_t* P, int32_t* pos_out) {
     return SHD_ROUTE_OK;
 }
 
+int shd_route_plan_refresh_async(shd_route_t* c, const shd_route_plan_t* P, void* stream) {
+    if (!c || !P || P->c != c) return SHD_ROUTE_EINVAL;
+    if (!P->lm_step) return SHD_ROUTE_OK;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    return lm_refresh(c, P, (hipStream_t)stream);
+}
+
 int shd_route_rows_planned_async(shd_route_t* c, const shd_route_plan_t* P, const int32_t* d_tgt, int32_t nt,
                                  int64_t ld, uint32_t flags, double* d_lat, double* d_rel, double* d_row_min,
                                  void* stream) {
@@ -2558,6 +2633,10 @@ int shd_route_rows_planned_async(shd_route_t* c, const shd_route_plan_t* P, cons
     if (!P->seeded) return shd_route_rows_async(c, P->d_src, nr, d_tgt, nt, ld, flags, d_lat, d_rel, d_row_min, stream);
     hipStream_t st = (hipStream_t)stream;
     if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    if (P->lm_step && !(flags & SHD_ROUTE_PLAN_REUSE)) {
+        const int rc = lm_refresh(c, P, st);  // the landmark rows and the jobs, on this stream
+        if (rc) return rc;
+    }
     // one launch: jobs in level order from one queue; a seeded job waits for its seed's
     // ready flag (set once the kept row is complete, before that row's phase C)
     if (hipMemsetAsync(P->d_next, 0, sizeof(int) * (1 + (size_t)P->nslots), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
@@ -2655,6 +2734,8 @@ int fw_prepare(shd_route* c, hipStream_t st) {
     std::sort(rbits.begin(), rbits.end());
     rbits.erase(std::unique(rbits.begin(), rbits.end()), rbits.end());
     uint8_t* rixd = nullptr;
+    double* rtd = nullptr;
+    int nrt = 0;
     if (rbits.size() <= 255 && !getenv("SHD_ROUTE_FWDENSER")) {
         std::vector<double> rt(rbits.size());
         for (size_t q = 0; q < rbits.size(); q++) std::memcpy(&rt[q], &rbits[q], 8);
@@ -2670,20 +2751,28 @@ int fw_prepare(shd_route* c, hipStream_t st) {
             if (!c->directed) rix[(size_t)b * c->n + a] = idx(c->e_rel[e]);
         }
         if (hipMalloc((void**)&rixd, rix.size()) != hipSuccess ||
-            hipMalloc((void**)&c->d_fwrtab, sizeof(double) * 256) != hipSuccess ||
+            hipMalloc((void**)&rtd, sizeof(double) * 256) != hipSuccess ||
             hipMemcpy(rixd, rix.data(), rix.size(), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(c->d_fwrtab, rt.data(), sizeof(double) * rt.size(), hipMemcpyHostToDevice) != hipSuccess) {
-            for (void* q : {(void*)rixd, (void*)c->d_fwrtab}) if (q) (void)hipFree(q);
-            c->d_fwrtab = nullptr;
+            hipMemcpy(rtd, rt.data(), sizeof(double) * rt.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            for (void* q : {(void*)rixd, (void*)rtd}) if (q) (void)hipFree(q);
             return undo(SHD_ROUTE_ENOMEM);
         }
-        c->d_fwrix = rixd;
-        c->allocs.push_back(c->d_fwrix);
-        c->allocs.push_back(c->d_fwrtab);
-        c->fw_nrtab = (int)rt.size();
+        nrt = (int)rt.size();
     }
     hipLaunchKernelGGL(fw_inlist_kernel, dim3(c->n), dim3(1024), 4 * sp, st, c->d_W, c->n, np, sp, inl, pos);
-    if ((rc = hip_check(hipGetLastError()))) return undo(rc);
+    if ((rc = hip_check(hipGetLastError()))) {
+        for (void* q : {(void*)rixd, (void*)rtd}) if (q) (void)hipFree(q);
+        return undo(rc);
+    }
+    // (published only now: a failed step above leaves the context as it was, and a retry
+    // builds every table again)
+    if (rixd) {
+        c->d_fwrix = rixd;
+        c->d_fwrtab = rtd;
+        c->allocs.push_back(c->d_fwrix);
+        c->allocs.push_back(c->d_fwrtab);
+        c->fw_nrtab = nrt;
+    }
     c->d_fwD = D;
     c->d_fwinl = inl;
     c->d_fwpos = pos;
@@ -2906,6 +2995,7 @@ struct HostMap {
     bool whole_reg = false;
     std::atomic<int> next{0};
     std::atomic<bool> stop{false};
+    int fail_chunk = getenv("SHD_ROUTE_REGFAIL_CHUNK") ? atoi(getenv("SHD_ROUTE_REGFAIL_CHUNK")) : -1;
     std::mutex mu;
     std::condition_variable cv;
     std::vector<std::thread> th;
@@ -2927,7 +3017,9 @@ struct HostMap {
             char* a = p + (size_t)k * chunk;
             const size_t n = std::min(chunk, len - (size_t)k * chunk);
             for (size_t o = 0; o < n; o += 4096) a[o] = 0;  // (nothing else touches a pending chunk)
-            const bool ok = whole || hipHostRegister(a, n, hipHostRegisterPortable) == hipSuccess;
+            // (SHD_ROUTE_REGFAIL_CHUNK=k: chunk k is left unregistered, as when the runtime
+            // refuses it -- the non-fatal path's test)
+            const bool ok = whole || (k != fail_chunk && hipHostRegister(a, n, hipHostRegisterPortable) == hipSuccess);
             {
                 std::lock_guard<std::mutex> lk(mu);
                 state[k].store(ok ? 1 : 2, std::memory_order_release);
@@ -3026,12 +3118,23 @@ int shd_route_host_wait(void* p) {
     auto m = host_map_of(p);
     if (!m) return SHD_ROUTE_OK;
     m->wait_range(0, m->len);
-    // a chunk the runtime refused to register stays pageable: copies into it still work,
-    // slower, and the caller is told
-    if (!m->whole)
-        for (int k = 0; k < m->nchunk; k++)
-            if (m->state[k].load(std::memory_order_acquire) == 2) return SHD_ROUTE_EDEVICE;
+    // a chunk the runtime refused to register stays pageable: copies into it still work
+    // (slower) and the data is complete, so this is not an error; shd_route_host_unpinned
+    // counts such chunks
     return SHD_ROUTE_OK;
+}
+
+int64_t shd_route_host_unpinned(void* p) {
+    if (!p) return SHD_ROUTE_EINVAL;
+    auto m = host_map_of(p);
+    if (!m) return 0;
+    m->wait_range(0, m->len);
+    if (m->whole) return m->whole_reg ? 0 : (int64_t)m->len;
+    int64_t bytes = 0;
+    for (int k = 0; k < m->nchunk; k++)
+        if (m->state[k].load(std::memory_order_acquire) == 2)
+            bytes += (int64_t)std::min(m->chunk, m->len - (size_t)k * m->chunk);
+    return bytes;
 }
 
 void shd_route_host_free(void* p) {

@@ -308,6 +308,7 @@ __device__ inline void fw_restp_tile(uint16_t* __restrict__ D, int np, int kb, i
     }
     if (role >= 2) {
         // the closed pivot pn: one relaxed poll loop, one agent acquire, then plain loads
+        __shared__ int s_open;
         if (tid == 0) {
             int spin = 0;
             while (__hip_atomic_load(&flag[pn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && spin < (1 << 24)) {
@@ -315,12 +316,21 @@ __device__ inline void fw_restp_tile(uint16_t* __restrict__ D, int np, int kb, i
                 spin++;
             }
             // a pivot never published (a lost or stalled closing workgroup): the product
-            // below would read an open tile, so the launch reports a device error
-            if (spin >= (1 << 24)) raise_err(err, SHD_ROUTE_EDEVICE);
+            // would read an open tile, so the launch reports a device error and this tile
+            // keeps its values (the flag is read once more: it may have been published
+            // between the last poll and the loop's exit)
+            const bool open = spin >= (1 << 24) &&
+                              __hip_atomic_load(&flag[pn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+            if (open) raise_err(err, SHD_ROUTE_EDEVICE);
+            s_open = open ? 1 : 0;
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // (also: every thread's product is done with At / Bt)
+        if (s_open) {
+            fw_store_block<T>(D, np, ti, tj, r, c, acc);
+            return;
+        }
         if (role == 2) {
             // row panel: C = D* (x) C -- A = D* transposed, B = C as it now stands
             fw_stage<T>(D, np, pn, pn, At, true);

@@ -607,10 +607,15 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
                 }
                 KBT_MARK(t_b);
                 [[maybe_unused]] const int kmax = 4 * nb;  // stamps only
-                // fold source-first: the last arc walked is the first factor
-                double rr[KB_WQ];
+                // fold source-first: the last arc walked is the first factor.  The fold starts
+                // from (1.0 * f_s) * f_t, the reference's order (topology.c:1443-1462 multiplies
+                // both vertex factors before the first arc, :1499), so vertex loss is bit-exact
+                double c0t[KB_WQ], rr[KB_WQ];
 #pragma unroll
-                for (int q = 0; q < KB_WQ; q++) rr[q] = cs;
+                for (int q = 0; q < KB_WQ; q++) {
+                    c0t[q] = isnan(ft[q]) ? cs : cs * ft[q];
+                    rr[q] = c0t[q];
+                }
 #pragma unroll 1
                 for (int k4 = nb - 1; k4 >= 0; k4--) {
                     uint32_t wq[KB_WQ];
@@ -633,7 +638,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
                     const int t = tq[q];
                     int depth = 0;
                     for (int c = t; c != s && depth <= n; c = (int)(wb[c] & 0xFFFFu)) depth++;
-                    double r = cs;
+                    double r = c0t[q];
                     for (int lo = 1; lo <= depth && lo <= n; lo += 16) {
                         const int hi = min(depth, lo + 15);
                         int c = t;
@@ -670,7 +675,7 @@ __global__ __launch_bounds__(KB_BLOCK) void sssp_batch_rows_kernel(DevKB g, cons
                             Lv = Rv = NAN;
                         } else {
                             Lv = (double)dt;
-                            Rv = isnan(ft[q]) ? rr[q] : rr[q] * ft[q];
+                            Rv = rr[q];
                         }
                     }
                     if (lrow) __builtin_nontemporal_store(Lv, lrow + c0 + j);

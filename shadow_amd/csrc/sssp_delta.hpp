@@ -832,9 +832,16 @@ __device__ __attribute__((noinline)) void kd_output(const int i, const int s, co
                 for (int q = 0; q < KD_WQ; q++) any = any || cur[q] != s;
                 if (any) sm->deep = 1;  // the level sweep below redoes the row
             }
+            // the fold starts from (1.0 * f_s) * f_t: the reference multiplies both vertex
+            // factors before the first arc (topology.c:1443-1462, then :1499), so a walked
+            // row is bit-exact under vertex loss too (the level sweep below multiplies f_t
+            // last: within 1e-12)
+            double f2[KD_WQ];
+#pragma unroll
+            for (int q = 0; q < KD_WQ; q++) f2[q] = g.has_vf ? g.vf[(t2[q] >= 0 && t2[q] < n) ? t2[q] : s] : (double)NAN;
             double rr[KD_WQ];
 #pragma unroll
-            for (int q = 0; q < KD_WQ; q++) rr[q] = cs;
+            for (int q = 0; q < KD_WQ; q++) rr[q] = isnan(f2[q]) ? cs : cs * f2[q];
 #pragma unroll
             for (int k4 = NB - 1; k4 >= 0; k4--) {  // source-first: the last arc walked first
                 if (k4 >= nb) continue;  // (uniform)
@@ -852,9 +859,6 @@ __device__ __attribute__((noinline)) void kd_output(const int i, const int s, co
                     for (int q = 0; q < KD_WQ; q++) rr[q] *= x[q];
                 }
             }
-            double f2[KD_WQ];
-#pragma unroll
-            for (int q = 0; q < KD_WQ; q++) f2[q] = g.has_vf ? g.vf[(t2[q] >= 0 && t2[q] < n) ? t2[q] : s] : (double)NAN;
             double Rv[KD_WQ];
 #pragma unroll
             for (int q = 0; q < KD_WQ; q++) {
@@ -862,7 +866,7 @@ __device__ __attribute__((noinline)) void kd_output(const int i, const int s, co
                 Rv[q] = NAN;
                 if (t >= 0 && t < n) {
                     if (t == s) Rv[q] = isnan(sw_s) ? NAN : cs * sr_s;
-                    else Rv[q] = isnan(f2[q]) ? rr[q] : rr[q] * f2[q];
+                    else Rv[q] = rr[q];
                 }
             }
             if (KD_OUT) {

@@ -1080,13 +1080,15 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(4))) void sss
                         if (j >= nt) continue;
                         const int t = t2[h];
                         if (t >= 0 && t < n && t != s && rixl[t] != 255) {
-                            double x = cs;
+                            // from (1.0 * f_s) * f_t, the reference's order (topology.c:1443-1462,
+                            // then :1499): bit-exact under vertex loss
+                            const double ft = g.vf[t];
+                            double x = isnan(ft) ? cs : cs * ft;
                             for (int k = min(ns2[h], 16) - 1; k >= 0; k--) {
                                 const unsigned r = (unsigned)((k < 8 ? lo2[h] >> (8 * k) : hi2[h] >> (8 * (k - 8))) & 0xFFull);
                                 x *= rtl[r];
                             }
-                            const double ft = g.vf[t];
-                            R2[h] = isnan(ft) ? x : x * ft;
+                            R2[h] = x;
                         }
                         rrow[j] = R2[h];
                     }

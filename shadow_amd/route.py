@@ -24,6 +24,7 @@ ENOEDGE = -4
 EUNREACH = -5
 EUNSUPPORTED = -6
 DISPATCH = 0x1
+PLAN_REUSE = 0x200  # shd_route.h SHD_ROUTE_PLAN_REUSE
 PAYLOAD_LAT16 = 0x1
 FILL_LAT16 = 0x100
 
@@ -73,6 +74,7 @@ EXPORTS = (
     "shd_route_rows_planned_async", "shd_route_fw_table_async", "shd_route_fw_rows_async",
     "shd_route_fill_triangle", "shd_route_host_alloc", "shd_route_host_free", "shd_route_tri_payload_async",
     "shd_route_kd_stats", "shd_route_host_alloc_lazy", "shd_route_host_wait",
+    "shd_route_host_unpinned", "shd_route_plan_refresh_async",
 )
 
 _lib = None
@@ -117,6 +119,8 @@ def load_library():
     L.shd_route_host_alloc_lazy.argtypes = [C.c_size_t]
     L.shd_route_host_wait.restype = C.c_int
     L.shd_route_host_wait.argtypes = [P]
+    L.shd_route_host_unpinned.restype = C.c_int64
+    L.shd_route_host_unpinned.argtypes = [P]
     L.shd_route_fw_table_async.restype = C.c_int
     L.shd_route_fw_table_async.argtypes = [P, P]
     L.shd_route_fw_rows_async.restype = C.c_int
@@ -132,6 +136,8 @@ def load_library():
     L.shd_route_plan_rows.argtypes = [P, P]
     L.shd_route_rows_planned_async.restype = C.c_int
     L.shd_route_rows_planned_async.argtypes = [P, P, P, I32, I64, U32, P, P, P, P]
+    L.shd_route_plan_refresh_async.restype = C.c_int
+    L.shd_route_plan_refresh_async.argtypes = [P, P, P]
     L.shd_route_kd_stats.restype = C.c_int
     L.shd_route_kd_stats.argtypes = [P, P, I32]
     _lib = L
@@ -316,14 +322,24 @@ class RoutePlan:
         except Exception:
             pass
 
-    def rows_async(self, d_tgt, d_lat, d_rel, d_rowmin, stream=None, dispatch=True, ld=None):
+    def rows_async(self, d_tgt, d_lat, d_rel, d_rowmin, stream=None, dispatch=True, ld=None, reuse=False):
+        """The plan's rows (shd_route_rows_planned_async).  A device-built landmark-only plan
+        recomputes its landmark rows and job records first, unless reuse=True
+        (SHD_ROUTE_PLAN_REUSE: the last refresh_async's, for timing the rows launch alone)."""
         nt = int(d_tgt.numel())
         ld = nt if ld is None else int(ld)
         ptr = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        flags = (DISPATCH if dispatch else 0) | (PLAN_REUSE if reuse else 0)
         rc = load_library().shd_route_rows_planned_async(
-            self.eng._h, self._h, ptr(d_tgt), nt, ld, DISPATCH if dispatch else 0, ptr(d_lat), ptr(d_rel),
+            self.eng._h, self._h, ptr(d_tgt), nt, ld, flags, ptr(d_lat), ptr(d_rel),
             ptr(d_rowmin), C.c_void_p(stream) if stream else None)
         _check(rc, "shd_route_rows_planned_async")
+
+    def refresh_async(self, stream=None):
+        """The landmark rows, queue order and job records of a device-built landmark-only
+        plan (shd_route_plan_refresh_async); nothing for other plans."""
+        rc = load_library().shd_route_plan_refresh_async(self.eng._h, self._h, C.c_void_p(stream) if stream else None)
+        _check(rc, "shd_route_plan_refresh_async")
 
 
 def tri16_lines(na: int, i: int | None = None) -> int:
@@ -349,6 +365,13 @@ class PinnedBuffer:
 
     def wait(self):
         _check(load_library().shd_route_host_wait(C.c_void_p(self.ptr)), "shd_route_host_wait")
+
+    def unpinned(self) -> int:
+        """Bytes of the buffer the runtime refused to register (pageable: still usable)."""
+        n = int(load_library().shd_route_host_unpinned(C.c_void_p(self.ptr)))
+        if n < 0:
+            _check(n, "shd_route_host_unpinned")
+        return n
 
     def array(self):
         buf = (C.c_double * (self.nbytes // 8)).from_address(self.ptr)

@@ -2,8 +2,10 @@
 
 Latency must be bit-exact everywhere.  Reliability is bit-exact against the oracle's
 engine tie rule (ORC_TIE_MINKEY) when vertex factors are 1.0/absent, and matches
-igraph's tie rule wherever the shortest path is unique.  With non-unit vertex loss
-the engine multiplies f_t last: tolerance REL_TOL relative (north_star: 1e-12).
+igraph's tie rule wherever the shortest path is unique.  With non-unit vertex loss the
+walk kernels (KBF, KD) fold from (1.0 * f_s) * f_t as the reference does (topology.c:
+1443-1462, then :1499): bit-exact; the level-sweep kernels (K32, f64, KF) multiply f_t
+last: tolerance REL_TOL relative (north_star: 1e-12).
 """
 import numpy as np
 import pytest
@@ -65,7 +67,8 @@ def test_c2_vertex_loss_within_tol(route, oracle_mod, kernel):
     eng = route.RouteEngine(g)
     og = oracle_mod.OracleGraph(g)
     src = np.arange(3, g.n, 97, dtype=np.int32)
-    _check_rows(eng, og, oracle_mod, src, g.targets(), rel_exact=False)
+    # walk kernels (auto = KBF, KD): bit-exact; level sweeps: within REL_TOL
+    _check_rows(eng, og, oracle_mod, src, g.targets(), rel_exact=kernel in ("auto", "kd"))
 
 
 def test_hbm_resident_path(route, oracle_mod, monkeypatch):

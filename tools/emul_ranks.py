@@ -20,6 +20,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c4")
 ap.add_argument("--world", type=int, nargs="+", default=[8])
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--shared", action="store_true",
+                help="one context for every rank (else each rank builds its own, so its plan pays "
+                     "for its own hub rows, as a real rank's would)")
 a = ap.parse_args()
 g = config(a.config)
 eng = RouteEngine(g)
@@ -29,7 +32,11 @@ d_tgt = torch.from_numpy(np.ascontiguousarray(T, np.int32)).to(dev)
 st = torch.cuda.current_stream(dev)
 for W in a.world:
     res = []
+    ttt = []
     for r in range(W):
+        if not a.shared and (r > 0 or W != a.world[0]):
+            eng.close()
+            eng = RouteEngine(g)
         t0 = time.perf_counter()
         plan = eng.plan(T, W, r)
         tp = time.perf_counter() - t0
@@ -49,8 +56,11 @@ for W in a.world:
             ms.append(e0.elapsed_time(e1))
         info = plan.info
         res.append(min(ms))
+        ttt.append(tp * 1e3 + min(ms))
         print(f"W={W} rank {r}: rows {ns} helpers {info['helpers']} roots {info['roots']} levels {info['levels']} "
-              f"kernel {min(ms):.2f} ms (plan {tp * 1e3:.0f} ms)", flush=True)
+              f"launches {info['launches']} step {min(ms):.2f} ms (plan {tp * 1e3:.1f} ms, time to table "
+              f"{ttt[-1]:.2f} ms)", flush=True)
         del lat, rel, plan
         torch.cuda.empty_cache()
-    print(f"W={W}: max {max(res):.2f} ms  mean {np.mean(res):.2f} ms", flush=True)
+    print(f"W={W}: max {max(res):.2f} ms  mean {np.mean(res):.2f} ms  time-to-table max {max(ttt):.2f} ms",
+          flush=True)

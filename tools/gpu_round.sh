@@ -23,9 +23,8 @@ tests)
   ;;
 bench)
   for cfg in ${CFGS:-c4 c3 c2 c5 c3f c2f c4f}; do
-    extra="--no-cpu-baseline"; steps=20
+    extra=""; steps=20
     [ $cfg = c4f ] && steps=3
-    case $cfg in c4|c5|c3f|c4f) extra="" ;; esac
     SHD_ROUTE_PLAN_DEBUG=1 timeout -k 10 500 python -u bench.py --config $cfg --steps $steps --warmup 5 $extra \
         > gpurun_out/${TAG}_bench_$cfg.json 2> gpurun_out/${TAG}_bench_$cfg.err || { echo BENCH $cfg FAILED; tail gpurun_out/${TAG}_bench_$cfg.err; exit 1; }
     python -c "import json;d=json.load(open('gpurun_out/${TAG}_bench_$cfg.json'));print('$cfg', round(d['value']), 'ms/step', round(d['ms_per_step'],3), 'kernel', round(d['kernel_ms'],3), 'ttt', d.get('time_to_table_ms'), 'frac', round(d['roofline']['frac'],4), 'verified', d.get('verified_rows_vs_oracle'), 'k4', d.get('k4',{}).get('fw_table_ms'), 'cpu', d.get('cpu_baseline') and (round(d['cpu_baseline']['value'],1), d['cpu_baseline']['cores']))"

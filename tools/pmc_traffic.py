@@ -27,6 +27,22 @@ def load(path):
     return agg
 
 
+def bench_build_id(logs):
+    """The build id bench.py printed in the profiled runs' JSON lines (both passes must agree)."""
+    ids = set()
+    for f in logs:
+        if not os.path.exists(f):
+            continue
+        for ln in open(f, errors="replace"):
+            ln = ln.strip()
+            if ln.startswith("{") and '"build_id"' in ln:
+                try:
+                    ids.add(json.loads(ln)["build_id"])
+                except Exception:
+                    pass
+    return ids.pop() if len(ids) == 1 else None
+
+
 def main(src_dir, out, cfg, sources, only=None):
     fetch = load(os.path.join(src_dir, "fetch_counter_collection.csv"))
     write = load(os.path.join(src_dir, "write_counter_collection.csv"))
@@ -41,7 +57,9 @@ def main(src_dir, out, cfg, sources, only=None):
                      "write_bytes": 1024 * sum(w) / len(w)}
     tot = sum(v["fetch_bytes"] + v["write_bytes"] for v in per.values())
     lo = sum(v["fetch_bytes_uncorrected"] + v["write_bytes"] for v in per.values())
-    res = {"config": cfg, "sources_per_launch": sources, "hbm_bytes_per_launch": tot,
+    # the bench lines of the two passes (tools/prof_round.sh: <dir>_FETCH_SIZE.log / _WRITE_SIZE.log)
+    build = bench_build_id([src_dir.rstrip("/") + "_FETCH_SIZE.log", src_dir.rstrip("/") + "_WRITE_SIZE.log"])
+    res = {"config": cfg, "sources_per_launch": sources, "build_id": build, "hbm_bytes_per_launch": tot,
            "hbm_bytes_per_launch_range": [lo, tot], "kernels": per,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
                      "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction)",

@@ -321,6 +321,14 @@ def main():
         dist.all_gather_object(pos_by_rank, pos)
         tindex = TriangleIndex(pos_by_rank, nt, seg)
         gathered = {}
+    # landmark-only plans split over ranks (C3-class): each rank computes its share of the
+    # landmark rows and the shares are all-gathered in the step (an emulated rank, one GPU:
+    # its share only, the others' rows present from the plan's creation, exchange unmeasured)
+    from shadow_amd.route import REFRESH_MINE, REFRESH_JOBS
+    from shadow_amd.shard import bind_landmark_store, exchange_landmarks, landmark_exchange_bytes
+    ew = int(args.emulate.split(":")[0]) if args.emulate and world == 1 else world
+    lm_split = ew > 1 and not weak and ns > 0 and plan.landmarks() is not None
+    lm_store = bind_landmark_store(plan, world, dev) if lm_split and world > 1 else None
     # +inf: a rank with an empty shard contributes nothing to the runahead MIN
     d_rmin = torch.full((max(ns, 1),), float("inf"), dtype=torch.float64, device=dev)
     d_min = torch.full((1,), float("inf"), dtype=torch.float64, device=dev)
@@ -342,11 +350,16 @@ def main():
         # kernel_ms / roofline.achieved describe the rows kernel (landmark_ms beside it).
         if t is not None:
             l_start[t].record(stream)
-            if ns:
-                plan.refresh_async(stream=sh)
+        if lm_split:
+            plan.refresh_async(stream=sh, what=REFRESH_MINE)
+            exchange_landmarks(lm_store, dist)
+            plan.refresh_async(stream=sh, what=REFRESH_JOBS)
+        elif t is not None and ns:
+            plan.refresh_async(stream=sh)
+        if t is not None:
             k_start[t].record(stream)
         if ns:
-            plan.rows_async(d_tgt, d_lat, d_rel, d_rmin, stream=sh, reuse=t is not None)
+            plan.rows_async(d_tgt, d_lat, d_rel, d_rmin, stream=sh, reuse=(t is not None) or lm_split)
         if t is not None:
             k_end[t].record(stream)
         eng.min_reduce_async(d_rmin, d_min, stream=sh)
@@ -459,8 +472,10 @@ def main():
         "pairs_per_s": total_src * nt * args.steps / dt,
         "kernel_ms": float(np.mean(kms)),
         "landmark_ms": float(np.mean(lms)),
-        "step_contents": ("landmark rows (hub-row launch) + queue order and job records (3 kernels) + the rows "
-                          "launch + runahead min: every SSSP of the table" if plan.info["launches"] > 1 else
+        "step_contents": (("this rank's share of the landmark rows + their all-gather over the ranks + queue order "
+                           "and job records (3 kernels) + the rows launch + runahead min" if lm_split else
+                           "landmark rows (hub-row launch) + queue order and job records (3 kernels) + the rows "
+                           "launch + runahead min: every SSSP of the table") if plan.info["launches"] > 1 else
                           "the rows launch (every row of the table) + runahead min"),
         "time_to_table_ms": t_plan * 1e3 + dt / args.steps * 1e3,
         "roofline": {
@@ -484,6 +499,12 @@ def main():
                         "it measures work avoided, not bandwidth used"},
         },
         "plan": {**plan.info, "plan_seconds": t_plan},
+        "landmark_split": ({**plan.landmarks(), "exchange_bytes_per_rank": (world - 1) * -(-plan.landmarks()["nland"] // ew)
+                            * plan.landmarks()["row_stride"] * 6 if world > 1 else None,
+                            "emulated_exchange_bytes": (ew - 1) * -(-plan.landmarks()["nland"] // ew)
+                            * plan.landmarks()["row_stride"] * 6,
+                            "note": "emulated rank: the exchange is not run (unmeasured on hardware)"
+                            if world == 1 else "exchange inside the step"} if lm_split else None),
         "runahead_min_latency_ms": runahead,
         "verified_rows_vs_oracle": verified,
     }

@@ -172,6 +172,8 @@ typedef struct shd_route_plan_info {
     int32_t stored_rows;   /* rows kept in the row store */
     int32_t world, rank;
     uint64_t store_bytes;  /* device bytes of the row store */
+    int32_t delta;         /* the rows' bucket width (ms; at most the context's, info.reserved) */
+    int32_t pad_;
 } shd_route_plan_info_t;
 
 int shd_route_plan_create(shd_route_t* ctx, const int32_t* src, int32_t ns, int32_t world, int32_t rank,
@@ -194,9 +196,28 @@ int shd_route_rows_planned_async(shd_route_t* ctx, const shd_route_plan_t* plan,
                                  int32_t nt, int64_t ld, uint32_t flags, double* d_lat, double* d_rel,
                                  double* d_row_min, void* stream);
 /* the landmark rows, queue order and job records of a device-built landmark-only plan,
- * enqueued on the stream (what shd_route_rows_planned_async runs first without
- * SHD_ROUTE_PLAN_REUSE); SHD_ROUTE_OK and nothing enqueued for other plans */
-int shd_route_plan_refresh_async(shd_route_t* ctx, const shd_route_plan_t* plan, void* stream);
+ * enqueued on the stream; SHD_ROUTE_OK and nothing enqueued for other plans.  `what`:
+ * SHD_ROUTE_REFRESH_ALL computes every landmark row into the plan's store,
+ * SHD_ROUTE_REFRESH_MINE only this rank's share (shd_route_plan_landmarks), and
+ * SHD_ROUTE_REFRESH_JOBS derives the queue order and the job records from the store as it
+ * stands; 0 = ALL | JOBS, what shd_route_rows_planned_async runs first without
+ * SHD_ROUTE_PLAN_REUSE.  A multi-GPU rank runs MINE, exchanges the store slots with the
+ * other ranks (an all-gather of equal shares), then JOBS and the rows with
+ * SHD_ROUTE_PLAN_REUSE: each landmark row is computed once per job instead of once per rank.
+ * No reference equivalent (Shadow 1.14 has no multi-process path, master.c:414-416). */
+#define SHD_ROUTE_REFRESH_ALL 0x1u
+#define SHD_ROUTE_REFRESH_MINE 0x2u
+#define SHD_ROUTE_REFRESH_JOBS 0x4u
+int shd_route_plan_refresh_async(shd_route_t* ctx, const shd_route_plan_t* plan, uint32_t what, void* stream);
+/* the landmark store of such a plan: nland rows of row_stride u16 distances (d_drow) and as
+ * many u32 parent records (d_prow), slot k = landmark k; this rank's share is the slots
+ * [first, first + count).  SHD_ROUTE_EUNSUPPORTED for other plans. */
+int shd_route_plan_landmarks(const shd_route_plan_t* plan, int32_t* nland, int32_t* first, int32_t* count,
+                             int64_t* row_stride);
+/* moves the plan's landmark store into caller memory (nland * row_stride elements each,
+ * device, kept alive by the caller for the plan's lifetime), e.g. buffers a collective
+ * library can all-gather into; the current contents are copied.  Blocks. */
+int shd_route_plan_bind_store(shd_route_t* ctx, shd_route_plan_t* plan, uint16_t* d_drow, uint32_t* d_prow);
 
 /* ---- the eager fill of a dense Path cache ------------------------------------------
  * The front end's cache (shd_topology.h) replaces topology.c's hash of Paths

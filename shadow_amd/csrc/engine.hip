@@ -120,6 +120,7 @@ struct shd_route {
     // the planner's unseeded hub rows on 256-thread contexts (C3): 1024-thread workgroups,
     // one row per CU, cut the latency of that launch (each row is unseeded and alone)
     int kd_hub_block = 0, kd_hub_qcap = 0, kd_hub_delta = 1;
+    int kd_delta_narrow = 1;  // the 12th percentile of arc latencies (<= kd_delta): split-rank plans
     size_t kd_hub_lds = 0;
     int* d_kd_lstart = nullptr;   // light in-CSR offsets (n+1)
     uint32_t* d_kd_orec = nullptr;  // out-arc records v | w << 16
@@ -532,6 +533,17 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 }
                 if (rc) return rc;
                 c->kd = 1; c->kd_block = blk; c->kd_lds = lds; c->kd_delta = delta; c->kd_qcap = qcap;
+                {
+                    // a narrower width for plans whose rows are mostly weakly seeded (a rank of a
+                    // multi-GPU split: its rows' seeds are often on other ranks).  Any width up
+                    // to the context's is exact: the light in-CSR above holds every in-arc with
+                    // w < delta, a superset of the narrower width's light arcs
+                    std::vector<int> ws3(c->nnz);
+                    for (int a = 0; a < c->nnz; a++) ws3[a] = (int)w[a];
+                    const size_t k12 = (size_t)c->nnz * 12 / 100;
+                    std::nth_element(ws3.begin(), ws3.begin() + k12, ws3.end());
+                    c->kd_delta_narrow = std::min(delta, std::max(1, ws3[k12]));
+                }
                 if (blk < 1024 && !getenv("SHD_ROUTE_DELTA") && !getenv("SHD_ROUTE_QCAP")) {
                     // hub rows in 1024-thread workgroups: that block's queue and bucket width
                     const size_t hb = kd_lds_bytes<1024>(n, 0);
@@ -1563,6 +1575,7 @@ struct shd_route_plan {
     shd_route* c = nullptr;
     int world = 1, rank = 0, ns_all = 0;
     int seeded = 0, nroots = 0, nhelpers = 0, nslots = 0;
+    int delta = 1;                 // bucket width of the rows (<= the context's kd_delta)
     int nland = 0;                 // landmark seed rows after the kept rows' slots (flags preset)
     std::vector<int32_t> row_pos;  // caller-list position of each output row of this rank
     std::vector<int> lvl_off;      // jobs of launch k: [lvl_off[k], lvl_off[k + 1])
@@ -1580,6 +1593,12 @@ struct shd_route_plan {
     bool lm_step = false;
     int nhub = 0, hub_grid = 0, klm = 0;
     bool hub1024 = false;
+    // multi-GPU landmark-only plans: this rank's share of the landmark rows (slots
+    // [lm_first, lm_first + lm_count), equal shares), the rest all-gathered from the other
+    // ranks by the caller (shd_route_plan_refresh_async with SHD_ROUTE_REFRESH_MINE, then the
+    // exchange into the store, then SHD_ROUTE_REFRESH_JOBS)
+    int lm_first = 0, lm_count = 0;
+    bool store_external = false;   // d_drow / d_prow are the caller's (shd_route_plan_bind_store)
     KDJob* d_hjobs = nullptr;
     int* d_hdone = nullptr;
     int* d_sq = nullptr;
@@ -1587,9 +1606,12 @@ struct shd_route_plan {
     int* d_slot = nullptr;
     unsigned long long* d_key = nullptr;
     ~shd_route_plan() {
-        for (void* q : {(void*)d_jobs, (void*)d_next, (void*)d_src, (void*)d_drow, (void*)d_prow, (void*)d_hjobs,
+        for (void* q : {(void*)d_jobs, (void*)d_next, (void*)d_src, (void*)d_hjobs,
                         (void*)d_hdone, (void*)d_sq, (void*)d_lv, (void*)d_slot, (void*)d_key})
             if (q) (void)hipFree(q);
+        if (!store_external)
+            for (void* q : {(void*)d_drow, (void*)d_prow})
+                if (q) (void)hipFree(q);
     }
 };
 
@@ -1759,19 +1781,30 @@ int ensure_lm_host(shd_route* c) {
 // A device-built landmark-only plan's in-launch work (shd_route_plan::lm_step), enqueued on
 // st: the landmark rows into the plan's store, then the queue order and the job records
 // from them.  No host synchronisation: errors surface at the next shd_route_sync.
-int lm_refresh(shd_route* c, const shd_route_plan* P, hipStream_t st) {
+// the hub-row launch's grid for k rows: up to 256 in 1024-thread workgroups (one per CU) where
+// the context's are smaller, more in the context's own
+inline bool hub_big(const shd_route* c, int k) { return c->kd_hub_block > 0 && k <= 256; }
+inline int hub_grid(const shd_route* c, int k) { return std::min(k, hub_big(c, k) ? 256 : std::max(256, c->kd_slots)); }
+
+int lm_refresh(shd_route* c, const shd_route_plan* P, uint32_t what, hipStream_t st) {
     const int n = c->n, nj = (int)P->row_pos.size();
     const long long rs = kd_row_stride(n);
-    // (the hub-row launch's scratch: the context's, grown at plan creation to this grid)
-    if (!c->d_hub_ws || c->hub_ws_bytes < c->kd_stride * (size_t)P->hub_grid) return SHD_ROUTE_EINVAL;
-    if (hipMemsetAsync(P->d_hdone, 0, sizeof(int) * (1 + (size_t)P->nhub), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
-    DevDelta g = kd_args(c);
-    g.jobs = P->d_hjobs;
-    g.drow = P->d_drow; g.drow_out = P->d_drow; g.prow = P->d_prow; g.rstride = rs;
-    g.done = P->d_hdone + 1;
-    int rc = kd_launch(c, g, P->d_hdone, nullptr, P->nhub, nullptr, 0, 0, nullptr, nullptr, nullptr, st, true,
-                       c->d_hub_ws, P->hub_grid, P->hub1024);
-    if (rc) return rc;
+    if (!what) what = SHD_ROUTE_REFRESH_ALL | SHD_ROUTE_REFRESH_JOBS;
+    if ((what & SHD_ROUTE_REFRESH_ALL) || (what & SHD_ROUTE_REFRESH_MINE)) {
+        const bool all = (what & SHD_ROUTE_REFRESH_ALL) != 0;
+        const int q0 = all ? 0 : P->lm_first, k = all ? P->nhub : P->lm_count;
+        // (the hub-row launch's scratch: the context's, grown at plan creation to this grid)
+        if (!c->d_hub_ws || c->hub_ws_bytes < c->kd_stride * (size_t)hub_grid(c, k)) return SHD_ROUTE_EINVAL;
+        if (hipMemsetAsync(P->d_hdone, 0, sizeof(int) * (1 + (size_t)P->nhub), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
+        DevDelta g = kd_args(c);
+        g.jobs = P->d_hjobs + q0;  // (a job's store slot is its global landmark index)
+        g.drow = P->d_drow; g.drow_out = P->d_drow; g.prow = P->d_prow; g.rstride = rs;
+        g.done = P->d_hdone + 1;
+        const int rc = kd_launch(c, g, P->d_hdone, nullptr, k, nullptr, 0, 0, nullptr, nullptr, nullptr, st, true,
+                                 c->d_hub_ws, hub_grid(c, k), hub_big(c, k));
+        if (rc) return rc;
+    }
+    if (!(what & SHD_ROUTE_REFRESH_JOBS)) return SHD_ROUTE_OK;
     if (hipMemsetAsync(P->d_next, 0, sizeof(int), st) != hipSuccess) return SHD_ROUTE_EDEVICE;  // (root count)
     const int nb = (nj + 255) / 256;
     hipLaunchKernelGGL(plan_lmall_keys_kernel, dim3(nb), dim3(256), 0, st, P->d_drow, rs, std::min(n, 16), P->d_sq, nj,
@@ -1794,6 +1827,13 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     for (int p = 0; p < ns; p++) if (src[p] < 0 || src[p] >= c->n) return SHD_ROUTE_EINVAL;
     auto P = std::make_unique<shd_route_plan>();
     P->c = c; P->world = world; P->rank = rank; P->ns_all = ns;
+    // bucket width: the context's, or for a rank of a multi-GPU split of 1024-thread rows the
+    // narrower 12th percentile (a split rank holds fewer well-seeded rows, and weakly seeded
+    // rows expand more vertices, which narrower buckets serve better: C4 8-way emulated 8.74
+    // -> 8.47 ms at 30 against 38, one GPU 41.1 -> 41.6 ms the other way round)
+    P->delta = c->kd_delta;
+    if (world > 1 && c->kd_block >= 1024 && !getenv("SHD_ROUTE_DELTA")) P->delta = c->kd_delta_narrow;
+    if (const char* e = getenv("SHD_ROUTE_PLAN_DELTA")) P->delta = std::max(1, std::min(c->kd_delta, atoi(e)));
     const auto t_start = std::chrono::steady_clock::now();
     double t_close = 0, t_land = 0, t_seeds = 0, t_store = 0, t_sched = 0, t_rk = 0, t_order = 0, t_hop = 0, t_loop0 = 0, t_alloc = 0, t_deps = 0;
     int n_recomp = 0;  // SHD_ROUTE_PLAN_DEBUG stage times
@@ -1849,8 +1889,12 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         if (const char* e = getenv("SHD_ROUTE_LMSEEDS")) P->klm = std::max(1, std::min(KD_SEEDS, atoi(e)));
         const long long rs = kd_row_stride(n);
         P->nhub = nh;
-        P->hub1024 = c->kd_hub_block > 0 && nh <= 256;
-        P->hub_grid = std::min(nh, P->hub1024 ? 256 : std::max(256, c->kd_slots));
+        P->hub1024 = hub_big(c, nh);
+        P->hub_grid = hub_grid(c, nh);
+        // a rank's share of the landmark rows (equal shares; the last rank's is the rest)
+        P->lm_count = (nh + world - 1) / world;
+        P->lm_first = std::min(nh, rank * P->lm_count);
+        P->lm_count = std::max(0, std::min(nh, P->lm_first + P->lm_count) - P->lm_first);
         std::vector<KDJob> hj(nh);
         for (int q = 0; q < nh; q++) {
             std::memset(&hj[q], 0, sizeof(KDJob));
@@ -1867,7 +1911,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             hipMalloc((void**)&P->d_jobs, sizeof(KDJob) * (size_t)nj) != hipSuccess ||
             hipMalloc((void**)&P->d_next, sizeof(int) * (1 + (size_t)nh)) != hipSuccess)
             return SHD_ROUTE_ENOMEM;
-        const size_t wsb = c->kd_stride * (size_t)P->hub_grid;
+        const size_t wsb = c->kd_stride * (size_t)std::max(P->hub_grid, hub_grid(c, std::max(1, P->lm_count)));
         if (c->hub_ws_bytes < wsb) {
             if (c->d_hub_ws) (void)hipFree(c->d_hub_ws);
             c->d_hub_ws = nullptr; c->hub_ws_bytes = 0;
@@ -1886,7 +1930,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         // (errors of earlier launches are reported by their own sync, not by this plan)
         if (hipDeviceSynchronize() != hipSuccess) return SHD_ROUTE_EDEVICE;
         if ((rc = take_err(c))) return rc;
-        if ((rc = lm_refresh(c, P.get(), nullptr))) return rc;
+        if ((rc = lm_refresh(c, P.get(), 0, nullptr))) return rc;
         int nroots = 0;
         if (hipMemcpy(&nroots, P->d_next, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return SHD_ROUTE_EDEVICE;
         if ((rc = take_err(c))) return rc;
@@ -2609,6 +2653,8 @@ int shd_route_plan_get_info(const shd_route_plan_t* P, shd_route_plan_info_t* in
     info->world = P->world;
     info->rank = P->rank;
     info->store_bytes = P->store_bytes;
+    info->delta = P->seeded ? P->delta : P->c->kd_delta;
+    info->pad_ = 0;
     return SHD_ROUTE_OK;
 }
 
@@ -2618,11 +2664,38 @@ int shd_route_plan_rows(const shd_route_plan_t* P, int32_t* pos_out) {
     return SHD_ROUTE_OK;
 }
 
-int shd_route_plan_refresh_async(shd_route_t* c, const shd_route_plan_t* P, void* stream) {
-    if (!c || !P || P->c != c) return SHD_ROUTE_EINVAL;
+int shd_route_plan_refresh_async(shd_route_t* c, const shd_route_plan_t* P, uint32_t what, void* stream) {
+    if (!c || !P || P->c != c || (what & ~(SHD_ROUTE_REFRESH_ALL | SHD_ROUTE_REFRESH_MINE | SHD_ROUTE_REFRESH_JOBS)))
+        return SHD_ROUTE_EINVAL;
     if (!P->lm_step) return SHD_ROUTE_OK;
     if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
-    return lm_refresh(c, P, (hipStream_t)stream);
+    return lm_refresh(c, P, what, (hipStream_t)stream);
+}
+
+int shd_route_plan_landmarks(const shd_route_plan_t* P, int32_t* nland, int32_t* first, int32_t* count,
+                             int64_t* row_stride) {
+    if (!P || !nland || !first || !count || !row_stride) return SHD_ROUTE_EINVAL;
+    if (!P->lm_step) return SHD_ROUTE_EUNSUPPORTED;
+    *nland = P->nhub; *first = P->lm_first; *count = P->lm_count;
+    *row_stride = kd_row_stride(P->c->n);
+    return SHD_ROUTE_OK;
+}
+
+int shd_route_plan_bind_store(shd_route_t* c, shd_route_plan_t* P, uint16_t* d_drow, uint32_t* d_prow) {
+    if (!c || !P || P->c != c || !d_drow || !d_prow) return SHD_ROUTE_EINVAL;
+    if (!P->lm_step) return SHD_ROUTE_EUNSUPPORTED;
+    if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
+    const size_t cells = (size_t)kd_row_stride(c->n) * P->nhub;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(d_drow, P->d_drow, sizeof(uint16_t) * cells, hipMemcpyDeviceToDevice) != hipSuccess ||
+        hipMemcpy(d_prow, P->d_prow, sizeof(uint32_t) * cells, hipMemcpyDeviceToDevice) != hipSuccess)
+        return SHD_ROUTE_EDEVICE;
+    if (!P->store_external) {
+        (void)hipFree(P->d_drow);
+        (void)hipFree(P->d_prow);
+    }
+    P->d_drow = d_drow; P->d_prow = d_prow; P->store_external = true;
+    return SHD_ROUTE_OK;
 }
 
 int shd_route_rows_planned_async(shd_route_t* c, const shd_route_plan_t* P, const int32_t* d_tgt, int32_t nt,
@@ -2634,7 +2707,7 @@ int shd_route_rows_planned_async(shd_route_t* c, const shd_route_plan_t* P, cons
     hipStream_t st = (hipStream_t)stream;
     if (hipSetDevice(c->device) != hipSuccess) return SHD_ROUTE_EDEVICE;
     if (P->lm_step && !(flags & SHD_ROUTE_PLAN_REUSE)) {
-        const int rc = lm_refresh(c, P, st);  // the landmark rows and the jobs, on this stream
+        const int rc = lm_refresh(c, P, 0, st);  // the landmark rows and the jobs, on this stream
         if (rc) return rc;
     }
     // one launch: jobs in level order from one queue; a seeded job waits for its seed's
@@ -2643,6 +2716,7 @@ int shd_route_rows_planned_async(shd_route_t* c, const shd_route_plan_t* P, cons
     if (P->nland && hipMemsetD32Async((hipDeviceptr_t)(P->d_next + 1 + P->nslots), 1, (size_t)P->nland, st) != hipSuccess)
         return SHD_ROUTE_EDEVICE;  // landmark rows: complete before the launch
     DevDelta k = kd_args(c);
+    k.delta = P->delta;
     k.drow = P->d_drow; k.drow_out = P->d_drow; k.prow = P->d_prow; k.rstride = kd_row_stride(c->n);
     k.jobs = P->d_jobs;
     k.done = P->d_next + 1;

@@ -25,6 +25,7 @@ EUNREACH = -5
 EUNSUPPORTED = -6
 DISPATCH = 0x1
 PLAN_REUSE = 0x200  # shd_route.h SHD_ROUTE_PLAN_REUSE
+REFRESH_ALL, REFRESH_MINE, REFRESH_JOBS = 0x1, 0x2, 0x4  # SHD_ROUTE_REFRESH_*
 PAYLOAD_LAT16 = 0x1
 FILL_LAT16 = 0x100
 
@@ -61,7 +62,7 @@ class _PlanInfo(C.Structure):
         ("rows", C.c_int32), ("seeded", C.c_int32), ("launches", C.c_int32), ("levels", C.c_int32),
         ("roots", C.c_int32),
         ("helpers", C.c_int32), ("stored_rows", C.c_int32), ("world", C.c_int32), ("rank", C.c_int32),
-        ("store_bytes", C.c_uint64),
+        ("store_bytes", C.c_uint64), ("delta", C.c_int32), ("pad_", C.c_int32),
     ]
 
 
@@ -74,7 +75,8 @@ EXPORTS = (
     "shd_route_rows_planned_async", "shd_route_fw_table_async", "shd_route_fw_rows_async",
     "shd_route_fill_triangle", "shd_route_host_alloc", "shd_route_host_free", "shd_route_tri_payload_async",
     "shd_route_kd_stats", "shd_route_host_alloc_lazy", "shd_route_host_wait",
-    "shd_route_host_unpinned", "shd_route_plan_refresh_async",
+    "shd_route_host_unpinned", "shd_route_plan_refresh_async", "shd_route_plan_landmarks",
+    "shd_route_plan_bind_store",
 )
 
 _lib = None
@@ -137,7 +139,12 @@ def load_library():
     L.shd_route_rows_planned_async.restype = C.c_int
     L.shd_route_rows_planned_async.argtypes = [P, P, P, I32, I64, U32, P, P, P, P]
     L.shd_route_plan_refresh_async.restype = C.c_int
-    L.shd_route_plan_refresh_async.argtypes = [P, P, P]
+    L.shd_route_plan_refresh_async.argtypes = [P, P, U32, P]
+    L.shd_route_plan_landmarks.restype = C.c_int
+    L.shd_route_plan_landmarks.argtypes = [P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                           C.POINTER(C.c_int64)]
+    L.shd_route_plan_bind_store.restype = C.c_int
+    L.shd_route_plan_bind_store.argtypes = [P, P, P, P]
     L.shd_route_kd_stats.restype = C.c_int
     L.shd_route_kd_stats.argtypes = [P, P, I32]
     _lib = L
@@ -305,7 +312,7 @@ class RoutePlan:
         self._h = h
         inf = _PlanInfo()
         _check(L.shd_route_plan_get_info(self._h, C.byref(inf)), "shd_route_plan_get_info")
-        self.info = {k: getattr(inf, k) for k, _ in _PlanInfo._fields_}
+        self.info = {k: getattr(inf, k) for k, _ in _PlanInfo._fields_ if not k.endswith("_")}
         pos = np.empty(max(1, self.info["rows"]), np.int32)
         _check(L.shd_route_plan_rows(self._h, _p(pos)), "shd_route_plan_rows")
         self.positions = pos[: self.info["rows"]]
@@ -335,11 +342,31 @@ class RoutePlan:
             ptr(d_rowmin), C.c_void_p(stream) if stream else None)
         _check(rc, "shd_route_rows_planned_async")
 
-    def refresh_async(self, stream=None):
+    def refresh_async(self, stream=None, what: int = 0):
         """The landmark rows, queue order and job records of a device-built landmark-only
-        plan (shd_route_plan_refresh_async); nothing for other plans."""
-        rc = load_library().shd_route_plan_refresh_async(self.eng._h, self._h, C.c_void_p(stream) if stream else None)
+        plan (shd_route_plan_refresh_async; what: REFRESH_ALL / REFRESH_MINE / REFRESH_JOBS,
+        0 = all landmark rows + jobs); nothing for other plans."""
+        rc = load_library().shd_route_plan_refresh_async(self.eng._h, self._h, int(what),
+                                                         C.c_void_p(stream) if stream else None)
         _check(rc, "shd_route_plan_refresh_async")
+
+    def landmarks(self):
+        """The landmark store of a device-built landmark-only plan: {nland, first, count,
+        row_stride} (this rank's share = slots [first, first + count)), or None."""
+        a, b, c, d = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+        rc = load_library().shd_route_plan_landmarks(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(d))
+        if rc == EUNSUPPORTED:
+            return None
+        _check(rc, "shd_route_plan_landmarks")
+        return {"nland": a.value, "first": b.value, "count": c.value, "row_stride": d.value}
+
+    def bind_store(self, d_drow, d_prow):
+        """Move the landmark store into caller tensors (int16 / int32, nland x row_stride at
+        least), which the plan keeps a reference to."""
+        rc = load_library().shd_route_plan_bind_store(self.eng._h, self._h, C.c_void_p(d_drow.data_ptr()),
+                                                      C.c_void_p(d_prow.data_ptr()))
+        _check(rc, "shd_route_plan_bind_store")
+        self._store = (d_drow, d_prow)
 
 
 def tri16_lines(na: int, i: int | None = None) -> int:

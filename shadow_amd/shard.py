@@ -154,3 +154,55 @@ def allgather_payload(lat_seg, rel_seg, seg: int, dist, group=None):
     dist.all_gather_into_tensor(byt(out_l), byt(pad(lat_seg)), group=group)
     dist.all_gather_into_tensor(out_r, pad(rel_seg), group=group)
     return out_l, out_r
+
+
+# ---- landmark rows of a multi-GPU landmark-only plan --------------------------------
+# A landmark-only plan (C3-class graphs) seeds every row from its nearest landmark rows (the
+# highest-degree vertices' exact rows).  Each rank computes an equal share of them
+# (RoutePlan.refresh_async(what=REFRESH_MINE)) and the shares are all-gathered into every
+# rank's store (u16 distances + u32 parent records per vertex, ~6 B x n per landmark: 57 MB
+# for C3's 1024), instead of every rank computing all of them.
+
+def bind_landmark_store(plan, world: int, device):
+    """Caller-owned store tensors for `plan` (padded to world equal shares), bound to the plan
+    (RoutePlan.bind_store): the buffers the all-gather writes.  None when the plan has no
+    landmark store (not landmark-only, or built on the host)."""
+    import torch
+    lm = plan.landmarks()
+    if lm is None:
+        return None
+    cnt = -(-lm["nland"] // world)
+    drow = torch.empty((cnt * world, lm["row_stride"]), dtype=torch.int16, device=device)
+    prow = torch.empty((cnt * world, lm["row_stride"]), dtype=torch.int32, device=device)
+    plan.bind_store(drow, prow)
+    return {"drow": drow, "prow": prow, "share": cnt, **lm}
+
+
+def exchange_landmarks(store, dist, group=None):
+    """All-gather every rank's share of the landmark rows into every rank's store (in place:
+    RCCL all_gather_into_tensor over xGMI for nccl; staged through host memory for gloo,
+    whose all-gather takes CPU tensors only).  Shares are equal (the store is padded)."""
+    world = dist.get_world_size(group) if dist is not None and dist.is_initialized() else 1
+    if world == 1 or store is None:
+        return
+    rank = dist.get_rank(group)
+    cnt = store["share"]
+    # (as bytes: neither RCCL nor gloo takes int16 tensors; a row of the store stays a row)
+    import torch
+    for buf in (store["drow"].view(torch.uint8), store["prow"].view(torch.uint8)):
+        mine = buf[rank * cnt:(rank + 1) * cnt]
+        if dist.get_backend(group) == "nccl":
+            dist.all_gather_into_tensor(buf, mine, group=group)
+        else:
+            outs = [buf[k * cnt:(k + 1) * cnt].cpu() for k in range(world)]
+            dist.all_gather(outs, mine.cpu().contiguous(), group=group)
+            for k in range(world):
+                if k != rank:
+                    buf[k * cnt:(k + 1) * cnt].copy_(outs[k])
+
+
+def landmark_exchange_bytes(store, world: int) -> int:
+    """Bytes each rank receives in exchange_landmarks (the other ranks' shares)."""
+    if store is None or world <= 1:
+        return 0
+    return (world - 1) * store["share"] * store["row_stride"] * 6

@@ -136,3 +136,60 @@ def test_triangle_payload_gather(world, oracle_mod):
     assert np.array_equal(decode_lat16(gl[k]), ref[ii, jj], equal_nan=True)
     assert np.array_equal(gr[k], rref[ii, jj])
     assert gl.nbytes + gr.nbytes <= 0.5 * 16 * na * na * world / world + 16 * world * na
+
+
+def _lm_worker(rank, world, port, q):
+    """Each rank fills only its share of a landmark store (the hub vertices' exact distance
+    rows as u16, a per-vertex record word), then exchange_landmarks all-gathers the shares."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle.oracle import OracleGraph, TIE_MINKEY
+    from shadow_amd.shard import exchange_landmarks, landmark_exchange_bytes
+    g = internet_like(120, 2, seed=23)
+    T = g.targets()
+    nland = 10  # (not a multiple of 3: the padded last share)
+    deg = np.bincount(np.concatenate([g.src, g.dst]), minlength=g.n)
+    hubs = sorted(range(g.n), key=lambda v: (-deg[v], v))[:nland]
+    rs = (g.n + 2 + 7) & ~7
+    cnt = -(-nland // world)
+    store = {"drow": torch.full((cnt * world, rs), -1, dtype=torch.int16),
+             "prow": torch.full((cnt * world, rs), -1, dtype=torch.int32),
+             "share": cnt, "nland": nland, "row_stride": rs}
+    og = OracleGraph(g)
+    for k in range(rank * cnt, min(nland, (rank + 1) * cnt)):
+        lat, _, _, _ = og.source_rows(np.array([hubs[k]], np.int32), T, TIE_MINKEY)
+        store["drow"][k, :g.n] = torch.from_numpy(lat[0].astype(np.int32)).to(torch.int16)
+        store["prow"][k, :g.n] = torch.arange(g.n, dtype=torch.int32) + 1000 * k
+    exchange_landmarks(store, dist)
+    q.put((rank, store["drow"][:nland, :g.n].numpy().copy(), store["prow"][:nland, :g.n].numpy().copy(),
+           landmark_exchange_bytes(store, world)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_landmark_store_exchange(world, oracle_mod):
+    """Round 6, multi-GPU landmark-only plans (C3 split over ranks): every rank ends with all
+    landmark rows although it computed only its share (bench.py: REFRESH_MINE, then this
+    exchange, then REFRESH_JOBS; RCCL all-gather in place on the GPU nodes)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lm_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    g = internet_like(120, 2, seed=23)
+    T = g.targets()
+    deg = np.bincount(np.concatenate([g.src, g.dst]), minlength=g.n)
+    hubs = sorted(range(g.n), key=lambda v: (-deg[v], v))[:10]
+    og = oracle_mod.OracleGraph(g)
+    want, _, _, _ = og.source_rows(np.array(hubs, np.int32), T, oracle_mod.TIE_MINKEY)
+    rs = (g.n + 2 + 7) & ~7
+    for rank, drow, prow, nbytes in got:
+        assert np.array_equal(drow.astype(np.int64), want.astype(np.int64)), rank
+        assert np.array_equal(prow, np.arange(g.n)[None, :] + 1000 * np.arange(10)[:, None]), rank
+        assert nbytes == (world - 1) * -(-10 // world) * rs * 6

@@ -79,3 +79,76 @@ def test_two_ranks_hip_rows_gathered(oracle_mod):
     olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(T[pos[keep]], T, oracle_mod.TIE_MINKEY)
     assert np.array_equal(lat[keep], olat) and np.array_equal(rel[keep], orel)
     assert mn == olat.min()
+
+
+def _lm_worker(rank, world, port, q):
+    """A landmark-only plan split over the ranks (round 6): each rank computes its share of
+    the landmark rows, the shares are all-gathered (gloo here, staged through host memory;
+    RCCL in place on the GPU nodes), then the job records and the rows."""
+    import torch
+    import torch.distributed as dist
+    torch.cuda.init()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["SHD_ROUTE_KERNEL"] = "kd"  # (a 3000-vertex graph would take KBF)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from shadow_amd import route
+    from shadow_amd.graph import internet_like
+    from shadow_amd.shard import allgather_rows, bind_landmark_store, exchange_landmarks
+    g = internet_like(3000, 3, seed=77, name="ba3000")
+    T = g.targets()
+    eng = route.RouteEngine(g)
+    plan = eng.plan(T, world, rank)
+    dev = torch.device("cuda", 0)
+    lm = plan.landmarks()
+    assert lm is not None and plan.info["launches"] == 5, plan.info
+    store = bind_landmark_store(plan, world, dev)
+    # poison the other ranks' shares: only the exchange can restore them
+    cnt = store["share"]
+    for k in range(world):
+        if k != rank:
+            store["drow"][k * cnt:(k + 1) * cnt] = 7
+    nr = plan.info["rows"]
+    d_tgt = torch.from_numpy(T.astype(np.int32)).to(dev)
+    d_lat = torch.empty((max(nr, 1), len(T)), dtype=torch.float64, device=dev)
+    d_rel = torch.empty_like(d_lat)
+    d_min = torch.full((max(nr, 1),), float("inf"), dtype=torch.float64, device=dev)
+    plan.refresh_async(what=route.REFRESH_MINE)
+    eng.sync()
+    exchange_landmarks(store, dist)
+    plan.refresh_async(what=route.REFRESH_JOBS)
+    plan.rows_async(d_tgt, d_lat, d_rel, d_min, dispatch=False, reuse=True)
+    eng.sync()
+    blk = torch.tensor([nr], dtype=torch.int64)
+    dist.all_reduce(blk, op=dist.ReduceOp.MAX)
+    n_total = int(blk.item()) * world
+    lat = allgather_rows(d_lat[:nr].cpu(), n_total, dist)
+    rel = allgather_rows(d_rel[:nr].cpu(), n_total, dist)
+    pos = allgather_rows(torch.from_numpy(np.pad(plan.positions.astype(np.int64), (0, int(blk.item()) - nr),
+                                                 constant_values=-1)).reshape(-1, 1), n_total, dist)
+    if rank == 0:
+        q.put((lat.numpy(), rel.numpy(), pos.numpy().ravel(), lm["count"], lm["nland"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_landmark_split(oracle_mod):
+    import torch.multiprocessing as mp
+    from shadow_amd.graph import internet_like
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    lat, rel, pos, cnt, nland = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    assert cnt == nland // 2
+    g = internet_like(3000, 3, seed=77, name="ba3000")
+    T = g.targets()
+    keep = pos >= 0
+    assert sorted(pos[keep].tolist()) == list(range(len(T)))
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(T[pos[keep]], T, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat[keep], olat) and np.array_equal(rel[keep], orel)

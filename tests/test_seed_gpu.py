@@ -60,6 +60,29 @@ def test_seeded_rows_bitexact(oracle_mod, kd, name, seeds, evcap):
     assert np.array_equal(mn, olat.min(axis=1))
 
 
+@pytest.mark.parametrize("pdelta", ["1", "7", "1000"])
+@pytest.mark.parametrize("name", ["ba400", "c2"])
+def test_plan_bucket_width_bitexact(oracle_mod, kd, name, pdelta):
+    """A plan's rows may take a narrower bucket width than the context's (round 6: ranks of a
+    split of 1024-thread rows take the 12th percentile); any width up to the context's is
+    exact (the light in-CSR holds the in-arcs below the context's width, a superset), and a
+    wider request is clamped to the context's."""
+    from shadow_amd import route
+    kd.setenv("SHD_ROUTE_PLAN_DELTA", pdelta)
+    g = _graph(name)
+    eng = route.RouteEngine(g)
+    T = g.targets()
+    S = T if name != "c2" else T[::3]
+    plan = eng.plan(S)
+    assert plan.info["seeded"] == 1
+    assert plan.info["delta"] == min(int(pdelta), eng.info["reserved"]), (plan.info, eng.info["reserved"])
+    lat, rel, mn = _plan_rows(eng, plan, T)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(S[plan.positions], T, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(rel, orel)
+    assert np.array_equal(mn, olat.min(axis=1))
+
+
 def test_seeded_equals_unseeded_shuffled_sources(kd):
     """Sources in arbitrary order with repeats: seeding picks seeds among the listed rows."""
     from shadow_amd import route
@@ -384,6 +407,8 @@ def test_c4_eight_rank_plans_balanced_and_golden(monkeypatch):
     for r in range(8):
         plan = eng.plan(T, 8, r)
         assert abs(plan.info["rows"] - 6250) <= 625, plan.info
+        # (split ranks of 1024-thread rows: the narrower 12th-percentile bucket width)
+        assert plan.info["delta"] == 30 and eng.info["reserved"] == 38, (plan.info, eng.info["reserved"])
         assert plan.info["helpers"] <= 2500, plan.info
         mine = [k for k, s in enumerate(plan.sources) if int(s) in want]
         if not mine:

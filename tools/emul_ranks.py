@@ -14,7 +14,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from shadow_amd.graph import config  # noqa: E402
-from shadow_amd.route import RouteEngine  # noqa: E402
+from shadow_amd.route import REFRESH_JOBS, REFRESH_MINE, RouteEngine  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c4")
@@ -44,13 +44,24 @@ for W in a.world:
         lat = torch.empty((max(ns, 1), len(T)), dtype=torch.float64, device=dev)
         rel = torch.empty_like(lat)
         mn = torch.full((max(ns, 1),), float("inf"), dtype=torch.float64, device=dev)
-        plan.rows_async(d_tgt, lat, rel, mn, stream=st.cuda_stream)
+        # a landmark-only plan's rank computes its share of the landmark rows and receives the
+        # rest (the all-gather is not run here: the other shares stay in the store from the
+        # plan's creation; its bytes are reported)
+        lm = plan.landmarks()
+        split = W > 1 and lm is not None
+
+        def run():
+            if split:
+                plan.refresh_async(stream=st.cuda_stream, what=REFRESH_MINE)
+                plan.refresh_async(stream=st.cuda_stream, what=REFRESH_JOBS)
+            plan.rows_async(d_tgt, lat, rel, mn, stream=st.cuda_stream, reuse=split)
+        run()
         eng.sync(st.cuda_stream)
         ms = []
         for _ in range(a.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
-            plan.rows_async(d_tgt, lat, rel, mn, stream=st.cuda_stream)
+            run()
             e1.record(st)
             eng.sync(st.cuda_stream)
             ms.append(e0.elapsed_time(e1))
@@ -59,7 +70,9 @@ for W in a.world:
         ttt.append(tp * 1e3 + min(ms))
         print(f"W={W} rank {r}: rows {ns} helpers {info['helpers']} roots {info['roots']} levels {info['levels']} "
               f"launches {info['launches']} step {min(ms):.2f} ms (plan {tp * 1e3:.1f} ms, time to table "
-              f"{ttt[-1]:.2f} ms)", flush=True)
+              f"{ttt[-1]:.2f} ms)" + (f" landmarks {lm['count']} of {lm['nland']}, exchange "
+                                      f"{(W - 1) * -(-lm['nland'] // W) * lm['row_stride'] * 6 / 1e6:.1f} MB in"
+                                      if split else ""), flush=True)
         del lat, rel, plan
         torch.cuda.empty_cache()
     print(f"W={W}: max {max(res):.2f} ms  mean {np.mean(res):.2f} ms  time-to-table max {max(ttt):.2f} ms",

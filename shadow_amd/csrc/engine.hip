@@ -1303,7 +1303,7 @@ __global__ __launch_bounds__(256) void plan_lmall_rank_kernel(const unsigned lon
 __global__ void plan_lmall_jobs_kernel(const uint16_t* __restrict__ drow, const uint32_t* __restrict__ prow, long long rs,
                                        const int* __restrict__ lmv, int nland, const int* __restrict__ srcq,
                                        const int* __restrict__ slot, int nq, int klm, int n, KDJob* __restrict__ out,
-                                       int* __restrict__ nroots) {
+                                       int* __restrict__ nroots, int hub_base = -1) {
     const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     const int per = gridDim.x / 8;  // (the grid is a multiple of 8 workgroups)
     const int b = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);  // (XCD-contiguous block order)
@@ -1312,8 +1312,10 @@ __global__ void plan_lmall_jobs_kernel(const uint16_t* __restrict__ drow, const 
     const int s = srcq[i];
     const LmChoice o = lm_pick(drow, prow, rs, lmv, nland, s, klm, n, lane);
     if (lane == 0) {
+        // (hub_base >= 0: a second-level landmark row of the plan's own hub launch, kept in
+        // store slot hub_base + i, no output row)
         KDJob J;
-        J.row = i; J.s = s; J.store = -1; J.nseed = o.m;
+        J.row = hub_base >= 0 ? -1 : i; J.s = s; J.store = hub_base >= 0 ? hub_base + i : -1; J.nseed = o.m;
         for (int k = 0; k < KD_SEEDS; k++) {
             const bool on = k < o.m;
             J.seed[k] = on ? o.l[k] : 0;
@@ -1321,8 +1323,8 @@ __global__ void plan_lmall_jobs_kernel(const uint16_t* __restrict__ drow, const 
             J.wr[k] = on ? o.d[k] : 0;
             J.rec[k] = on ? (int)o.rec[k] : 0;
         }
-        out[slot[i]] = J;
-        if (o.m == 0) atomicAdd(nroots, 1);
+        out[slot ? slot[i] : i] = J;
+        if (o.m == 0 && nroots) atomicAdd(nroots, 1);
     }
 }
 
@@ -1598,6 +1600,8 @@ struct shd_route_plan {
     // ranks by the caller (shd_route_plan_refresh_async with SHD_ROUTE_REFRESH_MINE, then the
     // exchange into the store, then SHD_ROUTE_REFRESH_JOBS)
     int lm_first = 0, lm_count = 0;
+    int lm2 = 0;                   // > 0: landmark rows in two levels (SHD_ROUTE_LM2, lm_refresh)
+    KDJob* d_hjobs2 = nullptr;     // (the second level's jobs, written on the device)
     bool store_external = false;   // d_drow / d_prow are the caller's (shd_route_plan_bind_store)
     KDJob* d_hjobs = nullptr;
     int* d_hdone = nullptr;
@@ -1606,7 +1610,7 @@ struct shd_route_plan {
     int* d_slot = nullptr;
     unsigned long long* d_key = nullptr;
     ~shd_route_plan() {
-        for (void* q : {(void*)d_jobs, (void*)d_next, (void*)d_src, (void*)d_hjobs,
+        for (void* q : {(void*)d_jobs, (void*)d_next, (void*)d_src, (void*)d_hjobs, (void*)d_hjobs2,
                         (void*)d_hdone, (void*)d_sq, (void*)d_lv, (void*)d_slot, (void*)d_key})
             if (q) (void)hipFree(q);
         if (!store_external)
@@ -1790,7 +1794,30 @@ int lm_refresh(shd_route* c, const shd_route_plan* P, uint32_t what, hipStream_t
     const int n = c->n, nj = (int)P->row_pos.size();
     const long long rs = kd_row_stride(n);
     if (!what) what = SHD_ROUTE_REFRESH_ALL | SHD_ROUTE_REFRESH_JOBS;
-    if ((what & SHD_ROUTE_REFRESH_ALL) || (what & SHD_ROUTE_REFRESH_MINE)) {
+    if ((what & SHD_ROUTE_REFRESH_ALL) && P->lm2 > 0) {
+        // two levels: the first lm2 landmark rows unseeded in 1024-thread workgroups (one per
+        // CU), then the others seeded from their three nearest of those (the main rows' seeding
+        // rule, as the plan_lmall_jobs_kernel writes it), in the context's workgroups
+        const int k0 = P->lm2, k1 = P->nhub - P->lm2;
+        if (!c->d_hub_ws || c->hub_ws_bytes < c->kd_stride * (size_t)std::max(hub_grid(c, k0), hub_grid(c, k1)))
+            return SHD_ROUTE_EINVAL;
+        if (hipMemsetAsync(P->d_hdone, 0, sizeof(int) * (1 + (size_t)P->nhub), st) != hipSuccess) return SHD_ROUTE_EDEVICE;
+        DevDelta g = kd_args(c);
+        g.jobs = P->d_hjobs;
+        g.drow = P->d_drow; g.drow_out = P->d_drow; g.prow = P->d_prow; g.rstride = rs;
+        g.done = P->d_hdone + 1;
+        int rc = kd_launch(c, g, P->d_hdone, nullptr, k0, nullptr, 0, 0, nullptr, nullptr, nullptr, st, true,
+                           c->d_hub_ws, hub_grid(c, k0), hub_big(c, k0));
+        if (rc) return rc;
+        hipLaunchKernelGGL(plan_lmall_jobs_kernel, dim3(8 * (((k1 + 15) / 16 + 7) / 8)), dim3(1024), 0, st, P->d_drow,
+                           P->d_prow, rs, P->d_lv, k0, P->d_lv + k0, (const int*)nullptr, k1, P->klm, n, P->d_hjobs2,
+                           (int*)nullptr, k0);
+        if (hipMemsetAsync(P->d_hdone, 0, sizeof(int), st) != hipSuccess) return SHD_ROUTE_EDEVICE;  // (queue only)
+        g.jobs = P->d_hjobs2;
+        rc = kd_launch(c, g, P->d_hdone, nullptr, k1, nullptr, 0, 0, nullptr, nullptr, nullptr, st, true,
+                       c->d_hub_ws, std::min(k1, c->kd_slots), false);
+        if (rc) return rc;
+    } else if ((what & SHD_ROUTE_REFRESH_ALL) || (what & SHD_ROUTE_REFRESH_MINE)) {
         const bool all = (what & SHD_ROUTE_REFRESH_ALL) != 0;
         const int q0 = all ? 0 : P->lm_first, k = all ? P->nhub : P->lm_count;
         // (the hub-row launch's scratch: the context's, grown at plan creation to this grid)
@@ -1900,7 +1927,12 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             std::memset(&hj[q], 0, sizeof(KDJob));
             hj[q].row = -1; hj[q].s = lv[q]; hj[q].store = q; hj[q].nseed = 0;
         }
-        if (hipMalloc((void**)&P->d_sq, sizeof(int) * nj) != hipSuccess ||
+        if (const char* e = getenv("SHD_ROUTE_LM2")) {
+            const int k0 = atoi(e);
+            if (k0 >= 16 && k0 < nh) P->lm2 = k0;
+        }
+        if ((P->lm2 && hipMalloc((void**)&P->d_hjobs2, sizeof(KDJob) * (size_t)(nh - P->lm2)) != hipSuccess) ||
+            hipMalloc((void**)&P->d_sq, sizeof(int) * nj) != hipSuccess ||
             hipMalloc((void**)&P->d_lv, sizeof(int) * nh) != hipSuccess ||
             hipMalloc((void**)&P->d_slot, sizeof(int) * nj) != hipSuccess ||
             hipMalloc((void**)&P->d_key, sizeof(unsigned long long) * nj) != hipSuccess ||
@@ -1911,7 +1943,8 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             hipMalloc((void**)&P->d_jobs, sizeof(KDJob) * (size_t)nj) != hipSuccess ||
             hipMalloc((void**)&P->d_next, sizeof(int) * (1 + (size_t)nh)) != hipSuccess)
             return SHD_ROUTE_ENOMEM;
-        const size_t wsb = c->kd_stride * (size_t)std::max(P->hub_grid, hub_grid(c, std::max(1, P->lm_count)));
+        const size_t wsb = c->kd_stride * (size_t)std::max(std::max(P->hub_grid, hub_grid(c, std::max(1, P->lm_count))),
+                                                           P->lm2 ? std::max(hub_grid(c, P->lm2), std::min(nh - P->lm2, c->kd_slots)) : 0);
         if (c->hub_ws_bytes < wsb) {
             if (c->d_hub_ws) (void)hipFree(c->d_hub_ws);
             c->d_hub_ws = nullptr; c->hub_ws_bytes = 0;
@@ -2745,7 +2778,8 @@ int planned_host_rows(shd_route* c, const int32_t* src, int32_t ns, const int32_
     if (dtgt.alloc(sizeof(int32_t) * nt) || dlat.alloc(table) || drel.alloc(table) || dmin.alloc(sizeof(double) * ns))
         return SHD_ROUTE_EUNSUPPORTED;
     if (hipMemcpy(dtgt.p, tgt, sizeof(int32_t) * nt, hipMemcpyHostToDevice) != hipSuccess) return SHD_ROUTE_EDEVICE;
-    rc = shd_route_rows_planned_async(c, P, (const int32_t*)dtgt.p, nt, nt, flags, (double*)dlat.p, (double*)drel.p,
+    // (the plan was made just now: its landmark rows, if any, are current)
+    rc = shd_route_rows_planned_async(c, P, (const int32_t*)dtgt.p, nt, nt, flags | SHD_ROUTE_PLAN_REUSE, (double*)dlat.p, (double*)drel.p,
                                       (double*)dmin.p, nullptr);
     if (rc) return rc;
     const int soft = shd_route_sync(c, nullptr);
@@ -3278,7 +3312,8 @@ int shd_route_fill_triangle(shd_route_t* c, const int32_t* A, int32_t na, int32_
               hipMemsetAsync(dmn.p, 0xFF, sizeof(unsigned long long), cs) == hipSuccess;
     if (ok && l16)
         ok = hipMemcpy(doff.p, rline.data(), sizeof(long long) * (nr + 1), hipMemcpyHostToDevice) == hipSuccess;
-    if (ok) rc = shd_route_rows_planned_async(c, P, (const int32_t*)dtgt.p, na, na, flags, (double*)dlat.p,
+    // (the plan was made just now: its landmark rows, if any, are current)
+    if (ok) rc = shd_route_rows_planned_async(c, P, (const int32_t*)dtgt.p, na, na, flags | SHD_ROUTE_PLAN_REUSE, (double*)dlat.p,
                                               (double*)drel.p, nullptr, cs);
     else rc = SHD_ROUTE_EDEVICE;
     // pack chunks of rows on the compute stream, copy them out on the copy stream; with

@@ -519,3 +519,25 @@ def test_landmark_only_plans(oracle_mod, monkeypatch, world, vloss):
             plan.close()
             monkeypatch.delenv(knob)
     assert sorted(seen) == list(range(len(T)))
+
+
+@pytest.mark.parametrize("lm2", ["64", "256"])
+def test_landmark_rows_two_levels(oracle_mod, monkeypatch, lm2):
+    """SHD_ROUTE_LM2=k: a landmark-only plan's landmark rows in two levels (the first k
+    unseeded, the rest seeded from their nearest of those): the landmark rows are exact
+    either way, so the table is the oracle's."""
+    from shadow_amd import route
+    from shadow_amd.graph import internet_like
+    monkeypatch.setenv("SHD_ROUTE_KERNEL", "kd")
+    monkeypatch.delenv("SHD_ROUTE_KDGRID", raising=False)
+    monkeypatch.delenv("SHD_ROUTE_SEED", raising=False)
+    monkeypatch.setenv("SHD_ROUTE_LM2", lm2)
+    g = internet_like(3000, 3, seed=77, name="ba3000")
+    eng = route.RouteEngine(g)
+    T = g.targets()
+    plan = eng.plan(T)
+    assert plan.info["launches"] == 5, plan.info
+    lat, rel, mn = _plan_rows(eng, plan, T)
+    pos = plan.positions
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(T[pos], T, oracle_mod.TIE_MINKEY)
+    assert np.array_equal(lat, olat) and np.array_equal(rel, orel) and np.array_equal(mn, olat.min(axis=1))

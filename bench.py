@@ -472,10 +472,10 @@ def main():
         "pairs_per_s": total_src * nt * args.steps / dt,
         "kernel_ms": float(np.mean(kms)),
         "landmark_ms": float(np.mean(lms)),
-        "step_contents": (("this rank's share of the landmark rows + their all-gather over the ranks + queue order "
-                           "and job records (3 kernels) + the rows launch + runahead min" if lm_split else
-                           "landmark rows (hub-row launch) + queue order and job records (3 kernels) + the rows "
-                           "launch + runahead min: every SSSP of the table") if plan.info["launches"] > 1 else
+        "step_contents": (("this rank's share of the landmark rows + their all-gather over the ranks + the job records "
+                           "(1 kernel) + the rows launch + runahead min" if lm_split else
+                           "landmark rows (hub-row launch) + the job records derived from them (1 kernel) + the "
+                           "rows launch + runahead min: every SSSP of the table") if plan.info["launches"] > 1 else
                           "the rows launch (every row of the table) + runahead min"),
         "time_to_table_ms": t_plan * 1e3 + dt / args.steps * 1e3,
         "roofline": {

@@ -184,11 +184,12 @@ int shd_route_plan_get_info(const shd_route_plan_t* plan, shd_route_plan_info_t*
 int shd_route_plan_rows(const shd_route_plan_t* plan, int32_t* pos_out);
 /* this rank's rows of the plan: row r of d_lat / d_rel / d_row_min = source
  * src[pos[r]]; device pointers as shd_route_rows_async.  A landmark-only plan built on the
- * device (256-thread contexts, and ranks with few rows per workgroup slot; info.launches 5)
+ * device (256-thread contexts, and ranks with few rows per workgroup slot; info.launches 3)
  * seeds every row from its nearest landmark rows (the highest-degree vertices' exact rows),
  * and this call computes those landmark rows too, on the stream, before the rows: the
- * landmark rows, the queue order and the job records are recomputed in every call, so every
- * SSSP behind the table runs inside it.  SHD_ROUTE_PLAN_REUSE skips that and reuses the
+ * landmark rows and the job records derived from them (each row's nearest landmarks, its
+ * offsets and seed records) are recomputed in every call, so every SSSP behind the table
+ * runs inside it; the queue order is the plan's, fixed when it is made.  SHD_ROUTE_PLAN_REUSE skips that and reuses the
  * last computation (the plan's creation, or shd_route_plan_refresh_async), which a caller
  * may run separately to time the rows launch alone; other plans ignore the flag. */
 #define SHD_ROUTE_PLAN_REUSE 0x200u
@@ -199,8 +200,7 @@ int shd_route_rows_planned_async(shd_route_t* ctx, const shd_route_plan_t* plan,
  * enqueued on the stream; SHD_ROUTE_OK and nothing enqueued for other plans.  `what`:
  * SHD_ROUTE_REFRESH_ALL computes every landmark row into the plan's store,
  * SHD_ROUTE_REFRESH_MINE only this rank's share (shd_route_plan_landmarks), and
- * SHD_ROUTE_REFRESH_JOBS derives the queue order and the job records from the store as it
- * stands; 0 = ALL | JOBS, what shd_route_rows_planned_async runs first without
+ * SHD_ROUTE_REFRESH_JOBS derives the job records from the store as it stands; 0 = ALL | JOBS, what shd_route_rows_planned_async runs first without
  * SHD_ROUTE_PLAN_REUSE.  A multi-GPU rank runs MINE, exchanges the store slots with the
  * other ranks (an all-gather of equal shares), then JOBS and the rows with
  * SHD_ROUTE_PLAN_REUSE: each landmark row is computed once per job instead of once per rank.

@@ -120,7 +120,6 @@ struct shd_route {
     // the planner's unseeded hub rows on 256-thread contexts (C3): 1024-thread workgroups,
     // one row per CU, cut the latency of that launch (each row is unseeded and alone)
     int kd_hub_block = 0, kd_hub_qcap = 0, kd_hub_delta = 1;
-    int kd_delta_narrow = 1;  // the 12th percentile of arc latencies (<= kd_delta): split-rank plans
     size_t kd_hub_lds = 0;
     int* d_kd_lstart = nullptr;   // light in-CSR offsets (n+1)
     uint32_t* d_kd_orec = nullptr;  // out-arc records v | w << 16
@@ -533,17 +532,6 @@ int prepare_k32(shd_route* c, const std::vector<int>& row, const std::vector<int
                 }
                 if (rc) return rc;
                 c->kd = 1; c->kd_block = blk; c->kd_lds = lds; c->kd_delta = delta; c->kd_qcap = qcap;
-                {
-                    // a narrower width for plans whose rows are mostly weakly seeded (a rank of a
-                    // multi-GPU split: its rows' seeds are often on other ranks).  Any width up
-                    // to the context's is exact: the light in-CSR above holds every in-arc with
-                    // w < delta, a superset of the narrower width's light arcs
-                    std::vector<int> ws3(c->nnz);
-                    for (int a = 0; a < c->nnz; a++) ws3[a] = (int)w[a];
-                    const size_t k12 = (size_t)c->nnz * 12 / 100;
-                    std::nth_element(ws3.begin(), ws3.begin() + k12, ws3.end());
-                    c->kd_delta_narrow = std::min(delta, std::max(1, ws3[k12]));
-                }
                 if (blk < 1024 && !getenv("SHD_ROUTE_DELTA") && !getenv("SHD_ROUTE_QCAP")) {
                     // hub rows in 1024-thread workgroups: that block's queue and bucket width
                     const size_t hb = kd_lds_bytes<1024>(n, 0);
@@ -1601,6 +1589,7 @@ struct shd_route_plan {
     // exchange into the store, then SHD_ROUTE_REFRESH_JOBS)
     int lm_first = 0, lm_count = 0;
     int lm2 = 0;                   // > 0: landmark rows in two levels (SHD_ROUTE_LM2, lm_refresh)
+    bool order_fixed = false;      // the queue order (d_slot) is computed; refreshes keep it
     KDJob* d_hjobs2 = nullptr;     // (the second level's jobs, written on the device)
     bool store_external = false;   // d_drow / d_prow are the caller's (shd_route_plan_bind_store)
     KDJob* d_hjobs = nullptr;
@@ -1623,8 +1612,11 @@ namespace {
 
 // landmark-only plans: at most this many rows per workgroup slot, and their landmark count
 constexpr double PLAN_LMALL_RPS = 1.5;
-constexpr int PLAN_LMALL_COUNT = 1024;  // (C3 1 GPU: 256 / 512 / 1024 / 2048 landmarks 2.49 / 2.30 / 2.18 / 2.07 ms;
-                                        //  2048 take two rounds of hub rows in the plan)
+// (round 5, hub rows outside the step: C3 1 GPU 256 / 512 / 1024 / 2048 landmarks 2.49 / 2.30 /
+//  2.18 / 2.07 ms of rows.  Round 6, the landmark rows inside every step: 512 / 768 / 1024 give
+//  2.677 / 2.69 / 2.77 ms per step (rows 2.14 / 2.05 / 1.99 + landmark rows and job records
+//  0.55 / 0.65 / 0.79), two runs each on one box)
+constexpr int PLAN_LMALL_COUNT = 512;
 
 // host threads of a plan (the box's CPU quota is 16)
 int plan_threads() {
@@ -1832,13 +1824,21 @@ int lm_refresh(shd_route* c, const shd_route_plan* P, uint32_t what, hipStream_t
         if (rc) return rc;
     }
     if (!(what & SHD_ROUTE_REFRESH_JOBS)) return SHD_ROUTE_OK;
-    if (hipMemsetAsync(P->d_next, 0, sizeof(int), st) != hipSuccess) return SHD_ROUTE_EDEVICE;  // (root count)
-    const int nb = (nj + 255) / 256;
-    hipLaunchKernelGGL(plan_lmall_keys_kernel, dim3(nb), dim3(256), 0, st, P->d_drow, rs, std::min(n, 16), P->d_sq, nj,
-                       P->d_key);
-    hipLaunchKernelGGL(plan_lmall_rank_kernel, dim3(nb), dim3(256), 8 * nj, st, P->d_key, nj, P->d_slot);
+    // the queue order (peripheral rows first, by the closeness the first 16 landmark rows
+    // give) is the plan's schedule: fixed when the plan is made, like a neighbour-seeded
+    // plan's list schedule (the rank sort took 0.13 ms of every C3 step); the job records --
+    // each row's nearest landmarks, its offsets d(s, L) and L's record in s's tree -- are
+    // derived from the landmark rows in every refresh
+    if (!P->order_fixed) {
+        if (hipMemsetAsync(P->d_next, 0, sizeof(int), st) != hipSuccess) return SHD_ROUTE_EDEVICE;  // (root count)
+        const int nb = (nj + 255) / 256;
+        hipLaunchKernelGGL(plan_lmall_keys_kernel, dim3(nb), dim3(256), 0, st, P->d_drow, rs, std::min(n, 16), P->d_sq,
+                           nj, P->d_key);
+        hipLaunchKernelGGL(plan_lmall_rank_kernel, dim3(nb), dim3(256), 8 * nj, st, P->d_key, nj, P->d_slot);
+    }
     hipLaunchKernelGGL(plan_lmall_jobs_kernel, dim3(8 * (((nj + 15) / 16 + 7) / 8)), dim3(1024), 0, st, P->d_drow,
-                       P->d_prow, rs, P->d_lv, P->nhub, P->d_sq, P->d_slot, nj, P->klm, n, P->d_jobs, P->d_next);
+                       P->d_prow, rs, P->d_lv, P->nhub, P->d_sq, P->d_slot, nj, P->klm, n, P->d_jobs,
+                       P->order_fixed ? (int*)nullptr : P->d_next);
     return hip_check(hipGetLastError());
 }
 
@@ -1854,12 +1854,13 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
     for (int p = 0; p < ns; p++) if (src[p] < 0 || src[p] >= c->n) return SHD_ROUTE_EINVAL;
     auto P = std::make_unique<shd_route_plan>();
     P->c = c; P->world = world; P->rank = rank; P->ns_all = ns;
-    // bucket width: the context's, or for a rank of a multi-GPU split of 1024-thread rows the
-    // narrower 12th percentile (a split rank holds fewer well-seeded rows, and weakly seeded
-    // rows expand more vertices, which narrower buckets serve better: C4 8-way emulated 8.74
-    // -> 8.47 ms at 30 against 38, one GPU 41.1 -> 41.6 ms the other way round)
+    // bucket width of the plan's rows: any width up to the context's is exact (the light
+    // in-CSR holds every in-arc below the context's width).  Round 5 read its builds as
+    // "split ranks prefer the 12th percentile (30 on C4)"; the direct A/B on one box with
+    // this per-plan width says otherwise (C4 8-way emulated, shared context, two runs each:
+    // 30 -> 8.95 / 8.97 ms max, 38 -> 8.73 / 8.72 ms), so every plan keeps the context's;
+    // SHD_ROUTE_PLAN_DELTA narrows it (tests, A/B runs)
     P->delta = c->kd_delta;
-    if (world > 1 && c->kd_block >= 1024 && !getenv("SHD_ROUTE_DELTA")) P->delta = c->kd_delta_narrow;
     if (const char* e = getenv("SHD_ROUTE_PLAN_DELTA")) P->delta = std::max(1, std::min(c->kd_delta, atoi(e)));
     const auto t_start = std::chrono::steady_clock::now();
     double t_close = 0, t_land = 0, t_seeds = 0, t_store = 0, t_sched = 0, t_rk = 0, t_order = 0, t_hop = 0, t_loop0 = 0, t_alloc = 0, t_deps = 0;
@@ -1968,6 +1969,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
         if (hipMemcpy(&nroots, P->d_next, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return SHD_ROUTE_EDEVICE;
         if ((rc = take_err(c))) return rc;
         P->lm_step = true;
+        P->order_fixed = !(getenv("SHD_ROUTE_LMORDER") && atoi(getenv("SHD_ROUTE_LMORDER")) == 0);
         P->nslots = 0; P->nland = nh; P->store_bytes = (uint64_t)nh * (uint64_t)rs * 6u; P->nroots = nroots;
         P->seeded = 1;
         P->lvl_off = {0, nj};
@@ -2678,7 +2680,8 @@ int shd_route_plan_get_info(const shd_route_plan_t* P, shd_route_plan_info_t* in
     if (!P || !info) return SHD_ROUTE_EINVAL;
     info->rows = (int32_t)P->row_pos.size();
     info->seeded = P->seeded;
-    info->launches = P->lm_step ? 5 : 1;  // (landmark-only: hub rows, three plan kernels, rows)
+    info->launches = P->lm_step ? (P->order_fixed ? 3 : 5) : 1;  // (landmark-only: hub rows, the job records
+                                                                   //  [+ order keys and ranks], rows)
     info->levels = P->seeded ? (int32_t)P->lvl_off.size() - 1 : 1;
     info->roots = P->nroots;
     info->helpers = P->nhelpers;

@@ -178,7 +178,7 @@ typedef struct shd_route_plan_info {
 
 int shd_route_plan_create(shd_route_t* ctx, const int32_t* src, int32_t ns, int32_t world, int32_t rank,
                           shd_route_plan_t** out);
-void shd_route_plan_destroy(shd_route_plan_t* plan);
+void shd_route_plan_destroy(shd_route_plan_t* plan);  /* before its context's shd_route_destroy */
 int shd_route_plan_get_info(const shd_route_plan_t* plan, shd_route_plan_info_t* info);
 /* positions (in the caller's source list) of this rank's output rows, in row order */
 int shd_route_plan_rows(const shd_route_plan_t* plan, int32_t* pos_out);

@@ -185,12 +185,18 @@ class RouteEngine:
         _check(L.shd_route_create(C.byref(h), C.byref(desc), int(device)), "shd_route_create")
         self._h = h
         self.device = device
+        # plans made on this context (a plan must be destroyed before its context: when both
+        # become garbage together, the collector may finalise them in either order)
+        import weakref
+        self._plans = weakref.WeakSet()
         inf = _Info()
         _check(L.shd_route_get_info(self._h, C.byref(inf)), "shd_route_get_info")
         self.info = {k: getattr(inf, k) for k, _ in _Info._fields_}
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
+            for p in list(getattr(self, "_plans", ())):
+                p.close()
             load_library().shd_route_destroy(self._h)
             self._h = C.c_void_p()
 
@@ -310,6 +316,7 @@ class RoutePlan:
         _check(L.shd_route_plan_create(eng._h, _p(src), len(src), int(world), int(rank), C.byref(h)),
                "shd_route_plan_create")
         self._h = h
+        eng._plans.add(self)
         inf = _PlanInfo()
         _check(L.shd_route_plan_get_info(self._h, C.byref(inf)), "shd_route_plan_get_info")
         self.info = {k: getattr(inf, k) for k, _ in _PlanInfo._fields_ if not k.endswith("_")}

@@ -270,13 +270,22 @@ def test_kfh_walks_and_deep_paths(route, oracle_mod, monkeypatch, lossy):
     olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(s_, tgt, oracle_mod.TIE_MINKEY)
     assert np.array_equal(lat_, olat)
     np.testing.assert_allclose(rel_, orel, rtol=REL_TOL, atol=0)
-    # the walks and the level passes agree bit for bit (vertex factors included): the same
-    # rows from the LDS kernel, which has only level passes
+    # a walked row folds from (1.0 * f_s) * f_t, the reference's order: bit-exact against the
+    # oracle; a row that fell back to the level passes multiplies f_t last, as the LDS kernel
+    # (level passes only) does: bit-exact against it.  Every row is one of the two; with 5% lossy
+    # arcs most rows walk, with every arc lossy every row falls back
     monkeypatch.delenv("SHD_ROUTE_KFH")
     e2 = route.RouteEngine(g)
     assert e2.info["lds_resident"] == 1
     l2, r2, _ = e2.rows(s_, tgt, dispatch=False)
-    assert np.array_equal(l2, lat_) and np.array_equal(r2, rel_)
+    assert np.array_equal(l2, lat_)
+    walked = np.array([np.array_equal(rel_[i], orel[i]) for i in range(len(s_))])
+    level = np.array([np.array_equal(rel_[i], r2[i]) for i in range(len(s_))])
+    assert np.all(walked | level)
+    if lossy == 1.0:
+        assert level.all()
+    else:
+        assert walked.mean() > 0.5, walked.mean()
 
 
 def test_kfh_20k_vertices(route, oracle_mod, monkeypatch):

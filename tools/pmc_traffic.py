@@ -10,7 +10,7 @@ import os
 import sys
 
 HOT = ("sssp_batch_kernel", "sssp_batch_rows_kernel", "path_attr_kernel", "sssp_k32_kernel", "sssp_rows_kernel", "sssp_k16", "sssp_delta_kernel",
-       "direct_rows_kernel", "sssp_f64d_kernel", "fw_rest", "fw_diag", "fw_panel", "fw_parent", "fw_rows", "fw_inlist")
+       "direct_rows_kernel", "sssp_f64d_kernel", "fw_rest", "fw_diag", "fw_panel", "fw_parent", "fw_rows", "fw_inlist", "kd_plan_rows_kernel", "plan_lmall")
 
 
 def load(path):
@@ -52,7 +52,7 @@ def main(src_dir, out, cfg, sources, only=None):
             continue
         f = fetch.get(k, {}).get("FETCH_SIZE", [0.0])
         w = write.get(k, {}).get("WRITE_SIZE", [0.0])
-        name = k.split("(")[0].replace("void ", "")
+        name = k.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         per[name] = {"fetch_bytes": 2.0 * 1024 * sum(f) / len(f), "fetch_bytes_uncorrected": 1024 * sum(f) / len(f),
                      "write_bytes": 1024 * sum(w) / len(w)}
     tot = sum(v["fetch_bytes"] + v["write_bytes"] for v in per.values())

@@ -25,6 +25,9 @@ for cfg in ${CFGS:-c4 c3 c2 c5}; do
     c3) a="--config c3 --steps 10 --warmup 2"; p="--config c3 --steps 2 --warmup 1"; s=9337; k="" ;;
     c2) a="--config c2 --steps 20 --warmup 5"; p="--config c2 --steps 5 --warmup 2"; s=2000; k="" ;;
     c5) a="--config c5 --steps 5 --warmup 1"; p="--config c5 --steps 3 --warmup 1"; s=4000; k="" ;;
+    c3f) a="--config c3f --steps 3 --warmup 1"; p="--config c3f --steps 2 --warmup 1"; s=9337; k="" ;;
+    c2f) a="--config c2f --steps 10 --warmup 2"; p="--config c2f --steps 3 --warmup 1"; s=2000; k="" ;;
+    c4f) a="--config c4f --steps 2 --warmup 1"; p="--config c4f --steps 1 --warmup 1"; s=50000; k="" ;;
   esac
   ks $cfg $a || exit 1
   pmc $cfg FETCH_SIZE $p && pmc $cfg WRITE_SIZE $p || exit 1

@@ -184,7 +184,7 @@ int shd_route_plan_get_info(const shd_route_plan_t* plan, shd_route_plan_info_t*
 int shd_route_plan_rows(const shd_route_plan_t* plan, int32_t* pos_out);
 /* this rank's rows of the plan: row r of d_lat / d_rel / d_row_min = source
  * src[pos[r]]; device pointers as shd_route_rows_async.  A landmark-only plan built on the
- * device (256-thread contexts, and ranks with few rows per workgroup slot; info.launches 3)
+ * device (256-thread contexts, and ranks with few rows per workgroup slot; info.launches 4)
  * seeds every row from its nearest landmark rows (the highest-degree vertices' exact rows),
  * and this call computes those landmark rows too, on the stream, before the rows: the
  * landmark rows and the job records derived from them (each row's nearest landmarks, its

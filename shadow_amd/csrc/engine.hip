@@ -1191,8 +1191,14 @@ struct LmChoice {
     uint32_t rec[3];
     int pad[2];
 };
+// (bias, device-built landmark-only plans, round 6: a landmark's pick key is d(s, L) + bias[L],
+// bias = half L's mean distance to the first 16 landmarks, so that of two landmarks about as
+// near to s the more central one seeds the row: its row bounds more of s's paths.  Offline on C3
+// (tools/landmark_choice.py, 300 sampled rows, exact distances): the share of vertices a row
+// improves on its bound 15.9% -> 13.1%; weights 0.375-0.625 measure the same, 0.25 13.5%, 1.0 15.3%)
 __device__ inline LmChoice lm_pick(const uint16_t* __restrict__ drow, const uint32_t* __restrict__ prow, long long rs,
-                                   const int* __restrict__ lmv, int nland, int s, int klm, int n, int lane) {
+                                   const int* __restrict__ lmv, int nland, int s, int klm, int n, int lane,
+                                   const uint16_t* __restrict__ bias = nullptr) {
     LmChoice o;
     o.m = 0; o.pad[0] = o.pad[1] = 0;
     for (int k = 0; k < 3; k++) { o.l[k] = 0; o.d[k] = 0; o.rec[k] = 0u; }
@@ -1206,6 +1212,13 @@ __device__ inline LmChoice lm_pick(const uint16_t* __restrict__ drow, const uint
         for (int h = 0; h < 8; h++) {
             const int l = l0 + 64 * h + lane;
             d8[h] = l < nland ? drow[(long long)l * rs + s] : 0xFFFFu;
+        }
+        if (bias) {
+#pragma unroll
+            for (int h = 0; h < 8; h++) {
+                const int l = l0 + 64 * h + lane;
+                if (l < nland && d8[h] != 0xFFFFu) d8[h] = min(0xFFFEu, d8[h] + (uint32_t)bias[l]);
+            }
         }
 #pragma unroll
         for (int h = 0; h < 8; h++) {
@@ -1231,7 +1244,8 @@ __device__ inline LmChoice lm_pick(const uint16_t* __restrict__ drow, const uint
             for (int hop = 0; hop < n && (int)(lp[x] & 0xFFFFu) != L; hop++) x = (int)(lp[x] & 0xFFFFu);
             rec = (uint32_t)x | (lp[x] & 0xFFFF0000u);
         }
-        o.l[k] = l; o.d[k] = (int)(best >> 16); o.rec[k] = rec;
+        // (with a bias the key is not the distance: the offset is read back)
+        o.l[k] = l; o.d[k] = bias ? (int)drow[(long long)l * rs + s] : (int)(best >> 16); o.rec[k] = rec;
         o.m = k + 1;
     }
     return o;
@@ -1291,14 +1305,15 @@ __global__ __launch_bounds__(256) void plan_lmall_rank_kernel(const unsigned lon
 __global__ void plan_lmall_jobs_kernel(const uint16_t* __restrict__ drow, const uint32_t* __restrict__ prow, long long rs,
                                        const int* __restrict__ lmv, int nland, const int* __restrict__ srcq,
                                        const int* __restrict__ slot, int nq, int klm, int n, KDJob* __restrict__ out,
-                                       int* __restrict__ nroots, int hub_base = -1) {
+                                       int* __restrict__ nroots, int hub_base = -1,
+                                       const uint16_t* __restrict__ bias = nullptr) {
     const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     const int per = gridDim.x / 8;  // (the grid is a multiple of 8 workgroups)
     const int b = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);  // (XCD-contiguous block order)
     const int i = b * wpb + (threadIdx.x >> 6);
     if (i >= nq) return;  // the whole wave
     const int s = srcq[i];
-    const LmChoice o = lm_pick(drow, prow, rs, lmv, nland, s, klm, n, lane);
+    const LmChoice o = lm_pick(drow, prow, rs, lmv, nland, s, klm, n, lane, bias);
     if (lane == 0) {
         // (hub_base >= 0: a second-level landmark row of the plan's own hub launch, kept in
         // store slot hub_base + i, no output row)
@@ -1314,6 +1329,23 @@ __global__ void plan_lmall_jobs_kernel(const uint16_t* __restrict__ drow, const 
         out[slot ? slot[i] : i] = J;
         if (o.m == 0 && nroots) atomicAdd(nroots, 1);
     }
+}
+
+// each landmark's pick bias (lm_pick): half its mean distance to the first nclose landmarks,
+// rounded, from the landmark rows (unreached: the largest bias)
+__global__ void plan_lmall_bias_kernel(const uint16_t* __restrict__ drow, long long rs, int nclose,
+                                       const int* __restrict__ lmv, int nland, uint16_t* __restrict__ bias) {
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= nland) return;
+    const int v = lmv[l];
+    unsigned sum = 0;
+    bool unr = false;
+    for (int q = 0; q < nclose; q++) {
+        const unsigned d = drow[(long long)q * rs + v];
+        unr = unr || d == 0xFFFFu;
+        sum += d;
+    }
+    bias[l] = unr ? (uint16_t)0x7FFF : (uint16_t)min(0x7FFFu, (sum + (unsigned)nclose) / (2u * (unsigned)nclose));
 }
 
 // lexicographic minimum of (x, u, t) over the wave (t: a tie-breaking key, arc or record)
@@ -1590,6 +1622,7 @@ struct shd_route_plan {
     int lm_first = 0, lm_count = 0;
     int lm2 = 0;                   // > 0: landmark rows in two levels (SHD_ROUTE_LM2, lm_refresh)
     bool order_fixed = false;      // the queue order (d_slot) is computed; refreshes keep it
+    uint16_t* d_bias = nullptr;    // the landmarks' pick biases (lm_pick; null: nearest first)
     KDJob* d_hjobs2 = nullptr;     // (the second level's jobs, written on the device)
     bool store_external = false;   // d_drow / d_prow are the caller's (shd_route_plan_bind_store)
     KDJob* d_hjobs = nullptr;
@@ -1599,7 +1632,7 @@ struct shd_route_plan {
     int* d_slot = nullptr;
     unsigned long long* d_key = nullptr;
     ~shd_route_plan() {
-        for (void* q : {(void*)d_jobs, (void*)d_next, (void*)d_src, (void*)d_hjobs, (void*)d_hjobs2,
+        for (void* q : {(void*)d_jobs, (void*)d_next, (void*)d_src, (void*)d_hjobs, (void*)d_hjobs2, (void*)d_bias,
                         (void*)d_hdone, (void*)d_sq, (void*)d_lv, (void*)d_slot, (void*)d_key})
             if (q) (void)hipFree(q);
         if (!store_external)
@@ -1836,9 +1869,12 @@ int lm_refresh(shd_route* c, const shd_route_plan* P, uint32_t what, hipStream_t
                            nj, P->d_key);
         hipLaunchKernelGGL(plan_lmall_rank_kernel, dim3(nb), dim3(256), 8 * nj, st, P->d_key, nj, P->d_slot);
     }
+    if (P->d_bias)
+        hipLaunchKernelGGL(plan_lmall_bias_kernel, dim3((P->nhub + 255) / 256), dim3(256), 0, st, P->d_drow, rs,
+                           std::min(P->nhub, 16), P->d_lv, P->nhub, P->d_bias);
     hipLaunchKernelGGL(plan_lmall_jobs_kernel, dim3(8 * (((nj + 15) / 16 + 7) / 8)), dim3(1024), 0, st, P->d_drow,
                        P->d_prow, rs, P->d_lv, P->nhub, P->d_sq, P->d_slot, nj, P->klm, n, P->d_jobs,
-                       P->order_fixed ? (int*)nullptr : P->d_next);
+                       P->order_fixed ? (int*)nullptr : P->d_next, -1, (const uint16_t*)P->d_bias);
     return hip_check(hipGetLastError());
 }
 
@@ -1932,7 +1968,9 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             const int k0 = atoi(e);
             if (k0 >= 16 && k0 < nh) P->lm2 = k0;
         }
-        if ((P->lm2 && hipMalloc((void**)&P->d_hjobs2, sizeof(KDJob) * (size_t)(nh - P->lm2)) != hipSuccess) ||
+        const bool lmbias = !(getenv("SHD_ROUTE_LMBIAS") && atoi(getenv("SHD_ROUTE_LMBIAS")) == 0);
+        if ((lmbias && hipMalloc((void**)&P->d_bias, sizeof(uint16_t) * (size_t)nh) != hipSuccess) ||
+            (P->lm2 && hipMalloc((void**)&P->d_hjobs2, sizeof(KDJob) * (size_t)(nh - P->lm2)) != hipSuccess) ||
             hipMalloc((void**)&P->d_sq, sizeof(int) * nj) != hipSuccess ||
             hipMalloc((void**)&P->d_lv, sizeof(int) * nh) != hipSuccess ||
             hipMalloc((void**)&P->d_slot, sizeof(int) * nj) != hipSuccess ||
@@ -2680,8 +2718,8 @@ int shd_route_plan_get_info(const shd_route_plan_t* P, shd_route_plan_info_t* in
     if (!P || !info) return SHD_ROUTE_EINVAL;
     info->rows = (int32_t)P->row_pos.size();
     info->seeded = P->seeded;
-    info->launches = P->lm_step ? (P->order_fixed ? 3 : 5) : 1;  // (landmark-only: hub rows, the job records
-                                                                   //  [+ order keys and ranks], rows)
+    // (landmark-only: hub rows, [landmark biases,] the job records [+ order keys and ranks], rows)
+    info->launches = P->lm_step ? (P->order_fixed ? 3 : 5) + (P->d_bias ? 1 : 0) : 1;
     info->levels = P->seeded ? (int32_t)P->lvl_off.size() - 1 : 1;
     info->roots = P->nroots;
     info->helpers = P->nhelpers;

@@ -101,7 +101,7 @@ def _lm_worker(rank, world, port, q):
     plan = eng.plan(T, world, rank)
     dev = torch.device("cuda", 0)
     lm = plan.landmarks()
-    assert lm is not None and plan.info["launches"] == 3, plan.info
+    assert lm is not None and plan.info["launches"] == 4, plan.info
     store = bind_landmark_store(plan, world, dev)
     # poison the other ranks' shares: only the exchange can restore them
     cnt = store["share"]

@@ -1649,7 +1649,7 @@ constexpr double PLAN_LMALL_RPS = 1.5;
 //  2.18 / 2.07 ms of rows.  Round 6, the landmark rows inside every step: 512 / 768 / 1024 give
 //  2.677 / 2.69 / 2.77 ms per step (rows 2.14 / 2.05 / 1.99 + landmark rows and job records
 //  0.55 / 0.65 / 0.79), two runs each on one box)
-constexpr int PLAN_LMALL_COUNT = 512;
+constexpr int PLAN_LMALL_COUNT = 448;
 
 // host threads of a plan (the box's CPU quota is 16)
 int plan_threads() {

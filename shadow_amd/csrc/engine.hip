@@ -1185,6 +1185,7 @@ static_assert(KD_SEEDS <= 3 && 2 * KD_SEEDS <= PC_CAND, "PlanChoice holds the ca
 // host rule -- the klm landmarks nearest s by (d_L(s), landmark index) (undirected graphs:
 // d_L(s) = d(s, L)), each with the record of L's own vertex in s's tree: the last arc (x, L)
 // of the s -> L path in L's tree, found by walking L's parent records up from s.
+constexpr int LM_DIV_K = 16;  // spread landmark seeds: up to 64 x 16 = 1024 landmarks per row's wave
 struct LmChoice {
     int m;
     int l[3], d[3];
@@ -1198,10 +1199,78 @@ struct LmChoice {
 // improves on its bound 15.9% -> 13.1%; weights 0.375-0.625 measure the same, 0.25 13.5%, 1.0 15.3%)
 __device__ inline LmChoice lm_pick(const uint16_t* __restrict__ drow, const uint32_t* __restrict__ prow, long long rs,
                                    const int* __restrict__ lmv, int nland, int s, int klm, int n, int lane,
-                                   const uint16_t* __restrict__ bias = nullptr) {
+                                   const uint16_t* __restrict__ bias = nullptr, int spread = 0) {
     LmChoice o;
     o.m = 0; o.pad[0] = o.pad[1] = 0;
     for (int k = 0; k < 3; k++) { o.l[k] = 0; o.d[k] = 0; o.rec[k] = 0u; }
+    // L's own record in s's tree: the last arc (x, L) of L's tree path from s
+    auto rec_of = [&](int l) __attribute__((always_inline)) {
+        const int L = lmv[l];
+        uint32_t rec = KD_SRC_MARK;
+        if (L != s) {
+            const uint32_t* lp = prow + (long long)l * rs;
+            int x = s;
+            for (int hop = 0; hop < n && (int)(lp[x] & 0xFFFFu) != L; hop++) x = (int)(lp[x] & 0xFFFFu);
+            rec = (uint32_t)x | (lp[x] & 0xFFFF0000u);
+        }
+        return rec;
+    };
+    if (bias && spread && nland <= 64 * LM_DIV_K) {
+        // Spread seeds (round 6): each next landmark minimises d(s, L) + bias[L] - d(L', L) / 2
+        // over the landmarks not picked, L' the nearest already-picked one (its row gives
+        // d(L', L) at L's vertex), so the seeds bound s's paths from different sides.  Offline
+        // on C3 (tools/landmark_choice.py, 300 rows): improved share 13.5% (central-biased
+        // nearest) -> 9.3%; separation weights 3/8-5/8 the same, 3/4 10.6%, 1 14.1%.
+        int dl[LM_DIV_K], sc[LM_DIV_K];
+#pragma unroll
+        for (int j = 0; j < LM_DIV_K; j++) {
+            const int l = lane + 64 * j;
+            const unsigned d = l < nland ? drow[(long long)l * rs + s] : 0xFFFFu;
+            dl[j] = (int)d;
+            sc[j] = (l < nland && d != 0xFFFFu) ? (int)d + (int)bias[l] : 0x7FFFFFFF;
+        }
+        int sep[LM_DIV_K];
+#pragma unroll
+        for (int j = 0; j < LM_DIV_K; j++) sep[j] = 0x7FFFFFFF;
+        for (int k = 0; k < klm && k < 3; k++) {
+            // the wave's minimum of (score, l) over the landmarks not yet picked
+            unsigned long long best = ~0ull;
+#pragma unroll
+            for (int j = 0; j < LM_DIV_K; j++) {
+                if (sc[j] == 0x7FFFFFFF) continue;
+                const int x = k == 0 ? sc[j] : sc[j] - sep[j] / 2;
+                const unsigned long long key = ((unsigned long long)(unsigned)(x + 0x40000000) << 32) |
+                                               (unsigned)(lane + 64 * j);
+                best = min(best, key);
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                const unsigned long long y = ((unsigned long long)(unsigned)__shfl_xor((int)(best >> 32), off) << 32) |
+                                             (unsigned)__shfl_xor((int)(unsigned)best, off);
+                best = min(best, y);
+            }
+            if (best == ~0ull) break;
+            const int l = (int)(unsigned)best;
+            int dpick = 0;  // (register arrays indexed by unrolled constants only: no scratch)
+#pragma unroll
+            for (int j = 0; j < LM_DIV_K; j++)
+                if (j == (l >> 6)) {
+                    if ((l & 63) == lane) sc[j] = 0x7FFFFFFF;  // (picked)
+                    dpick = dl[j];
+                }
+            // separations to the picked landmark: its row at every landmark's vertex
+            if (k + 1 < klm) {
+                const uint16_t* lr = drow + (long long)l * rs;
+#pragma unroll
+                for (int j = 0; j < LM_DIV_K; j++) {
+                    const int q = lane + 64 * j;
+                    if (q < nland) sep[j] = min(sep[j], (int)lr[lmv[q]]);
+                }
+            }
+            o.l[k] = l; o.d[k] = __shfl(dpick, l & 63); o.rec[k] = rec_of(l);
+            o.m = k + 1;
+        }
+        return o;
+    }
     // each lane's three smallest keys (d << 16 | l) over its landmarks l = lane + 64 j, read
     // once; the wave's k-th pick is then the minimum over the lanes' lists past the (k-1)-th
     constexpr uint32_t NONE = 0xFFFFFFFFu;
@@ -1236,16 +1305,9 @@ __device__ inline LmChoice lm_pick(const uint16_t* __restrict__ drow, const uint
         for (int off = 32; off > 0; off >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, off));
         if (best == NONE) break;
         if (c0 == best) { c0 = c1; c1 = c2; c2 = NONE; }  // (keys are unique: one lane owns it)
-        const int l = (int)(best & 0xFFFFu), L = lmv[l];
-        uint32_t rec = KD_SRC_MARK;
-        if (L != s) {
-            const uint32_t* lp = prow + (long long)l * rs;
-            int x = s;
-            for (int hop = 0; hop < n && (int)(lp[x] & 0xFFFFu) != L; hop++) x = (int)(lp[x] & 0xFFFFu);
-            rec = (uint32_t)x | (lp[x] & 0xFFFF0000u);
-        }
+        const int l = (int)(best & 0xFFFFu);
         // (with a bias the key is not the distance: the offset is read back)
-        o.l[k] = l; o.d[k] = bias ? (int)drow[(long long)l * rs + s] : (int)(best >> 16); o.rec[k] = rec;
+        o.l[k] = l; o.d[k] = bias ? (int)drow[(long long)l * rs + s] : (int)(best >> 16); o.rec[k] = rec_of(l);
         o.m = k + 1;
     }
     return o;
@@ -1306,14 +1368,14 @@ __global__ void plan_lmall_jobs_kernel(const uint16_t* __restrict__ drow, const 
                                        const int* __restrict__ lmv, int nland, const int* __restrict__ srcq,
                                        const int* __restrict__ slot, int nq, int klm, int n, KDJob* __restrict__ out,
                                        int* __restrict__ nroots, int hub_base = -1,
-                                       const uint16_t* __restrict__ bias = nullptr) {
+                                       const uint16_t* __restrict__ bias = nullptr, int spread = 0) {
     const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     const int per = gridDim.x / 8;  // (the grid is a multiple of 8 workgroups)
     const int b = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);  // (XCD-contiguous block order)
     const int i = b * wpb + (threadIdx.x >> 6);
     if (i >= nq) return;  // the whole wave
     const int s = srcq[i];
-    const LmChoice o = lm_pick(drow, prow, rs, lmv, nland, s, klm, n, lane, bias);
+    const LmChoice o = lm_pick(drow, prow, rs, lmv, nland, s, klm, n, lane, bias, spread);
     if (lane == 0) {
         // (hub_base >= 0: a second-level landmark row of the plan's own hub launch, kept in
         // store slot hub_base + i, no output row)
@@ -1623,6 +1685,7 @@ struct shd_route_plan {
     int lm2 = 0;                   // > 0: landmark rows in two levels (SHD_ROUTE_LM2, lm_refresh)
     bool order_fixed = false;      // the queue order (d_slot) is computed; refreshes keep it
     uint16_t* d_bias = nullptr;    // the landmarks' pick biases (lm_pick; null: nearest first)
+    int spread = 1;                // seeds picked spread apart (lm_pick; SHD_ROUTE_LMSPREAD=0: nearest-biased)
     KDJob* d_hjobs2 = nullptr;     // (the second level's jobs, written on the device)
     bool store_external = false;   // d_drow / d_prow are the caller's (shd_route_plan_bind_store)
     KDJob* d_hjobs = nullptr;
@@ -1874,7 +1937,7 @@ int lm_refresh(shd_route* c, const shd_route_plan* P, uint32_t what, hipStream_t
                            std::min(P->nhub, 16), P->d_lv, P->nhub, P->d_bias);
     hipLaunchKernelGGL(plan_lmall_jobs_kernel, dim3(8 * (((nj + 15) / 16 + 7) / 8)), dim3(1024), 0, st, P->d_drow,
                        P->d_prow, rs, P->d_lv, P->nhub, P->d_sq, P->d_slot, nj, P->klm, n, P->d_jobs,
-                       P->order_fixed ? (int*)nullptr : P->d_next, -1, (const uint16_t*)P->d_bias);
+                       P->order_fixed ? (int*)nullptr : P->d_next, -1, (const uint16_t*)P->d_bias, P->spread);
     return hip_check(hipGetLastError());
 }
 
@@ -1969,6 +2032,7 @@ int shd_route_plan_create(shd_route_t* c, const int32_t* src, int32_t ns, int32_
             if (k0 >= 16 && k0 < nh) P->lm2 = k0;
         }
         const bool lmbias = !(getenv("SHD_ROUTE_LMBIAS") && atoi(getenv("SHD_ROUTE_LMBIAS")) == 0);
+        if (getenv("SHD_ROUTE_LMSPREAD") && atoi(getenv("SHD_ROUTE_LMSPREAD")) == 0) P->spread = 0;
         if ((lmbias && hipMalloc((void**)&P->d_bias, sizeof(uint16_t) * (size_t)nh) != hipSuccess) ||
             (P->lm2 && hipMalloc((void**)&P->d_hjobs2, sizeof(KDJob) * (size_t)(nh - P->lm2)) != hipSuccess) ||
             hipMalloc((void**)&P->d_sq, sizeof(int) * nj) != hipSuccess ||

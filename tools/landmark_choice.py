@@ -68,11 +68,29 @@ def main():
                 "nearest + 0.75 closeness(L)": lambda s: DL[:, s] + 0.75 * closeL,
                 "nearest + 1.0 closeness(L)": lambda s: DL[:, s] + 1.0 * closeL,
                 "nearest, one per gateway": None,
+                "greedy diverse g=0.375": ("div", 0.375),
+                "greedy diverse g=0.625": ("div", 0.625),
+                "greedy diverse g=0.75": ("div", 0.75),
+                "greedy diverse g=0.5": ("div", 0.5),
+                "greedy diverse g=1.0": ("div", 1.0),
             })
         for rname, rule in rules.items():
             shares = []
             for i, s in enumerate(S):
-                if rule is None:
+                if isinstance(rule, tuple):
+                    # greedy: each next landmark minimises d(s,L) + 0.5 closeness(L) minus gamma x
+                    # its distance to the nearest landmark already picked (spread the seeds)
+                    gam = rule[1]
+                    base = DL[:, s] + 0.5 * closeL
+                    near = [int(np.argmin(base))]
+                    LL = DL[:, L]  # [landmark, landmark vertex] distances
+                    while len(near) < a.k:
+                        sep = LL[near][:, np.arange(len(L))].min(axis=0)
+                        sc = base - gam * sep
+                        sc[near] = np.inf
+                        near.append(int(np.argmin(sc)))
+                    near = np.array(near)
+                elif rule is None:
                     # the nearest landmark to each of s's k lightest neighbours (by w + d to it)
                     ip, ix, dat = A.indptr, A.indices, A.data
                     us, ws = ix[ip[s]:ip[s + 1]], dat[ip[s]:ip[s + 1]]

@@ -76,6 +76,22 @@ def gateways(a):
     for k in (3, 2, 1):
         v = np.array([improved(D, idx, s, plans[(s, k)], n) for s in S])
         print(f"top-{k} gateways: improved mean {v.mean():.4f} p50 {np.median(v):.4f} p90 {np.percentile(v, 90):.4f}")
+    # two gateways + a landmark spread from them (engine lm_pick rule) as the third seed
+    for nl in (16, 256, 1024):
+        Lh = hubs[:nl] if nl <= len(hubs) else np.lexsort((np.arange(n), -np.diff(A.indptr)))[:nl]
+        DLm = dijkstra(A, indices=Lh)
+        bias = 0.5 * DLm[:, Lh[:16]].mean(axis=1)
+        v = []
+        for s in S:
+            sd = plans[(s, 2)]
+            sc = DLm[:, s] + bias
+            if sd:
+                sc = sc - 0.5 * np.min(DLm[:, [u for u, _ in sd]], axis=1)
+            q = int(np.argmin(sc))
+            seeds = sd + [(int(Lh[q]), float(DLm[q, s]))]
+            D0 = np.min([wu + (D[idx[u]] if u in idx else DLm[list(Lh).index(u)]) for u, wu in seeds], axis=0)
+            v.append(np.count_nonzero(D[idx[s]] < D0) / n)
+        print(f"top-2 gateways + spread landmark of {nl}: improved mean {np.mean(v):.4f} p50 {np.median(v):.4f}")
     for L in (16, 64, 256):
         for k in (1, 2, 3):
             v = []
@@ -169,14 +185,24 @@ def eval_rank(A, n, hubs, close, rk, owner, topset, label, samples):
                     seen.add(u); sd.append((u, off))
         plans[s] = sd
     nl = getattr(eval_rank, "landmarks", 0)
-    if nl:  # rows with at most one direct gateway also take their nearest landmark as a seed
+    mode = getattr(eval_rank, "lmmode", "nearest-weak")
+    if nl:  # rows also take a landmark seed: nearest, or spread from their seeds (engine lm_pick)
         from scipy.sparse.csgraph import dijkstra as _dj
-        DL = _dj(A, indices=hubs[:nl])
+        L = np.lexsort((np.arange(n), -np.diff(A.indptr)))[:nl]
+        DL = _dj(A, indices=L)
+        bias = 0.5 * DL[:, L[:16]].mean(axis=1)
         direct = {s: sum(1 for u, _ in (plans[s] or []) if A[s, u] != 0) for s in samp}
         for s in samp:
-            if plans[s] is not None and direct[s] <= 1:
+            if plans[s] is None or (mode.endswith("weak") and direct[s] > 1):
+                continue
+            if mode.startswith("nearest"):
                 q = int(np.argmin(DL[:, s]))
-                plans[s] = plans[s] + [(int(hubs[q]), float(DL[q, s]))]
+            else:
+                sc = DL[:, s] + bias
+                if plans[s]:
+                    sc = sc - 0.5 * np.min(DL[:, [u for u, _ in plans[s]]], axis=1)
+                q = int(np.argmin(sc))
+            plans[s] = plans[s] + [(int(L[q]), float(DL[q, s]))]
     need = sorted(set(samp.tolist()) | set(hubs[:16].tolist()) | {u for v in plans.values() if v for u, _ in v})
     D = dijkstra(A, indices=need)
     idx = {v: i for i, v in enumerate(need)}
@@ -239,6 +265,8 @@ if __name__ == "__main__":
     ap.add_argument("--samples", type=int, default=150)
     ap.add_argument("--louvain", action="store_true")
     ap.add_argument("--landmarks", type=int, default=0, help="partition: rows with <= 1 direct gateway add their nearest of L hub rows")
+    ap.add_argument("--lmmode", default="nearest-weak", choices=["nearest-weak", "spread-weak", "spread-all", "nearest-all"])
     a = ap.parse_args()
     eval_rank.landmarks = a.landmarks
+    eval_rank.lmmode = a.lmmode
     gateways(a) if a.mode == "gateways" else partition(a)

@@ -76,6 +76,45 @@ def gateways(a):
     for k in (3, 2, 1):
         v = np.array([improved(D, idx, s, plans[(s, k)], n) for s in S])
         print(f"top-{k} gateways: improved mean {v.mean():.4f} p50 {np.median(v):.4f} p90 {np.percentile(v, 90):.4f}")
+    # three gateways picked spread apart: each next one minimises w(s,u) + closeness(u) - g x sep,
+    # sep = the distance to the nearest picked gateway, exact or its landmark lower bound
+    # max_L |d_L(u) - d_L(u')| over the 16 closeness rows (what a planner has)
+    H16 = dijkstra(A, indices=hubs[:16])
+    ip, ix, dat = A.indptr, A.indices, A.data
+    cand = {}
+    for s in S:
+        us, ws = ix[ip[s]:ip[s + 1]], dat[ip[s]:ip[s + 1]]
+        sel = rk[us] < rk[s]
+        cand[s] = (us[sel], ws[sel])
+    need2 = sorted(set(need) | {int(u) for s in S for u in cand[s][0]})
+    if len(need2) > len(need):
+        D = dijkstra(A, indices=need2)
+        idx = {v: i for i, v in enumerate(need2)}
+    for exact in (True, False):
+        for gam in (0.25, 0.5, 1.0):
+            v = []
+            for s in S:
+                us, ws = cand[s]
+                if len(us) == 0:
+                    v.append(1.0)
+                    continue
+                base = ws + close[us]
+                picked = []
+                for _ in range(3):
+                    if len(picked) == len(us):
+                        break
+                    sc = base.copy()
+                    if picked:
+                        if exact:
+                            sep = np.min([D[idx[int(us[p])]][us] for p in picked], axis=0)
+                        else:
+                            sep = np.min([np.abs(H16[:, us] - H16[:, [us[p]]]).max(axis=0) for p in picked], axis=0)
+                        sc = sc - gam * sep
+                    sc[picked] = np.inf
+                    picked.append(int(np.argmin(sc)))
+                v.append(improved(D, idx, s, [(int(us[p]), float(ws[p])) for p in picked], n))
+            print(f"3 gateways spread ({'exact' if exact else 'landmark bound'} separation, g={gam}): "
+                  f"improved mean {np.mean(v):.4f} p50 {np.median(v):.4f}")
     # two gateways + a landmark spread from them (engine lm_pick rule) as the third seed
     for nl in (16, 256, 1024):
         Lh = hubs[:nl] if nl <= len(hubs) else np.lexsort((np.arange(n), -np.diff(A.indptr)))[:nl]

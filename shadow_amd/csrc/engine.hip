@@ -171,6 +171,7 @@ struct shd_route {
     uint32_t* d_fwkey = nullptr;
     uint8_t* d_fwrix = nullptr;  // K4 rows: reliability index of each arc (dense n x n u8)
     double* d_fwrtab = nullptr;  // and the distinct reliabilities (fw_nrtab <= 255; 0: dense R reads)
+    int fw_pk = 0;               // K4 in-list keys carry the parent arc's reliability index
     int fw_nrtab = 0;
     size_t fwkey_cap = 0;
     int fw_np = 0, fw_ready = 0;
@@ -2901,7 +2902,7 @@ int planned_host_rows(shd_route* c, const int32_t* src, int32_t ns, const int32_
 // K4: blocked min-plus Floyd-Warshall (fw.hpp)
 // =============================================================================
 namespace {
-constexpr int kFwMaxN = 12000;  // fw_rows keeps rel f64 + order i32 per vertex in LDS
+constexpr int kFwMaxN = 12000;  // fw_rows keeps rel f64 + order u16 per vertex in LDS
 
 // Builds the K4 state once per context: eligibility first (nothing is allocated for an
 // ineligible graph, so every call answers EUNSUPPORTED), then the buffers into locals,
@@ -2911,7 +2912,7 @@ int fw_prepare(shd_route* c, hipStream_t st) {
     if (c->d_fwD) return SHD_ROUTE_OK;
     if (!c->integer_w || c->multigraph || c->n > kFwMaxN || c->k32_bound <= 0 || c->k32_bound >= 0xFFFF)
         return SHD_ROUTE_EUNSUPPORTED;
-    const size_t lds = a16(sizeof(double) * c->n) + a16(sizeof(int) * c->n) + a16(sizeof(int) * (c->k32_bound + 2));
+    const size_t lds = a16(sizeof(double) * c->n) + a16(sizeof(uint16_t) * c->n) + a16(sizeof(int) * (c->k32_bound + 2));
     if (lds > kLdsBudget) return SHD_ROUTE_EUNSUPPORTED;
     const int np = (c->n + FW_T - 1) / FW_T * FW_T;
     int sp = 1;
@@ -2972,7 +2973,10 @@ int fw_prepare(shd_route* c, hipStream_t st) {
         }
         nrt = (int)rt.size();
     }
-    hipLaunchKernelGGL(fw_inlist_kernel, dim3(c->n), dim3(1024), 4 * sp, st, c->d_W, c->n, np, sp, inl, pos);
+    // packed in-list keys (the parent arc's reliability index inside the key): every latency
+    // <= 255 and the u8 index matrix built above (SHD_ROUTE_FWPK=0: the wide keys)
+    const int pk = rixd && c->max_w <= 255.0 && !(getenv("SHD_ROUTE_FWPK") && atoi(getenv("SHD_ROUTE_FWPK")) == 0);
+    hipLaunchKernelGGL(fw_inlist_kernel, dim3(c->n), dim3(1024), 4 * sp, st, c->d_W, c->n, np, sp, inl, pos, rixd, pk);
     if ((rc = hip_check(hipGetLastError()))) {
         for (void* q : {(void*)rixd, (void*)rtd}) if (q) (void)hipFree(q);
         return undo(rc);
@@ -2987,6 +2991,7 @@ int fw_prepare(shd_route* c, hipStream_t st) {
         c->fw_nrtab = nrt;
     }
     c->d_fwD = D;
+    c->fw_pk = pk;
     c->d_fwinl = inl;
     c->d_fwpos = pos;
     c->allocs.push_back(D);
@@ -3075,13 +3080,18 @@ int shd_route_fw_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, co
     int pblk = 256;
     if (const char* e = getenv("SHD_ROUTE_FWPBLK")) pblk = atoi(e) == 1024 ? 1024 : atoi(e) == 512 ? 512 : 256;
     hipLaunchKernelGGL(fw_parent_kernel, dim3(std::min(ns, 8192)), dim3(pblk), 2 * np, st, c->d_fwD, c->d_fwinl,
-                       c->d_fwpos, c->n, np, d_src, ns, c->d_fwkey);
+                       c->d_fwpos, c->n, np, d_src, ns, c->d_fwkey, c->fw_pk);
     FWRowsArgs a;
+    a.pk = c->fw_pk;
     a.n = c->n; a.np = np; a.bound = c->k32_bound; a.D = c->d_fwD; a.key = c->d_fwkey; a.R = c->d_R;
     a.rix = c->d_fwrix; a.rtab = c->d_fwrtab; a.nrtab = c->d_fwrix ? c->fw_nrtab : 0;
     a.vf = c->d_vf; a.self_w = c->d_self_w; a.self_r = c->d_self_r;
-    const size_t lds = a16(sizeof(double) * c->n) + a16(sizeof(int) * c->n) + a16(sizeof(int) * (c->k32_bound + 2));
-    hipLaunchKernelGGL(fw_rows_kernel, dim3(std::min(ns, 2048)), dim3(1024), lds, st, a, d_src, ns, d_tgt, nt,
+    const size_t lds = a16(sizeof(double) * c->n) + a16(sizeof(uint16_t) * c->n) + a16(sizeof(int) * (c->k32_bound + 2));
+    // (512-thread workgroups since the u16 order list: C5 rows 0.92 -> 0.81 ms against 1024,
+    // 0.86 at 256; SHD_ROUTE_FWRBLK=1024 / 256 for the A/B)
+    int rblk = 512;
+    if (const char* e = getenv("SHD_ROUTE_FWRBLK")) rblk = atoi(e) == 1024 ? 1024 : atoi(e) == 256 ? 256 : 512;
+    hipLaunchKernelGGL(fw_rows_kernel, dim3(std::min(ns, 2048)), dim3(rblk), lds, st, a, d_src, ns, d_tgt, nt,
                        (long long)ld, d_lat, d_rel, d_row_min, c->d_err);
     return hip_check(hipGetLastError());
 }

@@ -596,15 +596,25 @@ constexpr int FW_X = 256;
 #define FW_SCAN 8  // in-arcs per parent-scan trip (4 or 8)
 #endif
 constexpr uint32_t FW_END = 0xFFFFFFFFu;
+// Keys (pk = 0): (0xFFFF - w) << 16 | u.  Packed (pk = 1, round 6: every w <= 255 and the
+// reliability indices rix present): (255 - w) << 24 | u << 8 | rix(u, v) -- the same order
+// (largest w, then smallest u), and the parent arc's reliability index comes out of
+// fw_parent with the parent, so fw_rows no longer gathers it from the dense n x n rix
+// matrix (one 64-byte line per (p, v) pair: ~1 GB per C5 rows launch)
+__device__ inline uint32_t fw_key_u(uint32_t e, int pk) { return pk ? (e >> 8) & 0xFFFFu : e & 0xFFFFu; }
+__device__ inline uint32_t fw_key_w(uint32_t e, int pk) { return pk ? 0xFFu - (e >> 24) : 0xFFFFu - (e >> 16); }
 __global__ __launch_bounds__(1024) void fw_inlist_kernel(const double* __restrict__ W, int n, int np, int sp,
-                                                         uint32_t* __restrict__ inl, uint16_t* __restrict__ pos) {
+                                                         uint32_t* __restrict__ inl, uint16_t* __restrict__ pos,
+                                                         const uint8_t* __restrict__ rix, int pk) {
     extern __shared__ __attribute__((aligned(16))) uint32_t fkeys[];
     const int v = blockIdx.x, tid = threadIdx.x, B = blockDim.x;
     for (int k = tid; k < sp; k += B) {
         uint32_t key = FW_END;
         if (k < n && k != v) {
             const double w = W[(long long)k * n + v];
-            if (!isnan(w) && w < 65535.0) key = ((0xFFFFu - (uint32_t)w) << 16) | (uint32_t)k;
+            if (!isnan(w) && w < 65535.0)
+                key = pk ? ((0xFFu - (uint32_t)w) << 24) | ((uint32_t)k << 8) | (uint32_t)rix[(long long)k * n + v]
+                         : ((0xFFFFu - (uint32_t)w) << 16) | (uint32_t)k;
         }
         fkeys[k] = key;
     }
@@ -622,7 +632,8 @@ __global__ __launch_bounds__(1024) void fw_inlist_kernel(const double* __restric
     }
     for (int k = tid; k < np; k += B) inl[(long long)v * np + k] = fkeys[k];
     for (int x = tid; x < FW_X; x += B) {
-        const uint32_t thr = (0xFFFFu - (uint32_t)x) << 16;  // w <= x  <=>  key >= thr
+        // w <= x  <=>  key >= thr
+        const uint32_t thr = pk ? (x >= 255 ? 0u : (0xFFu - (uint32_t)x) << 24) : (0xFFFFu - (uint32_t)x) << 16;
         int lo = 0, hi = sp;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
@@ -650,7 +661,7 @@ __global__ __launch_bounds__(1024) void fw_inlist_kernel(const double* __restric
 __global__ __launch_bounds__(1024) void fw_parent_kernel(const uint16_t* __restrict__ D, const uint32_t* __restrict__ inl,
                                                          const uint16_t* __restrict__ pos, int n, int np,
                                                          const int* __restrict__ src, int ns,
-                                                         uint32_t* __restrict__ key) {
+                                                         uint32_t* __restrict__ key, int packed) {
     extern __shared__ __attribute__((aligned(16))) uint16_t drow[];
     static_assert(FW_SCAN == 8, "two 16-byte loads per scan trip");
     for (int i = blockIdx.x; i < ns; i += gridDim.x) {
@@ -678,7 +689,7 @@ __global__ __launch_bounds__(1024) void fw_parent_kernel(const uint16_t* __restr
                 sv[q] = v; sd[q] = d; sk[q] = -1;
                 if (d >= (unsigned)FW_X) {
                     const uint32_t* lv = inl + (long long)v * np;
-                    const uint32_t thr = (0xFFFFu - d) << 16;
+                    const uint32_t thr = packed ? 0u : (0xFFFFu - d) << 16;  // (packed: every w <= 255 < d)
                     int lo = 0, hi = pos[(long long)v * FW_X + FW_X - 1];
                     while (lo < hi) {
                         const int mid = (lo + hi) >> 1;
@@ -720,14 +731,14 @@ __global__ __launch_bounds__(1024) void fw_parent_kernel(const uint16_t* __restr
                 const uint32_t e[FW_SCAN] = {ea[q].x, ea[q].y, ea[q].z, ea[q].w, eb[q].x, eb[q].y, eb[q].z, eb[q].w};
                 unsigned dd[FW_SCAN];
 #pragma unroll
-                for (int h = 0; h < FW_SCAN; h++) dd[h] = drow[e[h] == FW_END ? 0u : (e[h] & 0xFFFFu)];
+                for (int h = 0; h < FW_SCAN; h++) dd[h] = drow[e[h] == FW_END ? 0u : fw_key_u(e[h], packed)];
                 uint32_t best = FW_END;
                 bool done = false;
 #pragma unroll
                 for (int h = 0; h < FW_SCAN; h++) {
                     if (done) continue;
                     if (e[h] == FW_END) done = true;
-                    else if (dd[h] + (0xFFFFu - (e[h] >> 16)) == sd[q]) { best = e[h]; done = true; }
+                    else if (dd[h] + fw_key_w(e[h], packed) == sd[q]) { best = e[h]; done = true; }
                 }
                 sk[q] += FW_SCAN;
                 if (!done && sk[q] >= np) done = true;  // (np: a multiple of 64; lists end in FW_END)
@@ -757,16 +768,18 @@ struct FWRowsArgs {
     const double* vf;
     const double* self_w;
     const double* self_r;
+    int pk;                  // packed keys: parent << 8 | rix in the key (fw_inlist_kernel)
 };
 __global__ __launch_bounds__(1024) void fw_rows_kernel(FWRowsArgs a, const int* __restrict__ src, int ns,
                                                        const int* __restrict__ tgt, int nt, long long ld,
                                                        double* __restrict__ lat_out, double* __restrict__ rel_out,
                                                        double* __restrict__ row_min, int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    // rel f64[n] | order int[n] | bucket starts int[bound + 2]
+    // rel f64[n] | order u16[n] | bucket starts int[bound + 2] (u16 order, round 6: C5's
+    // 8000 vertices fit two workgroups per CU, 80 KB each, instead of one at 96 KB)
     double* rel = reinterpret_cast<double*>(smem);
-    int* order = reinterpret_cast<int*>(smem + a16(sizeof(double) * a.n));
-    int* bstart = reinterpret_cast<int*>(smem + a16(sizeof(double) * a.n) + a16(sizeof(int) * a.n));
+    uint16_t* order = reinterpret_cast<uint16_t*>(smem + a16(sizeof(double) * a.n));
+    int* bstart = reinterpret_cast<int*>(smem + a16(sizeof(double) * a.n) + a16(sizeof(uint16_t) * a.n));
     __shared__ unsigned long long rmin;
     __shared__ double rtl[256];
     for (int k = threadIdx.x; k < a.nrtab; k += blockDim.x) rtl[k] = a.rtab[k];
@@ -790,7 +803,7 @@ __global__ __launch_bounds__(1024) void fw_rows_kernel(FWRowsArgs a, const int* 
         __syncthreads();
         for (int v = threadIdx.x; v < a.n; v += blockDim.x) {
             const unsigned d = Ds[v];
-            if (d <= (unsigned)a.bound) order[atomicAdd(&bstart[d], 1)] = v;
+            if (d <= (unsigned)a.bound) order[atomicAdd(&bstart[d], 1)] = (uint16_t)v;
         }
         __syncthreads();
         // bstart[d] now holds the end of bucket d; buckets in increasing distance
@@ -805,8 +818,9 @@ __global__ __launch_bounds__(1024) void fw_rows_kernel(FWRowsArgs a, const int* 
                 const int v = order[q];
                 const uint32_t k = Ks[v];
                 if (k == 0xFFFFFFFFu) { raise_err(err, SHD_ROUTE_EUNREACH); rel[v] = NAN; continue; }
-                const int p = (int)(k & 0xFFFFu);
-                rel[v] = rel[p] * (a.nrtab > 0 ? rtl[a.rix[(long long)p * a.n + v]] : a.R[(long long)p * a.n + v]);
+                const int p = (int)fw_key_u(k, a.pk);
+                rel[v] = rel[p] * (a.pk ? rtl[k & 0xFFu]
+                                        : a.nrtab > 0 ? rtl[a.rix[(long long)p * a.n + v]] : a.R[(long long)p * a.n + v]);
             }
             __syncthreads();
         }

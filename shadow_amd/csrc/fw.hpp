@@ -775,8 +775,8 @@ __global__ __launch_bounds__(1024) void fw_rows_kernel(FWRowsArgs a, const int* 
                                                        double* __restrict__ lat_out, double* __restrict__ rel_out,
                                                        double* __restrict__ row_min, int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    // rel f64[n] | order u16[n] | bucket starts int[bound + 2] (u16 order, round 6: C5's
-    // 8000 vertices fit two workgroups per CU, 80 KB each, instead of one at 96 KB)
+    // rel f64[n] | order u16[n] | bucket starts int[bound + 2] (u16 order since round 6:
+    // 40 KB per workgroup on C5's 4000 vertices, so four 512-thread workgroups fit a CU)
     double* rel = reinterpret_cast<double*>(smem);
     uint16_t* order = reinterpret_cast<uint16_t*>(smem + a16(sizeof(double) * a.n));
     int* bstart = reinterpret_cast<int*>(smem + a16(sizeof(double) * a.n) + a16(sizeof(uint16_t) * a.n));

@@ -629,12 +629,16 @@ def bench_c5(args, torch, dist, world, rank, dev, barrier):
     e1.record(stream)
     torch.cuda.synchronize()
     fw_s = e0.elapsed_time(e1) / 1e3 / reps
-    e0.record(stream)
+    # rows: one untimed call first (it allocates the parent-key buffer), then reps timed
     eng.fw_rows_async(d_src, d_tgt, d_lat, d_rel, d_rmin, stream=sh)
+    eng.sync(sh)
+    e0.record(stream)
+    for _ in range(reps):
+        eng.fw_rows_async(d_src, d_tgt, d_lat, d_rel, d_rmin, stream=sh)
     e1.record(stream)
     torch.cuda.synchronize()
     eng.sync(sh)
-    fwr_s = e0.elapsed_time(e1) / 1e3
+    fwr_s = e0.elapsed_time(e1) / 1e3 / reps
     fw_ok = None
     if args.verify and rank == 0:
         from oracle.oracle import OracleGraph, TIE_MINKEY

@@ -86,9 +86,54 @@ __device__ inline void fw_st(uint16_t* p, const uint32_t (&v)[H]) {
 // 256 threads as 16 x 16, each an R x R block (R = T / 16: rows R r.., columns R c..) held
 // as R x R/2 packed column pairs.  Per k: one R-wide read of A's column and of B's row
 // (8- or 16-byte LDS reads) for R^2 relaxations.
+#ifndef FW_PIPE
+#define FW_PIPE 0  // (round 6, FW_PIPE 1 / 2 / 3: C5 table 2.88 / 2.88 / 2.88 ms against 2.80-2.84 off)
+#endif
+// one step k of the product: per row the adds into temporaries before the mins (an op_sel'd
+// add followed directly by its dependent min costs an s_nop)
+template <int R, int H>
+__device__ inline void fw_step(const uint32_t (&av)[H], const uint32_t (&bv)[H], uint32_t (&acc)[R][H]) {
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+        // a row value broadcast to both halves is a shuffle the packed add takes as an
+        // op_sel modifier: no instruction of its own
+        const fw_us2 x = __builtin_bit_cast(fw_us2, av[i >> 1]);
+        const fw_us2 a2 = (i & 1) ? __builtin_shufflevector(x, x, 1, 1) : __builtin_shufflevector(x, x, 0, 0);
+        uint32_t t[H];
+#pragma unroll
+        for (int h = 0; h < H; h++)
+            t[h] = __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(a2, __builtin_bit_cast(fw_us2, bv[h])));
+#pragma unroll
+        for (int h = 0; h < H; h++) acc[i][h] = fw_pkmin(acc[i][h], t[h]);
+    }
+}
 template <int T>
 __device__ inline void fw_tile_product(const uint16_t* At, const uint16_t* Bt, uint32_t (&acc)[T / 16][T / 32], int r, int c) {
     constexpr int R = T / 16, H = R / 2;
+    if constexpr (FW_PIPE > 0) {
+        // (round 6, measured and off) LDS reads FW_PIPE steps ahead in a ring of FW_PIPE + 1
+        // register sets, the loop unrolled in full, and a scheduling barrier between a step's
+        // reads and its compute: the compiler's own schedule of the loop below merges two
+        // steps' reads into one ds_read2 right before an lgkmcnt(0) wait and its use, but the
+        // other three waves of the SIMD already cover that latency: no gain
+        constexpr int P = FW_PIPE, NB = FW_PIPE + 1;
+        uint32_t av[NB][H], bv[NB][H];
+#pragma unroll
+        for (int k = 0; k < P; k++) {
+            fw_ld<H>(At + k * T + R * r, av[k]);
+            fw_ld<H>(Bt + k * T + R * c, bv[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < T; k++) {
+            if (k + P < T) {
+                fw_ld<H>(At + (k + P) * T + R * r, av[(k + P) % NB]);
+                fw_ld<H>(Bt + (k + P) * T + R * c, bv[(k + P) % NB]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            fw_step<R, H>(av[k % NB], bv[k % NB], acc);
+        }
+        return;
+    }
     // software-pipelined LDS reads (step k + 1's in flight while step k computes), and per
     // row the adds into temporaries before the mins (an op_sel'd add followed directly by
     // its dependent min costs an s_nop)

@@ -701,7 +701,9 @@ __global__ __launch_bounds__(1024) void fw_inlist_kernel(const double* __restric
 // have w > D[s][v], never tight (D[s][u] + w > D[s][v]), so they cost a compare, not a
 // result.  In-arc lists hold np entries padded with FW_END, so a scan always ends.
 #ifndef FW_PQ
-#define FW_PQ 4
+// (round 6, with the packed keys: C5 rows 0.640 ms at 2, 0.655 at 4, 0.733 at 6 and 8; two
+// runs each, spread 0.005)
+#define FW_PQ 2
 #endif
 __global__ __launch_bounds__(1024) void fw_parent_kernel(const uint16_t* __restrict__ D, const uint32_t* __restrict__ inl,
                                                          const uint16_t* __restrict__ pos, int n, int np,

@@ -256,3 +256,27 @@ def test_fw_rows_reliability_paths(oracle_mod, monkeypatch, case):
     olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(S, T, oracle_mod.TIE_MINKEY)
     assert np.array_equal(lat, olat)
     assert np.array_equal(rel, orel)
+
+
+@pytest.mark.parametrize("fwpk", ["1", "0"])
+def test_fw_rows_key_forms(oracle_mod, monkeypatch, fwpk):
+    """The two in-list key forms (round 6): packed (every latency <= 255: (255 - w) << 24 |
+    u << 8 | reliability index, the parent search hands the index to fw_rows) and wide
+    ((0xFFFF - w) << 16 | u, the index gathered from the dense matrix; SHD_ROUTE_FWPK=0).
+    A sparse graph with w <= 250 whose distances reach ~870, so most targets start the
+    packed search at the list head (distance past 255) and the rest from the threshold
+    table; lossy arcs, so the reliability index matters."""
+    from shadow_amd import route
+    monkeypatch.setenv("SHD_ROUTE_FWPK", fwpk)
+    g = internet_like(400, 2, seed=4)
+    assert g.latency.max() <= 255
+    eng = route.RouteEngine(g)
+    T = np.arange(g.n, dtype=np.int32)
+    S = T[::3]
+    lat, rel, mn = _fw_rows(eng, S, T)
+    olat, orel, _, _ = oracle_mod.OracleGraph(g).source_rows(S, T, oracle_mod.TIE_MINKEY)
+    assert np.nanmax(olat) > 255 and (olat[np.isfinite(olat)] < 255).any()
+    assert (orel[np.isfinite(orel)] < 1.0).any()
+    assert np.array_equal(lat, olat)
+    assert np.array_equal(rel, orel)
+    assert np.array_equal(mn, olat.min(axis=1))

@@ -2924,7 +2924,9 @@ int fw_prepare(shd_route* c, hipStream_t st) {
                                             (int)lds))) ||
         (rc = hip_check(hipFuncSetAttribute((const void*)fw_inlist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)(4 * sp)))) ||
-        (rc = hip_check(hipFuncSetAttribute((const void*)fw_parent_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (rc = hip_check(hipFuncSetAttribute((const void*)fw_parent_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)(2 * np)))) ||
+        (rc = hip_check(hipFuncSetAttribute((const void*)fw_parent_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)(2 * np)))))
         return rc;
     const size_t cells = (size_t)np * np;
@@ -3079,8 +3081,12 @@ int shd_route_fw_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, co
     // 1024 threads: C5 rows 1.02 -> 0.94 ms; SHD_ROUTE_FWPBLK=512 / 1024 for the A/B)
     int pblk = 256;
     if (const char* e = getenv("SHD_ROUTE_FWPBLK")) pblk = atoi(e) == 1024 ? 1024 : atoi(e) == 512 ? 512 : 256;
-    hipLaunchKernelGGL(fw_parent_kernel, dim3(std::min(ns, 8192)), dim3(pblk), 2 * np, st, c->d_fwD, c->d_fwinl,
-                       c->d_fwpos, c->n, np, d_src, ns, c->d_fwkey, c->fw_pk);
+    if (c->fw_pk)
+        hipLaunchKernelGGL(fw_parent_kernel<true>, dim3(std::min(ns, 8192)), dim3(pblk), 2 * np, st, c->d_fwD, c->d_fwinl,
+                           c->d_fwpos, c->n, np, d_src, ns, c->d_fwkey);
+    else
+        hipLaunchKernelGGL(fw_parent_kernel<false>, dim3(std::min(ns, 8192)), dim3(pblk), 2 * np, st, c->d_fwD, c->d_fwinl,
+                           c->d_fwpos, c->n, np, d_src, ns, c->d_fwkey);
     FWRowsArgs a;
     a.pk = c->fw_pk;
     a.n = c->n; a.np = np; a.bound = c->k32_bound; a.D = c->d_fwD; a.key = c->d_fwkey; a.R = c->d_R;

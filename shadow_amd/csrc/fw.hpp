@@ -705,10 +705,16 @@ __global__ __launch_bounds__(1024) void fw_inlist_kernel(const double* __restric
 // runs each, spread 0.005)
 #define FW_PQ 2
 #endif
+// (round 6) The key form is a template parameter and a trip's 8 arcs are checked without
+// branches: the hits (tight arcs, and the FW_END padding that ends a list) are folded by a
+// min, which is the first hit since a list ascends and its padding comes last.  The SQ
+// counters had the lane-per-target scan VALU-bound (255 M VALU instructions per C5 launch,
+// ~88% issue), not memory-bound: the runtime key form doubled every decode into a select.
+template <bool PK>
 __global__ __launch_bounds__(1024) void fw_parent_kernel(const uint16_t* __restrict__ D, const uint32_t* __restrict__ inl,
                                                          const uint16_t* __restrict__ pos, int n, int np,
                                                          const int* __restrict__ src, int ns,
-                                                         uint32_t* __restrict__ key, int packed) {
+                                                         uint32_t* __restrict__ key) {
     extern __shared__ __attribute__((aligned(16))) uint16_t drow[];
     static_assert(FW_SCAN == 8, "two 16-byte loads per scan trip");
     for (int i = blockIdx.x; i < ns; i += gridDim.x) {
@@ -736,7 +742,7 @@ __global__ __launch_bounds__(1024) void fw_parent_kernel(const uint16_t* __restr
                 sv[q] = v; sd[q] = d; sk[q] = -1;
                 if (d >= (unsigned)FW_X) {
                     const uint32_t* lv = inl + (long long)v * np;
-                    const uint32_t thr = packed ? 0u : (0xFFFFu - d) << 16;  // (packed: every w <= 255 < d)
+                    const uint32_t thr = PK ? 0u : (0xFFFFu - d) << 16;  // (packed: every w <= 255 < d)
                     int lo = 0, hi = pos[(long long)v * FW_X + FW_X - 1];
                     while (lo < hi) {
                         const int mid = (lo + hi) >> 1;
@@ -778,14 +784,15 @@ __global__ __launch_bounds__(1024) void fw_parent_kernel(const uint16_t* __restr
                 const uint32_t e[FW_SCAN] = {ea[q].x, ea[q].y, ea[q].z, ea[q].w, eb[q].x, eb[q].y, eb[q].z, eb[q].w};
                 unsigned dd[FW_SCAN];
 #pragma unroll
-                for (int h = 0; h < FW_SCAN; h++) dd[h] = drow[e[h] == FW_END ? 0u : fw_key_u(e[h], packed)];
+                for (int h = 0; h < FW_SCAN; h++) dd[h] = drow[e[h] == FW_END ? 0u : fw_key_u(e[h], PK)];
                 uint32_t best = FW_END;
                 bool done = false;
 #pragma unroll
                 for (int h = 0; h < FW_SCAN; h++) {
-                    if (done) continue;
-                    if (e[h] == FW_END) done = true;
-                    else if (dd[h] + fw_key_w(e[h], packed) == sd[q]) { best = e[h]; done = true; }
+                    const bool end = e[h] == FW_END;
+                    const bool tight = !end && dd[h] + fw_key_w(e[h], PK) == sd[q];
+                    best = min(best, tight ? e[h] : FW_END);
+                    done = done || end || tight;
                 }
                 sk[q] += FW_SCAN;
                 if (!done && sk[q] >= np) done = true;  // (np: a multiple of 64; lists end in FW_END)

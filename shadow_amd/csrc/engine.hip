@@ -2927,7 +2927,12 @@ int fw_prepare(shd_route* c, hipStream_t st) {
         (rc = hip_check(hipFuncSetAttribute((const void*)fw_parent_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)(2 * np)))) ||
         (rc = hip_check(hipFuncSetAttribute((const void*)fw_parent_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)(2 * np)))))
+                                            (int)(2 * np)))) ||
+        ((size_t)16 * np <= kLdsBudget &&
+         ((rc = hip_check(hipFuncSetAttribute((const void*)fw_parent8_kernel<true>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(16 * np)))) ||
+          (rc = hip_check(hipFuncSetAttribute((const void*)fw_parent8_kernel<false>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(16 * np)))))))
         return rc;
     const size_t cells = (size_t)np * np;
     uint16_t* D = nullptr;
@@ -3081,7 +3086,19 @@ int shd_route_fw_rows_async(shd_route_t* c, const int32_t* d_src, int32_t ns, co
     // 1024 threads: C5 rows 1.02 -> 0.94 ms; SHD_ROUTE_FWPBLK=512 / 1024 for the A/B)
     int pblk = 256;
     if (const char* e = getenv("SHD_ROUTE_FWPBLK")) pblk = atoi(e) == 1024 ? 1024 : atoi(e) == 512 ? 512 : 256;
-    if (c->fw_pk)
+    // eight sources per workgroup where their interleaved rows fit the LDS (C5 rows 0.62 ->
+    // 0.41 ms at 1024 threads, 0.44 at 512, 0.50 at 256; SHD_ROUTE_FWP8=0: one source per
+    // workgroup, SHD_ROUTE_FWP8BLK=512 / 256 for the A/B)
+    const bool p8 = (size_t)16 * np <= kLdsBudget && !(getenv("SHD_ROUTE_FWP8") && atoi(getenv("SHD_ROUTE_FWP8")) == 0);
+    int p8blk = 1024;
+    if (const char* e = getenv("SHD_ROUTE_FWP8BLK")) p8blk = atoi(e) == 512 ? 512 : atoi(e) == 256 ? 256 : 1024;
+    if (p8 && c->fw_pk)
+        hipLaunchKernelGGL(fw_parent8_kernel<true>, dim3(std::min((ns + 7) / 8, 2048)), dim3(p8blk), 16 * np, st, c->d_fwD,
+                           c->d_fwinl, c->d_fwpos, c->n, np, d_src, ns, c->d_fwkey);
+    else if (p8)
+        hipLaunchKernelGGL(fw_parent8_kernel<false>, dim3(std::min((ns + 7) / 8, 2048)), dim3(p8blk), 16 * np, st, c->d_fwD,
+                           c->d_fwinl, c->d_fwpos, c->n, np, d_src, ns, c->d_fwkey);
+    else if (c->fw_pk)
         hipLaunchKernelGGL(fw_parent_kernel<true>, dim3(std::min(ns, 8192)), dim3(pblk), 2 * np, st, c->d_fwD, c->d_fwinl,
                            c->d_fwpos, c->n, np, d_src, ns, c->d_fwkey);
     else

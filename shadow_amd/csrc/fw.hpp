@@ -805,6 +805,105 @@ __global__ __launch_bounds__(1024) void fw_parent_kernel(const uint16_t* __restr
     }
 }
 
+// parents for 8 sources at once (round 6): D[s][.] of 8 sources interleaved in LDS as u16 x 8
+// per vertex, so one 16-byte LDS read gives D[s_b][u] for all 8 and one pass over v's in-list
+// serves the 8 scans: the arc loads (one cache line per lane and 8 arcs, the bound of the
+// per-source kernel) are shared by 8 sources, and the 8 tightness tests are 4 packed adds and
+// compares.  A lane scans from the start of the largest distance among its 8 (pos table:
+// the earliest start) until every source has its first tight arc (or the list's padding):
+// an arc before a source's own start is never tight for it (w > d), so the union scan finds
+// the same first hit per source.  Needs 16 np bytes of LDS.  (C5: fw_parent 0.48 -> ~0.27 ms.)
+template <bool PK>
+__global__ __launch_bounds__(1024) void fw_parent8_kernel(const uint16_t* __restrict__ D, const uint32_t* __restrict__ inl,
+                                                          const uint16_t* __restrict__ pos, int n, int np,
+                                                          const int* __restrict__ src, int ns,
+                                                          uint32_t* __restrict__ key) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t dl[];  // [np][8]
+    for (int i0 = blockIdx.x * 8; i0 < ns; i0 += gridDim.x * 8) {
+        int sb[8];
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const int i = i0 + b;
+            int s = i < ns ? src[i] : -1;
+            sb[b] = s >= 0 && s < n ? s : -1;  // (fw_rows raises the error for a bad source)
+        }
+        __syncthreads();  // the previous batch is done with dl
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const uint16_t* Ds = sb[b] >= 0 ? D + (long long)sb[b] * np : nullptr;
+            for (int u = threadIdx.x; u < np; u += blockDim.x) dl[8 * u + b] = Ds ? Ds[u] : (uint16_t)0xFFFFu;
+        }
+        __syncthreads();
+        for (int v = threadIdx.x; v < n; v += blockDim.x) {
+            const uint4 dq = *reinterpret_cast<const uint4*>(dl + 8 * v);
+            const uint32_t dw[4] = {dq.x, dq.y, dq.z, dq.w};
+            unsigned pend = 0u;
+            int dmax = -1;
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+                const int db = (int)((dw[b >> 1] >> (16 * (b & 1))) & 0xFFFFu);
+                if (sb[b] >= 0 && v != sb[b] && db != 0xFFFF) { pend |= 1u << b; dmax = max(dmax, db); }
+            }
+            uint32_t best[8];
+#pragma unroll
+            for (int b = 0; b < 8; b++) best[b] = FW_END;
+            if (pend) {
+                const uint32_t* lv = inl + (long long)v * np;
+                int lo = 0;
+                if (dmax < FW_X) lo = pos[(long long)v * FW_X + dmax];
+                else if (!PK) {  // (packed: every w <= 255 < dmax, the whole list)
+                    const uint32_t thr = (0xFFFFu - (uint32_t)dmax) << 16;
+                    int hi = pos[(long long)v * FW_X + FW_X - 1];
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (lv[mid] < thr) lo = mid + 1; else hi = mid;
+                    }
+                }
+                int a = lo & ~7;
+                uint4 ea = *reinterpret_cast<const uint4*>(lv + a), eb = *reinterpret_cast<const uint4*>(lv + a + 4);
+                while (pend) {
+                    const uint32_t e[8] = {ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, eb.z, eb.w};
+                    const int an = a + 8;
+                    if (an < np) {  // the next trip's arcs in flight during this one's checks
+                        ea = *reinterpret_cast<const uint4*>(lv + an);
+                        eb = *reinterpret_cast<const uint4*>(lv + an + 4);
+                    }
+#pragma unroll
+                    for (int h = 0; h < 8; h++) {
+                        const uint32_t x = e[h];
+                        if (x == FW_END) pend = 0u;  // (the padding follows every arc)
+                        if (!pend) continue;
+                        const uint32_t u = fw_key_u(x, PK), w = fw_key_w(x, PK);
+                        const fw_us2 w2 = {(unsigned short)w, (unsigned short)w};
+                        const uint4 uq = *reinterpret_cast<const uint4*>(dl + 8 * u);
+                        const uint32_t uw[4] = {uq.x, uq.y, uq.z, uq.w};
+                        uint32_t y = 0u;
+#pragma unroll
+                        for (int k = 0; k < 4; k++) {
+                            // halves of z are 0 exactly where D[s][u] + w == D[s][v] (an
+                            // unreachable u saturates at 0xFFFF, never a reached distance)
+                            const uint32_t z = __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(
+                                                   __builtin_bit_cast(fw_us2, uw[k]), w2)) ^ dw[k];
+                            const fw_us2 zm = __builtin_bit_cast(fw_us2, z) - fw_us2{1, 1};
+                            const uint32_t t = __builtin_bit_cast(uint32_t, zm) & ~z & 0x80008000u;  // bit 15 / 31: half == 0
+                            y |= t >> (15 - 2 * k);
+                        }
+                        const unsigned hit = ((y | (y >> 15)) & 0xFFu) & pend;
+#pragma unroll
+                        for (int b = 0; b < 8; b++) best[b] = ((hit >> b) & 1u) ? x : best[b];
+                        pend &= ~hit;
+                    }
+                    a = an;
+                    if (a >= np) pend = 0u;  // (unreached: every list ends in FW_END)
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < 8; b++)
+                if (sb[b] >= 0) key[(long long)(i0 + b) * np + v] = best[b];
+        }
+    }
+}
+
 // rows: per source (one workgroup), rel down the parent tree in distance order (LDS
 // buckets by distance), then the lat / rel rows for the targets; the self entry is the
 // batch self-loop (lat = w_ss, rel = (1*f_s)*r_ss) as in every SOURCE row

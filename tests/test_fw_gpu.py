@@ -258,16 +258,19 @@ def test_fw_rows_reliability_paths(oracle_mod, monkeypatch, case):
     assert np.array_equal(rel, orel)
 
 
+@pytest.mark.parametrize("fwp8", ["1", "0"])
 @pytest.mark.parametrize("fwpk", ["1", "0"])
-def test_fw_rows_key_forms(oracle_mod, monkeypatch, fwpk):
+def test_fw_rows_key_forms(oracle_mod, monkeypatch, fwpk, fwp8):
     """The two in-list key forms (round 6): packed (every latency <= 255: (255 - w) << 24 |
     u << 8 | reliability index, the parent search hands the index to fw_rows) and wide
     ((0xFFFF - w) << 16 | u, the index gathered from the dense matrix; SHD_ROUTE_FWPK=0).
     A sparse graph with w <= 250 whose distances reach ~870, so most targets start the
     packed search at the list head (distance past 255) and the rest from the threshold
-    table; lossy arcs, so the reliability index matters."""
+    table; lossy arcs, so the reliability index matters.  Both parent searches: eight
+    sources per workgroup (fw_parent8_kernel) and one (fw_parent_kernel, SHD_ROUTE_FWP8=0)."""
     from shadow_amd import route
     monkeypatch.setenv("SHD_ROUTE_FWPK", fwpk)
+    monkeypatch.setenv("SHD_ROUTE_FWP8", fwp8)
     g = internet_like(400, 2, seed=4)
     assert g.latency.max() <= 255
     eng = route.RouteEngine(g)
